@@ -1,0 +1,824 @@
+// gi_oracle.cpp — TEST INFRASTRUCTURE ONLY: CPU restatement of the reference per-pixel radiance
+// loop (preon7/2019global) and of the build-defined Mode X integrator.  Own code; it
+// restates glm 0.9.8.2's operation order explicitly instead of including glm.  Compiled with
+// -ffp-contract=off (no FMA contraction) so every fp op rounds exactly as the reference's does.
+//
+// Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load this library.
+#include "gi_oracle.h"
+
+#include <cfloat>
+#include <climits>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <sstream>
+#include <string>
+#include <vector>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+namespace {
+
+thread_local std::string g_err;
+
+// ---------------------------------------------------------------------------------------------
+// glm 0.9.8.2 arithmetic, restated (3rd_party/glm/detail/func_geometric.inl:54-96,
+// func_exponential.inl:128-133, type_vec3.inl operators): dot = (x*x'+y*y')+z*z';
+// cross = (y*z'-y'*z, z*x'-z'*x, x*y'-x'*y); normalize(v) = v * (1/sqrt(dot(v,v))).
+// ---------------------------------------------------------------------------------------------
+struct V3 { double x, y, z; };
+inline V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline V3 operator-(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline V3 operator-(V3 a) { return {-a.x, -a.y, -a.z}; }
+inline V3 operator*(V3 a, double s) { return {a.x * s, a.y * s, a.z * s}; }
+inline V3 operator*(double s, V3 a) { return {s * a.x, s * a.y, s * a.z}; }
+inline V3 mul(V3 a, V3 b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
+inline double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+inline V3 cross(V3 x, V3 y) { return {x.y * y.z - y.y * x.z, x.z * y.x - y.z * x.x, x.x * y.y - y.x * x.y}; }
+inline V3 normalize(V3 v) { return v * (1.0 / std::sqrt(dot(v, v))); }
+inline double length(V3 v) { return std::sqrt(dot(v, v)); }
+// pow(a.x,2)+pow(a.y,2)+pow(a.z,2): g++ folds pow(x,2) to x*x (identical at -O0)
+inline double sq3(V3 v) { return v.x * v.x + v.y * v.y + v.z * v.z; }
+inline double smin(double a, double b) { return (b < a) ? b : a; }   // std::min
+inline double smax(double a, double b) { return (a < b) ? b : a; }   // std::max
+inline float sminf(float a, float b) { return (b < a) ? b : a; }
+
+// x86-64 cvttsd2si: NaN / out-of-range -> INT_MIN; the reference's int() casts.
+inline int32_t x86_trunc(double d) {
+    if (!(d > -2147483649.0 && d < 2147483648.0)) return INT32_MIN;
+    return (int32_t)d;
+}
+
+const double REF_PI = 3.1415926535;   // entities.h:16
+
+struct Mat {
+    V3 color{1, 0, 0};
+    V3 shader{0.1, 0.7, 1.0};   // material.h:27
+    double spec_pow = 5.0;      // material.h:29
+};
+
+// ImpTriangle (entities.h:136-306): members initialised in declaration order.
+struct Tri {
+    V3 p1, p2, p3, e1, e2, n, pos;
+    float e1f[3], e2f[3];
+};
+Tri make_tri(V3 p1, V3 p2, V3 p3) {
+    Tri t;
+    t.p1 = p1; t.p2 = p2; t.p3 = p3;
+    t.e1 = p2 - p1;                  // :146
+    t.e2 = p3 - p1;                  // :147
+    t.n = normalize(cross(t.e1, t.e2));   // :148
+    t.pos = 0.5 * (0.5 * (p1 + p2) + p3); // :139
+    t.e1f[0] = (float)t.e1.x; t.e1f[1] = (float)t.e1.y; t.e1f[2] = (float)t.e1.z;
+    t.e2f[0] = (float)t.e2.x; t.e2f[1] = (float)t.e2.y; t.e2f[2] = (float)t.e2.z;
+    return t;
+}
+
+// ImpTriangle::intersect (entities.h:150-249).  The 3x3 solve runs in fp32: glm::mat3 of the
+// dvec3 columns (type_mat3x3.inl:99-109, float casts), transpose, glm's cofactor inverse
+// (func_matrix.inl:272-294), then vec3(right) * A_i (type_mat3x3.inl:437-443).  Only sol.z is used.
+bool tri_intersect(const Tri& t, V3 o, V3 d, V3& P, V3& N) {
+    if (dot(t.n, d) == 0) return false;   // :151
+    // m = transpose(mat3(e1, e2, -dir)): m[c][r]
+    const float m00 = t.e1f[0], m01 = t.e2f[0], m02 = (float)(-d.x);
+    const float m10 = t.e1f[1], m11 = t.e2f[1], m12 = (float)(-d.y);
+    const float m20 = t.e1f[2], m21 = t.e2f[2], m22 = (float)(-d.z);
+    const float det = m00 * (m11 * m22 - m21 * m12) - m10 * (m01 * m22 - m21 * m02) + m20 * (m01 * m12 - m11 * m02);
+    const float ood = 1.0f / det;
+    const float i20 = (m10 * m21 - m20 * m11) * ood;
+    const float i21 = (-(m00 * m21 - m20 * m01)) * ood;
+    const float i22 = (m00 * m11 - m10 * m01) * ood;
+    const V3 right = o - t.pos;   // :156
+    const float vx = (float)right.x, vy = (float)right.y, vz = (float)right.z;
+    const float solz = i20 * vx + i21 * vy + i22 * vz;
+    const V3 point = o + (double)solz * d;   // :166
+    const V3 d1 = normalize(cross(t.p1 - point, t.p2 - point));
+    const V3 d2 = normalize(cross(t.p2 - point, t.p3 - point));
+    const V3 d3 = normalize(cross(t.p3 - point, t.p1 - point));
+    const double eps = 1.0e-3;
+    const V3 nn = dot(d, t.n) < 0 ? t.n : -t.n;
+    if (length(d1) < eps || length(d2) < eps || length(d3) < eps) {   // :201-230 (dead for finite input)
+        P = point; N = nn; return true;
+    }
+    const V3 f1 = d1 - d2, f2 = d2 - d3;
+    const bool cp1 = sq3(f1) < eps, cp2 = sq3(f2) < eps;   // :232-235
+    if (cp1 && cp2) { P = point; N = nn; return true; }
+    return false;
+}
+
+// ImpSphere::intersect (entities.h:53-96): fp32/fp64 mix exactly as written.
+bool sphere_intersect(V3 pos, float radius, V3 o, V3 d, V3& P, V3& N) {
+    const V3 np = pos - o;
+    float a1 = 1, a2 = 1, a3 = 1;
+    if (d.x != 0) { a2 = (float)(d.y / d.x); a3 = (float)(d.z / d.x); }
+    else if (d.y != 0) { a1 = (float)(d.x / d.y); a3 = (float)(d.z / d.y); }
+    else if (d.z != 0) { a2 = (float)(d.y / d.z); a1 = (float)(d.x / d.z); }
+    else return false;
+    const double A1 = a1, A2 = a2, A3 = a3;
+    const float a = (float)(A1 * A1 + A2 * A2 + A3 * A3);
+    const float b = (float)(-2.0 * (np.x * A1 + np.y * A2 + np.z * A3));
+    const double R = radius;
+    const float c = (float)(np.x * np.x + np.y * np.y + np.z * np.z - R * R);
+    const double B = b;
+    const float ac4 = (4.0f * a) * c;
+    const double disc = B * B - (double)ac4;
+    if (disc < 0) return false;
+    const double s = std::sqrt(disc);
+    const float a2f = 2.0f * a;
+    const float v1 = (float)((-(double)b + s) / (double)a2f);   // -b is exact in float
+    const float v2 = (float)((-(double)b - s) / (double)a2f);
+    const float base = sminf(std::fabs(v1), std::fabs(v2));
+    V3 ip{(double)(base * a1), (double)(base * a2), (double)(base * a3)};
+    ip = ip + o;
+    P = ip;
+    N = normalize(ip - pos);
+    return true;
+}
+
+enum Kind { IMP_SPHERE = 1, IMP_TRIANGLE = 2, EXP_QUAD = 3 };
+
+struct Ent {
+    int kind = 0;
+    Mat mat;
+    V3 pos{0, 0, 0};
+    float radius = 0, width = 0, length_ = 0, alpha = 0;
+    Tri tri;
+    std::vector<Tri> tris;   // ExpQuad triangles
+    V3 qv[4];                // ExpQuad vertices
+    V3 bmin, bmax;           // boundingBox() as the reference reports it (A.5, A.13)
+};
+
+// ---- constructors ----------------------------------------------------------------------------
+Ent make_imp_sphere(V3 pos, double radius_arg, V3 color) {
+    Ent e;
+    e.kind = IMP_SPHERE;
+    e.mat.color = color;
+    e.radius = (float)radius_arg;
+    e.pos = pos;
+    // bbox member initialised while pos is still {0,0,0} (entities.h:98-99, A.5); glm::vec3
+    const double r = e.radius;
+    e.bmin = {(double)(float)(0.0 - r), (double)(float)(0.0 - r), (double)(float)(0.0 - r)};
+    e.bmax = {(double)(float)(0.0 + r), (double)(float)(0.0 + r), (double)(float)(0.0 + r)};
+    return e;
+}
+
+void tri_bbox(const Tri& t, V3& mn, V3& mx) {   // entities.h:251-275 (A.13)
+    mn = {smin(smin(t.p1.x, t.p2.x), t.p3.x), smin(smin(t.p1.y, t.p2.y), t.p3.y), smin(smin(t.p1.z, t.p2.z), t.p3.z)};
+    mx = {smax(smax(t.p1.x, t.p2.x), t.p3.x), smax(smax(t.p1.y, t.p2.y), t.p3.y), smax(smax(t.p1.z, t.p2.z), t.p3.z) + 0.01};
+    if (mx.x == mn.x) mx.x += 1e-5;
+    if (mx.y == mn.y) mx.y += 1e-5;
+    if (mx.z == mn.z) mx.z += 1e-5;
+}
+
+Ent make_imp_triangle(V3 p1, V3 p2, V3 p3) {
+    Ent e;
+    e.kind = IMP_TRIANGLE;   // Entity() default material: red (entities.h:21)
+    e.tri = make_tri(p1, p2, p3);
+    e.pos = e.tri.pos;
+    tri_bbox(e.tri, e.bmin, e.bmax);
+    return e;
+}
+
+Ent make_exp_quad(V3 pos, double w_arg, double l_arg, double a_arg, V3 color) {   // entities.h:581-590
+    Ent e;
+    e.kind = EXP_QUAD;
+    e.mat.color = color;
+    e.width = (float)w_arg; e.length_ = (float)l_arg; e.alpha = (float)a_arg;
+    e.pos = pos;
+    const float hw = e.width / 2, hl = e.length_ / 2;
+    const double ca = (double)std::cos(e.alpha), sa = (double)std::sin(e.alpha);   // float overloads
+    e.qv[0] = {(pos.x + hw) * ca, pos.y + hl, pos.z + (pos.x + hw) * sa};
+    e.qv[1] = {(pos.x - hw) * ca, pos.y + hl, pos.z + (pos.x - hw) * sa};
+    e.qv[2] = {(pos.x + hw) * ca, pos.y - hl, pos.z + (pos.x + hw) * sa};
+    e.qv[3] = {(pos.x - hw) * ca, pos.y - hl, pos.z + pos.z + (pos.x - hw) * sa};   // :586 typo
+    e.tris.push_back(make_tri(e.qv[1], e.qv[2], e.qv[0]));
+    e.tris.push_back(make_tri(e.qv[1], e.qv[3], e.qv[2]));
+    // bbox with pos = {0,0,0} (entities.h:623-624, A.5), through glm::vec3
+    e.bmin = {(double)(float)(0.0 - hw), (double)(float)(0.0 - hl), (double)(float)0.0};
+    e.bmax = {(double)(float)(0.0 + hw), (double)(float)(0.0 + hl), (double)(float)(0.0 + (0.0 + hw) * sa)};
+    return e;
+}
+
+// Entity::intersect dispatch (Mode R)
+bool ent_intersect(const Ent& e, V3 o, V3 d, V3& P, V3& N) {
+    switch (e.kind) {
+    case IMP_SPHERE: return sphere_intersect(e.pos, e.radius, o, d, P, N);
+    case IMP_TRIANGLE: return tri_intersect(e.tri, o, d, P, N);
+    case EXP_QUAD: {   // entities.h:596-620: nearest by <= over its triangles (ties -> later)
+        bool flag = false;
+        double md = DBL_MAX;
+        V3 mi{DBL_MAX, DBL_MAX, DBL_MAX}, cn{0, 0, 0};
+        for (const Tri& t : e.tris) {
+            V3 p, n;
+            if (tri_intersect(t, o, d, p, n)) {
+                const double dd = sq3(p - o);
+                if (dd <= md) { mi = p; cn = n; md = dd; }
+                flag = true;
+            }
+        }
+        P = mi; N = cn;
+        return flag;
+    }
+    }
+    return false;
+}
+
+// ---- texture coordinates (entities.h:108-130, 277-303, 630-641) --------------------------
+void tex_imp_sphere(const Ent& e, V3 ip, int32_t& x, int32_t& y) {
+    const double r = e.radius;
+    const double unit_v = 2.0 * REF_PI * r / 320.0;
+    const V3 to = ip - e.pos;
+    const V3 up{0, 0, r};
+    const double cos_vert = dot(to, up) / (r * r);
+    const double ang = std::acos(cos_vert);
+    y = x86_trunc((r * ang) / unit_v);
+    const double small_r = r * std::sin(ang);
+    const V3 lm{0, small_r, 0};
+    const double cos_hori = dot(V3{to.x, to.y, 0}, lm) / (small_r * small_r);
+    const double unit_h = 2.0 * REF_PI * small_r / 320.0;
+    x = x86_trunc(small_r * std::acos(cos_hori) / unit_h);
+}
+
+void tex_imp_triangle(const Tri& t, V3 ip, int32_t& x, int32_t& y) {
+    const V3 p21 = t.p2 - t.p1, p31 = t.p3 - t.p1, p32 = t.p3 - t.p2, i1 = ip - t.p1;
+    const double p21l = std::sqrt(sq3(p21));
+    const double i1l = std::sqrt(sq3(i1));
+    const double theta = std::acos(dot(p21, i1) / (p21l * i1l));
+    const double ixl = i1l * std::sin(theta);
+    const V3 v = 0.5 * (p21 + p31);
+    const double vl = std::sqrt(sq3(v));
+    const V3 h = 0.5 * ((-p32) + (-p31));
+    const double hl = std::sqrt(sq3(h));
+    const double uv = vl / 160.0, uh = hl / 160.0;
+    y = x86_trunc(i1l / uh);
+    x = x86_trunc(ixl / uv);
+}
+
+void tex_exp_quad(const Ent& e, V3 ip, int32_t& x, int32_t& y) {
+    const double uv = (double)e.width / 160.0, uh = (double)e.length_ / 160.0;
+    const V3 rv = e.qv[0] - e.qv[1];
+    const V3 i1 = ip - e.qv[1];
+    const double i1l = std::sqrt(sq3(i1));
+    const double theta = std::acos(dot(i1, rv) / ((double)e.width * i1l));
+    y = x86_trunc(i1l * std::sin(theta) / uh);
+    x = x86_trunc(i1l * std::cos(theta) / uv);
+}
+
+void tex_coord(const Ent& e, V3 ip, int32_t& x, int32_t& y) {
+    switch (e.kind) {
+    case IMP_SPHERE: tex_imp_sphere(e, ip, x, y); return;
+    case IMP_TRIANGLE: tex_imp_triangle(e.tri, ip, x, y); return;
+    case EXP_QUAD: tex_exp_quad(e, ip, x, y); return;
+    }
+    x = y = 0;
+}
+
+// Texture (material.h:65-106): 32x32 int checker; colours truncated to int (A.7).  A negative
+// index is out-of-bounds UB in the reference (A.9); this restatement wraps it into [0,32).
+V3 texel(V3 color, int32_t u, int32_t v) {
+    int i = u % 32, j = v % 32;
+    if (i < 0) i += 32;
+    if (j < 0) j += 32;
+    if ((i <= 16 && j <= 16) || (i > 16 && j > 16)) return {1, 1, 1};
+    return {(double)x86_trunc(color.x), (double)x86_trunc(color.y), (double)x86_trunc(color.z)};
+}
+
+// Material::blinn_phong_texture (material.h:48-62)
+V3 shade_ref(const Mat& m, V3 dir, V3 light, V3 ip, V3 n, int32_t u, int32_t v) {
+    const V3 tc = texel(m.color, u, v);
+    const V3 tdc = tc * 0.5;
+    const V3 la = tc * m.shader.x;
+    const V3 ld = (smax(0.0, dot(n, normalize(light - ip))) * tdc) * m.shader.y;
+    const V3 bis = normalize(normalize(-dir) + normalize(light - ip));
+    const V3 ls = (std::pow(smax(0.0, dot(n, bis)), m.spec_pow) * V3{1, 1, 1}) * m.shader.z;
+    const V3 out = (la + ld) + ls;
+    return {smin(out.x, 1.0), smin(out.y, 1.0), smin(out.z, 1.0)};
+}
+
+// Image::setPixel (image.h:14-16) + QColor range check
+void quantize(const double* c, uint8_t* q) {
+    int32_t r = x86_trunc(255 * c[0]), g = x86_trunc(255 * c[1]), b = x86_trunc(255 * c[2]);
+    if (r < 0 || r > 255 || g < 0 || g > 255 || b < 0 || b > 255) { q[0] = q[1] = q[2] = 0; return; }
+    q[0] = (uint8_t)r; q[1] = (uint8_t)g; q[2] = (uint8_t)b;
+}
+
+// ---- octree (octree.h:12-163, bbox.h:25-39) ------------------------------------------------
+bool bb_intersect(V3 amin, V3 amax, V3 bmin, V3 bmax) {
+    const V3 p1 = 0.5 * (amin + amax), p2 = 0.5 * (bmin + bmax);
+    const V3 d = p1 - p2;
+    const bool xo = std::fabs(d.x) < (0.5 * (amax.x - amin.x) + 0.5 * (bmax.x - bmin.x));
+    const bool yo = std::fabs(d.y) < (0.5 * (amax.y - amin.y) + 0.5 * (bmax.y - bmin.y));
+    const bool zo = std::fabs(d.z) < (0.5 * (amax.z - amin.z) + 0.5 * (bmax.z - bmin.z));
+    return xo && yo && zo;
+}
+inline bool le3(V3 a, V3 b) { return a.x <= b.x && a.y <= b.y && a.z <= b.z; }
+
+struct Node {
+    V3 mn, mx;
+    std::vector<int> ents;
+    int child0 = -1;
+};
+
+struct Octree {
+    std::vector<Node> nodes;
+    const std::vector<Ent>* ents = nullptr;
+
+    void init(V3 mn, V3 mx) { nodes.clear(); nodes.push_back(Node{mn, mx, {}, -1}); }
+
+    void partition(int ni) {   // octree.h:176-211
+        if (nodes[ni].child0 >= 0) return;
+        const V3 mn = nodes[ni].mn, mx = nodes[ni].mx;
+        const V3 mid = (mn + mx) * 0.5;
+        bool all_in = true;
+        for (int e : nodes[ni].ents) {
+            const Ent& E = (*ents)[e];
+            all_in = all_in && le3(E.bmin, mid) && le3(mid, E.bmax);
+        }
+        if (all_in) return;
+        const int c0 = (int)nodes.size();
+        const V3 bx[8][2] = {
+            {mn, mid},
+            {{mn.x, mid.y, mn.z}, {mid.x, mx.y, mid.z}},
+            {{mid.x, mn.y, mn.z}, {mx.x, mid.y, mid.z}},
+            {{mid.x, mid.y, mn.z}, {mx.x, mx.y, mid.z}},
+            {mid, mx},
+            {{mn.x, mid.y, mid.z}, {mid.x, mx.y, mx.z}},
+            {{mid.x, mn.y, mid.z}, {mx.x, mid.y, mx.z}},
+            {{mn.x, mn.y, mid.z}, {mid.x, mid.y, mx.z}},
+        };
+        for (int c = 0; c < 8; ++c) nodes.push_back(Node{bx[c][0], bx[c][1], {}, -1});
+        nodes[ni].child0 = c0;
+    }
+
+    void push_obj(int ni, int e) {   // octree.h:216-230
+        nodes[ni].ents.push_back(e);
+        partition(ni);
+        if (nodes[ni].child0 < 0) return;
+        const Ent& E = (*ents)[e];
+        for (int c = 0; c < 8; ++c) {
+            const int ci = nodes[ni].child0 + c;
+            if (le3(nodes[ci].mn, E.bmin) && le3(E.bmax, nodes[ci].mx)) push_obj(ci, e);
+            else if (bb_intersect(nodes[ci].mn, nodes[ci].mx, E.bmin, E.bmax)) nodes[ci].ents.push_back(e);
+        }
+    }
+
+    void push_back(int e) {   // octree.h:121-144
+        const Ent& E = (*ents)[e];
+        if (!bb_intersect(nodes[0].mn, nodes[0].mx, E.bmin, E.bmax)) return;   // A.14
+        push_obj(0, e);
+    }
+};
+
+// ExpBox node test (entities.h:379-440): OR over 6 ExpRectangle faces, each t1=(p1,p2,p3) or
+// t2=(p1,p2,p4) with p4 = -p3 (A.4).  Only the bool is used by Octree::Node::intersect.
+bool rect_hit(V3 p1, V3 p2, V3 p3, V3 o, V3 d) {
+    V3 P, N;
+    if (tri_intersect(make_tri(p1, p2, p3), o, d, P, N)) return true;
+    return tri_intersect(make_tri(p1, p2, -p3), o, d, P, N);
+}
+bool box_hit(V3 mn, V3 mx, V3 o, V3 d) {
+    const V3 dlb = mn, drb{mx.x, mn.y, mn.z}, dlt{mn.x, mx.y, mn.z}, drt{mx.x, mx.y, mn.z};
+    const V3 ulb{mn.x, mn.y, mx.z}, urb{mx.x, mn.y, mx.z}, ult{mn.x, mx.y, mx.z}, urt = mx;
+    bool hit = false;
+    hit = rect_hit(dlb, urb, ulb, o, d) || hit;
+    hit = rect_hit(dlb, ult, dlt, o, d) || hit;
+    hit = rect_hit(dlb, drt, dlt, o, d) || hit;
+    hit = rect_hit(urt, ulb, ult, o, d) || hit;
+    hit = rect_hit(urt, drb, drt, o, d) || hit;
+    hit = rect_hit(urt, dlt, drt, o, d) || hit;
+    return hit;
+}
+
+void query(const Octree& t, int ni, V3 o, V3 d, std::vector<int>& out, int& ntests) {   // octree.h:233-256
+    const Node& n = t.nodes[ni];
+    if (n.child0 < 0) { out.insert(out.end(), n.ents.begin(), n.ents.end()); return; }
+    for (int c = 0; c < 8; ++c) {
+        const int ci = n.child0 + c;
+        if (t.nodes[ci].ents.empty()) continue;
+        ++ntests;
+        if (box_hit(t.nodes[ci].mn, t.nodes[ci].mx, o, d)) query(t, ci, o, d, out, ntests);
+    }
+}
+
+// ---- scene -----------------------------------------------------------------------------------
+struct Scene {
+    V3 omin{-20, -20, -20}, omax{20, 20, 20};
+    V3 cpos{-10, 0, 0}, clook{1, 0, 0};
+    double focal = 0.1;
+    V3 light{-10, 10, 10};
+    std::vector<Ent> ents;
+    Octree tree;
+};
+
+bool parse(const char* text, Scene& s) {
+    std::istringstream in(text);
+    std::string line;
+    while (std::getline(in, line)) {
+        size_t h = line.find('#');
+        if (h != std::string::npos) line = line.substr(0, h);
+        std::istringstream is(line);
+        std::string kw;
+        if (!(is >> kw)) continue;
+        std::vector<double> v;
+        double x;
+        while (is >> x) v.push_back(x);
+        auto need = [&](size_t n) { return v.size() >= n; };
+        if (kw == "octree" && need(6)) { s.omin = {v[0], v[1], v[2]}; s.omax = {v[3], v[4], v[5]}; }
+        else if (kw == "camera" && need(7)) { s.cpos = {v[0], v[1], v[2]}; s.clook = {v[3], v[4], v[5]}; s.focal = v[6]; }
+        else if (kw == "light" && need(3)) s.light = {v[0], v[1], v[2]};
+        else if (kw == "impsphere" && need(7)) s.ents.push_back(make_imp_sphere({v[0], v[1], v[2]}, v[3], {v[4], v[5], v[6]}));
+        else if (kw == "imptriangle" && need(9)) s.ents.push_back(make_imp_triangle({v[0], v[1], v[2]}, {v[3], v[4], v[5]}, {v[6], v[7], v[8]}));
+        else if (kw == "expquad" && need(9)) s.ents.push_back(make_exp_quad({v[0], v[1], v[2]}, v[3], v[4], v[5], {v[6], v[7], v[8]}));
+        else if (kw == "material" && need(3)) {
+            if (s.ents.empty()) { g_err = "material before entity"; return false; }
+            Mat m;
+            m.color = {v[0], v[1], v[2]};
+            if (v.size() >= 6) m.shader = {v[3], v[4], v[5]};
+            if (v.size() >= 7) m.spec_pow = v[6];
+            s.ents.back().mat = m;
+        } else { g_err = "unsupported scene line: " + line; return false; }
+    }
+    s.tree.ents = &s.ents;
+    s.tree.init(s.omin, s.omax);
+    for (int i = 0; i < (int)s.ents.size(); ++i) s.tree.push_back(i);
+    return true;
+}
+
+struct Cam {
+    V3 pos, up{0, 0, 1}, fwd, left, top_left;
+    double focal, rx = 0.0002, ry = 0.0002;
+};
+Cam make_cam(const Scene& s, int w) {   // camera.h:8-10, raytracer.h:26-30
+    Cam c;
+    c.pos = s.cpos;
+    c.fwd = normalize(s.clook - s.cpos);
+    c.focal = s.focal;
+    c.left = normalize(cross(c.up, c.fwd));
+    c.top_left = (((c.pos + c.focal * c.fwd) + ((c.left * (double)w) * 0.5) * c.rx) + ((c.up * (double)w) * 0.5) * c.ry) - c.pos;
+    return c;
+}
+
+// ---- Mode R pixel (raytracer.h:41-84) -------------------------------------------------------
+void pixel_mode_r(const Scene& s, const Cam& c, int x, int y, double* rgb, int32_t& hit, int32_t& u,
+                  int32_t& v, int32_t& ncand, int32_t& nnode) {
+    const V3 dir0 = (c.top_left - (c.left * (double)x) * c.rx) - (c.up * (double)y) * c.ry;
+    const V3 o = c.pos, d = normalize(dir0);   // Ray ctor (ray.h:6)
+    std::vector<int> cand;
+    int nt = 0;
+    query(s.tree, 0, o, d, cand, nt);
+    ncand = (int32_t)cand.size();
+    nnode = nt;
+    int front = -1;
+    V3 ip{DBL_MAX, DBL_MAX, DBL_MAX}, nrm{0, 0, 0};
+    for (int e : cand) {   // last hitting candidate wins (A.1)
+        V3 P, N;
+        if (ent_intersect(s.ents[e], o, d, P, N)) {
+            const double d2 = sq3(P - o);
+            if (d2 < DBL_MAX) { ip = P; nrm = N; front = e; }
+        }
+    }
+    hit = front;
+    if (front < 0) { rgb[0] = rgb[1] = rgb[2] = 0; u = v = 0; return; }
+    tex_coord(s.ents[front], ip, u, v);
+    const V3 col = shade_ref(s.ents[front].mat, d, s.light, ip, nrm, u, v);
+    rgb[0] = col.x; rgb[1] = col.y; rgb[2] = col.z;
+}
+
+// ============================================================================================
+// Mode X — build-defined integrator (DESIGN.md "Mode X").  Only +,-,*,/,sqrt and comparisons
+// (all correctly rounded, no contraction), so the GPU kernel can match it bit for bit.
+// ============================================================================================
+const double MX_TMIN = 1e-7;
+const double MX_PI = 0x1.921fb54442d18p+1, MX_PIO2 = 0x1.921fb54442d18p+0;
+const double ASIN_C[30] = {
+    0x1.0000000000000p+0, 0x1.5555555555555p-3, 0x1.3333333333333p-4, 0x1.6db6db6db6db7p-5,
+    0x1.f1c71c71c71c7p-6, 0x1.6e8ba2e8ba2e9p-6, 0x1.1c4ec4ec4ec4fp-6, 0x1.c99999999999ap-7,
+    0x1.7a87878787878p-7, 0x1.3fde50d79435ep-7, 0x1.12ef3cf3cf3cfp-7, 0x1.df3bd37a6f4dfp-8,
+    0x1.a6863d70a3d71p-8, 0x1.782dda12f684cp-8, 0x1.51ba308d3dcb1p-8, 0x1.31683bdef7bdfp-8,
+    0x1.15ee9d45d1746p-8, 0x1.fcaf8fb6db6dbp-9, 0x1.d3d2a8e0dd67dp-9, 0x1.b026f57b13b14p-9,
+    0x1.90cb77f60c7cep-9, 0x1.750de64d7d05fp-9, 0x1.5c5f56efaaaabp-9, 0x1.464c0950f7d47p-9,
+    0x1.3275586c5f2f0p-9, 0x1.208d3570ae5a6p-9, 0x1.1052bc5fa960ap-9, 0x1.018f963c229bfp-9,
+    0x1.e82be60d9127ep-10, 0x1.cf7dea5b6e830p-10};
+
+double mx_asin_small(double y) {   // |y| <= 0.5: Taylor series, Horner, 30 terms
+    const double z = y * y;
+    double p = ASIN_C[29];
+    for (int k = 28; k >= 0; --k) p = p * z + ASIN_C[k];
+    return y * p;
+}
+double mx_acos(double x) {
+    if (!(x >= -1.0 && x <= 1.0)) return NAN;
+    if (x >= -0.5 && x <= 0.5) return MX_PIO2 - mx_asin_small(x);
+    if (x > 0.5) return 2.0 * mx_asin_small(std::sqrt((1.0 - x) * 0.5));
+    return MX_PI - 2.0 * mx_asin_small(std::sqrt((1.0 + x) * 0.5));
+}
+double mx_sin_acos(double c) { return std::sqrt(1.0 - c * c); }            // NaN for |c| > 1
+double mx_cos_acos(double c) { return (c >= -1.0 && c <= 1.0) ? c : NAN; }
+
+double mx_powi(double x, int p) {
+    double r = 1.0, b = x;
+    while (p) {
+        if (p & 1) r = r * b;
+        b = b * b;
+        p >>= 1;
+    }
+    return r;
+}
+
+inline uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+inline double mx_u01(uint64_t seed, uint64_t pixel, uint32_t sample, uint32_t bounce, uint32_t dim) {
+    uint64_t k = mix64(seed + 0x9E3779B97F4A7C15ULL * (pixel + 1));
+    k = mix64(k ^ (((uint64_t)sample << 32) | ((uint64_t)(bounce & 0xFFFF) << 16) | (uint64_t)(dim & 0xFFFF)));
+    return (double)(k >> 11) * 0x1.0p-53;
+}
+
+struct Prim {
+    int kind;     // 0 = triangle, 1 = sphere
+    int ent;
+    V3 v0, e1, e2, n;   // triangle: p1, p2-p1, p3-p1, normalize(cross(e1,e2))
+    V3 c;               // sphere centre
+    double r;           // sphere radius (the float radius widened)
+};
+
+void build_prims(const Scene& s, std::vector<Prim>& prims) {
+    for (int i = 0; i < (int)s.ents.size(); ++i) {
+        const Ent& e = s.ents[i];
+        auto add_tri = [&](const Tri& t) {
+            Prim p{};
+            p.kind = 0; p.ent = i; p.v0 = t.p1; p.e1 = t.e1; p.e2 = t.e2; p.n = t.n;
+            prims.push_back(p);
+        };
+        if (e.kind == IMP_SPHERE) {
+            Prim p{};
+            p.kind = 1; p.ent = i; p.c = e.pos; p.r = (double)e.radius;
+            prims.push_back(p);
+        } else if (e.kind == IMP_TRIANGLE) add_tri(e.tri);
+        else for (const Tri& t : e.tris) add_tri(t);
+    }
+}
+
+// Möller–Trumbore, two-sided; returns t or +inf
+double mx_tri_t(const Prim& p, V3 o, V3 d, double tmin) {
+    const V3 pv = cross(d, p.e2);
+    const double det = dot(p.e1, pv);
+    if (det == 0.0) return INFINITY;
+    const double inv = 1.0 / det;
+    const V3 tv = o - p.v0;
+    const double u = dot(tv, pv) * inv;
+    if (u < 0.0 || u > 1.0) return INFINITY;
+    const V3 qv = cross(tv, p.e1);
+    const double v = dot(d, qv) * inv;
+    if (v < 0.0 || u + v > 1.0) return INFINITY;
+    const double t = dot(p.e2, qv) * inv;
+    return (t > tmin) ? t : INFINITY;
+}
+double mx_sph_t(const Prim& p, V3 o, V3 d, double tmin) {
+    const V3 oc = o - p.c;
+    const double b = dot(oc, d);
+    const double c2 = dot(oc, oc) - p.r * p.r;
+    const double disc = b * b - c2;
+    if (disc < 0.0) return INFINITY;
+    const double sq = std::sqrt(disc);
+    double t = -b - sq;
+    if (t > tmin) return t;
+    t = -b + sq;
+    return (t > tmin) ? t : INFINITY;
+}
+inline double mx_prim_t(const Prim& p, V3 o, V3 d, double tmin) {
+    return p.kind == 0 ? mx_tri_t(p, o, d, tmin) : mx_sph_t(p, o, d, tmin);
+}
+
+int mx_closest(const std::vector<Prim>& prims, V3 o, V3 d, double& tbest) {
+    int best = -1;
+    tbest = INFINITY;
+    for (int i = 0; i < (int)prims.size(); ++i) {
+        const double t = mx_prim_t(prims[i], o, d, MX_TMIN);
+        if (t < tbest) { tbest = t; best = i; }   // strict: ties keep the lower index
+    }
+    return best;
+}
+bool mx_occluded(const std::vector<Prim>& prims, V3 o, V3 d, double tmax) {
+    for (const Prim& p : prims) {
+        const double t = mx_prim_t(p, o, d, MX_TMIN);
+        if (t < tmax) return true;
+    }
+    return false;
+}
+
+void mx_texcoord(const Ent& e, V3 ip, int32_t& x, int32_t& y) {
+    if (e.kind == IMP_SPHERE) {
+        const double r = e.radius;
+        const double unit_v = 2.0 * REF_PI * r / 320.0;
+        const V3 to = ip - e.pos;
+        const double cv = dot(to, V3{0, 0, r}) / (r * r);
+        y = x86_trunc((r * mx_acos(cv)) / unit_v);
+        const double small_r = r * mx_sin_acos(cv);
+        const double ch = dot(V3{to.x, to.y, 0}, V3{0, small_r, 0}) / (small_r * small_r);
+        const double unit_h = 2.0 * REF_PI * small_r / 320.0;
+        x = x86_trunc(small_r * mx_acos(ch) / unit_h);
+    } else if (e.kind == IMP_TRIANGLE) {
+        const Tri& t = e.tri;
+        const V3 p21 = t.p2 - t.p1, p31 = t.p3 - t.p1, p32 = t.p3 - t.p2, i1 = ip - t.p1;
+        const double p21l = std::sqrt(sq3(p21)), i1l = std::sqrt(sq3(i1));
+        const double c = dot(p21, i1) / (p21l * i1l);
+        const double ixl = i1l * mx_sin_acos(c);
+        const double vl = std::sqrt(sq3(0.5 * (p21 + p31)));
+        const double hl = std::sqrt(sq3(0.5 * ((-p32) + (-p31))));
+        y = x86_trunc(i1l / (hl / 160.0));
+        x = x86_trunc(ixl / (vl / 160.0));
+    } else if (e.kind == EXP_QUAD) {
+        const double uv = (double)e.width / 160.0, uh = (double)e.length_ / 160.0;
+        const V3 rv = e.qv[0] - e.qv[1], i1 = ip - e.qv[1];
+        const double i1l = std::sqrt(sq3(i1));
+        const double c = dot(i1, rv) / ((double)e.width * i1l);
+        y = x86_trunc(i1l * mx_sin_acos(c) / uh);
+        x = x86_trunc(i1l * mx_cos_acos(c) / uv);
+    } else x = y = 0;
+}
+
+void pixel_mode_x(const Scene& s, const std::vector<Prim>& prims, const Cam& c, int w, int x, int y,
+                  int spp, int depth, uint64_t seed, double* rgb, int32_t& hit0, int32_t& u0, int32_t& v0,
+                  int32_t& nrays) {
+    const uint64_t pix = (uint64_t)y * (uint64_t)w + (uint64_t)x;
+    double sum[3] = {0, 0, 0};
+    hit0 = -1; u0 = v0 = 0;
+    long rays = 0;
+    for (int smp = 0; smp < spp; ++smp) {
+        double jx = 0.0, jy = 0.0;
+        if (spp > 1) { jx = mx_u01(seed, pix, smp, 0xFFFF, 0); jy = mx_u01(seed, pix, smp, 0xFFFF, 1); }
+        const V3 dir0 = (c.top_left - (c.left * ((double)x + jx)) * c.rx) - (c.up * ((double)y + jy)) * c.ry;
+        V3 o = c.pos, d = normalize(dir0);
+        V3 L{0, 0, 0}, T{1, 1, 1};
+        for (int b = 0; b < depth; ++b) {
+            double t;
+            const int pi = mx_closest(prims, o, d, t);
+            ++rays;
+            if (pi < 0) break;
+            const Prim& p = prims[pi];
+            const Ent& e = s.ents[p.ent];
+            const V3 P = o + t * d;
+            V3 N = p.kind == 0 ? p.n : normalize(P - p.c);
+            if (!(dot(d, N) < 0)) N = -N;
+            int32_t tu, tv;
+            mx_texcoord(e, P, tu, tv);
+            if (smp == 0 && b == 0) { hit0 = p.ent; u0 = tu; v0 = tv; }
+            const V3 tc = texel(e.mat.color, tu, tv);
+            // local Blinn-Phong with a shadow ray toward the point light
+            const V3 lv = s.light - P;
+            const double ldist = std::sqrt(dot(lv, lv));
+            const V3 Ld = normalize(lv);
+            const bool vis = !mx_occluded(prims, P, Ld, ldist);
+            ++rays;
+            const V3 la = tc * e.mat.shader.x;
+            V3 loc = la;
+            if (vis) {
+                const V3 ld = (smax(0.0, dot(N, Ld)) * (tc * 0.5)) * e.mat.shader.y;
+                const V3 bis = normalize(normalize(-d) + Ld);
+                const double sp = mx_powi(smax(0.0, dot(N, bis)), (int)e.mat.spec_pow);
+                const V3 ls = V3{sp, sp, sp} * e.mat.shader.z;
+                loc = (la + ld) + ls;
+            }
+            loc = {smin(loc.x, 1.0), smin(loc.y, 1.0), smin(loc.z, 1.0)};
+            L = L + mul(T, loc);
+            if (b == depth - 1) break;
+            T = mul(T, tc * 0.5);
+            if (T.x == 0.0 && T.y == 0.0 && T.z == 0.0) break;
+            // cosine-weighted direction: disk rejection sampling (<= 16 tries) + Malley's projection
+            double sx = 0, sy = 0, r2 = 0;
+            for (int k = 0; k < 16; ++k) {
+                const double ax = 2.0 * mx_u01(seed, pix, smp, b, 2 + 2 * k) - 1.0;
+                const double ay = 2.0 * mx_u01(seed, pix, smp, b, 3 + 2 * k) - 1.0;
+                const double q = ax * ax + ay * ay;
+                if (q < 1.0) { sx = ax; sy = ay; r2 = q; break; }
+            }
+            const double sz = std::sqrt(1.0 - r2);
+            const double sg = N.z >= 0.0 ? 1.0 : -1.0;   // Duff et al. 2017 orthonormal basis
+            const double aa = -1.0 / (sg + N.z);
+            const double bb = N.x * N.y * aa;
+            const V3 t1{1.0 + sg * N.x * N.x * aa, sg * bb, -sg * N.x};
+            const V3 t2{bb, sg + N.y * N.y * aa, -N.y};
+            d = normalize((t1 * sx + t2 * sy) + N * sz);
+            o = P;
+        }
+        sum[0] = sum[0] + L.x; sum[1] = sum[1] + L.y; sum[2] = sum[2] + L.z;
+    }
+    for (int k = 0; k < 3; ++k) rgb[k] = smin(sum[k] / (double)spp, 1.0);
+    nrays = (int32_t)rays;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* gio_last_error(void) { return g_err.c_str(); }
+
+int gio_render(const char* scn, int w, int h, int mode, int spp, int depth, uint64_t seed, int x0, int y0,
+               int x1, int y1, int threads, double* rgb, int32_t* hit, int32_t* uv, int32_t* ncand,
+               int32_t* nnode, uint8_t* q) {
+    Scene s;
+    if (!parse(scn, s)) return -1;
+    if (w <= 0 || h <= 0 || x0 < 0 || y0 < 0 || x1 > w || y1 > h || x0 > x1 || y0 > y1) { g_err = "bad window"; return -2; }
+    if (mode == 1) {
+        if (spp < 1 || depth < 1) { g_err = "mode X needs spp >= 1 and depth >= 1"; return -3; }
+        for (const Ent& e : s.ents)
+            if (!(e.mat.spec_pow >= 0 && e.mat.spec_pow <= 64 && e.mat.spec_pow == (double)(int)e.mat.spec_pow)) {
+                g_err = "mode X needs integer specular_power in [0,64]"; return -3;
+            }
+    }
+    std::vector<Prim> prims;
+    if (mode == 1) build_prims(s, prims);
+    const Cam c = make_cam(s, w);
+    const int ww = x1 - x0;
+    const long npx = (long)ww * (y1 - y0);
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#endif
+#pragma omp parallel for schedule(dynamic, 16)
+    for (long i = 0; i < npx; ++i) {
+        const int x = x0 + (int)(i % ww), y = y0 + (int)(i / ww);
+        double col[3];
+        int32_t hh, u, v, nc = 0, nn = 0;
+        if (mode == 0) pixel_mode_r(s, c, x, y, col, hh, u, v, nc, nn);
+        else { pixel_mode_x(s, prims, c, w, x, y, spp, depth, seed, col, hh, u, v, nc); nn = 0; }
+        if (rgb) { rgb[3 * i] = col[0]; rgb[3 * i + 1] = col[1]; rgb[3 * i + 2] = col[2]; }
+        if (hit) hit[i] = hh;
+        if (uv) { uv[2 * i] = u; uv[2 * i + 1] = v; }
+        if (ncand) ncand[i] = nc;
+        if (nnode) nnode[i] = nn;
+        if (q) quantize(col, q + 3 * i);
+    }
+    return 0;
+}
+
+long gio_tree(const char* scn, char* buf, long cap) {
+    Scene s;
+    if (!parse(scn, s)) return -1;
+    std::string out;
+    char tmp[512];
+    for (size_t i = 0; i < s.ents.size(); ++i) {
+        const Ent& e = s.ents[i];
+        snprintf(tmp, sizeof tmp, "bbox %zu %.17g %.17g %.17g %.17g %.17g %.17g\n", i, e.bmin.x, e.bmin.y, e.bmin.z,
+                 e.bmax.x, e.bmax.y, e.bmax.z);
+        out += tmp;
+    }
+    struct R {
+        static void dump(const Octree& t, int ni, int depth, int slot, std::string& out) {
+            const Node& n = t.nodes[ni];
+            char b[512];
+            snprintf(b, sizeof b, "node %d %d %d %.17g %.17g %.17g %.17g %.17g %.17g %zu", depth, slot, n.child0 < 0 ? 1 : 0,
+                     n.mn.x, n.mn.y, n.mn.z, n.mx.x, n.mx.y, n.mx.z, n.ents.size());
+            out += b;
+            for (int e : n.ents) { snprintf(b, sizeof b, " %d", e); out += b; }
+            out += "\n";
+            if (n.child0 >= 0)
+                for (int c = 0; c < 8; ++c) dump(t, n.child0 + c, depth + 1, c, out);
+        }
+    };
+    R::dump(s.tree, 0, 0, -1, out);
+    if (buf && cap > 0) {
+        long n = (long)out.size() < cap - 1 ? (long)out.size() : cap - 1;
+        memcpy(buf, out.data(), (size_t)n);
+        buf[n] = 0;
+    }
+    return (long)out.size();
+}
+
+int gio_rays(const char* scn, int n, const double* rays, int32_t* out_hit, double* out_pn, int32_t* out_uv) {
+    Scene s;
+    if (!parse(scn, s)) return -1;
+    const size_t E = s.ents.size();
+    for (int i = 0; i < n; ++i) {
+        const V3 o{rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]};
+        const V3 d = normalize(V3{rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]});
+        for (size_t k = 0; k < E; ++k) {
+            V3 P{0, 0, 0}, N{0, 0, 0};
+            const size_t j = (size_t)i * E + k;
+            const bool h = ent_intersect(s.ents[k], o, d, P, N);
+            int32_t u = 0, v = 0;
+            if (h) tex_coord(s.ents[k], P, u, v);
+            else if (s.ents[k].kind == EXP_QUAD) { /* outputs are overwritten on miss too (:616-617) */ }
+            else { P = {0, 0, 0}; N = {0, 0, 0}; }
+            out_hit[j] = h ? 1 : 0;
+            double* pn = out_pn + 6 * j;
+            pn[0] = P.x; pn[1] = P.y; pn[2] = P.z; pn[3] = N.x; pn[4] = N.y; pn[5] = N.z;
+            out_uv[2 * j] = u; out_uv[2 * j + 1] = v;
+        }
+    }
+    return 0;
+}
+
+int gio_boxes(int n, const double* recs, int32_t* out) {
+    for (int i = 0; i < n; ++i) {
+        const double* q = recs + 12 * (size_t)i;
+        out[i] = box_hit({q[0], q[1], q[2]}, {q[3], q[4], q[5]}, {q[6], q[7], q[8]},
+                         normalize(V3{q[9], q[10], q[11]})) ? 1 : 0;
+    }
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,176 @@
+"""Helpers shared by the tests: load the CPU oracle (oracle/_build/libgi_oracle.so), run the
+compiled reference harness (oracle/_ref/ref_harness, only where /root/reference was present at
+build time), and read/write golden fixtures.  Test infrastructure only."""
+from __future__ import annotations
+
+import ctypes
+import importlib
+import os
+import struct
+import subprocess
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "_build", "libgi_oracle.so")
+REF_HARNESS = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+REF_RUN = os.path.join(ROOT, "oracle", "_ref", "ref_run")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pkg():
+    """The product package (its directory name starts with a digit, so import by string)."""
+    return importlib.import_module("2019global_amd")
+
+
+def scenes():
+    return importlib.import_module("2019global_amd.scenes")
+
+
+_oracle = None
+
+
+def oracle():
+    global _oracle
+    if _oracle is None:
+        if not os.path.exists(ORACLE_SO):
+            subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "oracle"], check=True,
+                           stdout=subprocess.DEVNULL)
+        lib = ctypes.CDLL(ORACLE_SO)
+        i32p = ctypes.POINTER(ctypes.c_int32)
+        f64p = ctypes.POINTER(ctypes.c_double)
+        lib.gio_render.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_int, ctypes.c_int, f64p, i32p, i32p, i32p, i32p,
+                                   ctypes.POINTER(ctypes.c_uint8)]
+        lib.gio_tree.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_long]
+        lib.gio_tree.restype = ctypes.c_long
+        lib.gio_rays.argtypes = [ctypes.c_char_p, ctypes.c_int, f64p, i32p, f64p, i32p]
+        lib.gio_boxes.argtypes = [ctypes.c_int, f64p, i32p]
+        lib.gio_last_error.restype = ctypes.c_char_p
+        _oracle = lib
+    return _oracle
+
+
+def _p(a, t):
+    return a.ctypes.data_as(ctypes.POINTER(t))
+
+
+def oracle_render(scn: str, w: int, h: int, mode: int = 0, spp: int = 1, depth: int = 1, seed: int = 0,
+                  window=None, threads: int = 0) -> dict:
+    x0, y0, x1, y1 = window if window is not None else (0, 0, w, h)
+    n = (x1 - x0) * (y1 - y0)
+    out = dict(rgb=np.zeros((n, 3)), hit=np.zeros(n, np.int32), uv=np.zeros((n, 2), np.int32),
+               ncand=np.zeros(n, np.int32), nnode=np.zeros(n, np.int32), q=np.zeros((n, 3), np.uint8))
+    lib = oracle()
+    rc = lib.gio_render(scn.encode(), w, h, mode, spp, depth, seed, x0, y0, x1, y1, threads,
+                        _p(out["rgb"], ctypes.c_double), _p(out["hit"], ctypes.c_int32),
+                        _p(out["uv"], ctypes.c_int32), _p(out["ncand"], ctypes.c_int32),
+                        _p(out["nnode"], ctypes.c_int32), _p(out["q"], ctypes.c_uint8))
+    if rc != 0:
+        raise RuntimeError(f"gio_render failed ({rc}): {lib.gio_last_error().decode()}")
+    return out
+
+
+def oracle_tree(scn: str) -> str:
+    lib = oracle()
+    n = lib.gio_tree(scn.encode(), None, 0)
+    buf = ctypes.create_string_buffer(n + 1)
+    lib.gio_tree(scn.encode(), buf, n + 1)
+    return buf.value.decode()
+
+
+def oracle_rays(scn: str, rays: np.ndarray, n_ent: int) -> dict:
+    rays = np.ascontiguousarray(rays, np.float64)
+    n = rays.shape[0]
+    hit = np.zeros((n, n_ent), np.int32)
+    pn = np.zeros((n, n_ent, 6))
+    uv = np.zeros((n, n_ent, 2), np.int32)
+    rc = oracle().gio_rays(scn.encode(), n, _p(rays, ctypes.c_double), _p(hit, ctypes.c_int32),
+                           _p(pn, ctypes.c_double), _p(uv, ctypes.c_int32))
+    assert rc == 0
+    return dict(hit=hit, pn=pn, uv=uv)
+
+
+def oracle_boxes(recs: np.ndarray) -> np.ndarray:
+    recs = np.ascontiguousarray(recs, np.float64)
+    out = np.zeros(recs.shape[0], np.int32)
+    assert oracle().gio_boxes(recs.shape[0], _p(recs, ctypes.c_double), _p(out, ctypes.c_int32)) == 0
+    return out
+
+
+# ---- compiled reference (oracle/_ref) -------------------------------------------------------
+
+def have_ref() -> bool:
+    return os.path.exists(REF_HARNESS)
+
+
+def ref_render(scn: str, w: int, h: int, window=None, stride: int = 1) -> dict:
+    with tempfile.TemporaryDirectory() as td:
+        sp = os.path.join(td, "s.scn")
+        op = os.path.join(td, "o.bin")
+        open(sp, "w").write(scn)
+        args = [REF_HARNESS, "render", sp, str(w), str(h), op]
+        if window is not None or stride != 1:
+            x0, y0, x1, y1 = window if window is not None else (0, 0, w, h)
+            args += [str(x0), str(y0), str(x1), str(y1), str(stride)]
+        subprocess.run(args, check=True)
+        return read_ref_render(open(op, "rb").read())
+
+
+def read_ref_render(b: bytes) -> dict:
+    assert b[:6] == b"GIREF1"
+    w, h, n, _ = struct.unpack("<4i", b[8:24])
+    off = 24
+
+    def take(dtype, count):
+        nonlocal off
+        a = np.frombuffer(b, dtype=dtype, count=count, offset=off)
+        off += a.nbytes
+        return a.copy()
+
+    xs = take(np.int32, n)
+    ys = take(np.int32, n)
+    rgb = take(np.float64, 3 * n).reshape(n, 3)
+    hit = take(np.int32, n)
+    uv = take(np.int32, 2 * n).reshape(n, 2)
+    ncand = take(np.int32, n)
+    nnode = take(np.int32, n)
+    q = take(np.uint8, 3 * n).reshape(n, 3)
+    return dict(w=w, h=h, x=xs, y=ys, rgb=rgb, hit=hit, uv=uv, ncand=ncand, nnode=nnode, q=q)
+
+
+def ref_tree(scn: str) -> str:
+    with tempfile.TemporaryDirectory() as td:
+        sp = os.path.join(td, "s.scn")
+        open(sp, "w").write(scn)
+        return subprocess.run([REF_HARNESS, "tree", sp], check=True, capture_output=True, text=True).stdout
+
+
+def ref_rays(scn: str, rays: np.ndarray, n_ent: int) -> dict:
+    with tempfile.TemporaryDirectory() as td:
+        sp, rp, op = (os.path.join(td, f) for f in ("s.scn", "r.bin", "o.bin"))
+        open(sp, "w").write(scn)
+        with open(rp, "wb") as f:
+            f.write(struct.pack("<i", rays.shape[0]))
+            f.write(np.ascontiguousarray(rays, "<f8").tobytes())
+        subprocess.run([REF_HARNESS, "rays", sp, rp, op], check=True)
+        rec = np.dtype([("hit", "<i4"), ("pn", "<f8", 6), ("uv", "<i4", 2)])
+        a = np.frombuffer(open(op, "rb").read(), dtype=rec).reshape(rays.shape[0], n_ent)
+        return dict(hit=a["hit"].copy(), pn=a["pn"].copy(), uv=a["uv"].copy())
+
+
+def ref_boxes(recs: np.ndarray) -> np.ndarray:
+    with tempfile.TemporaryDirectory() as td:
+        rp, op = os.path.join(td, "r.bin"), os.path.join(td, "o.bin")
+        with open(rp, "wb") as f:
+            f.write(struct.pack("<i", recs.shape[0]))
+            f.write(np.ascontiguousarray(recs, "<f8").tobytes())
+        subprocess.run([REF_HARNESS, "boxes", rp, op], check=True)
+        return np.frombuffer(open(op, "rb").read(), dtype="<i4").copy()
+
+
+def bits_equal(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """Elementwise bit equality of float64 arrays (NaN == NaN when the payload matches)."""
+    return np.ascontiguousarray(a, np.float64).view(np.int64) == np.ascontiguousarray(b, np.float64).view(np.int64)
