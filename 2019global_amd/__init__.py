@@ -1,0 +1,409 @@
+"""2019global_amd — MI355X-native (gfx950) per-pixel radiance path for preon7/2019global.
+
+Host-side mirror of the reference's render API over the C-ABI in ``include/gi.h`` (``libgi.so``):
+
+  reference (C++ header-only)                         here
+  ---------------------------------------------------  ------------------------------------------
+  Camera(pos, lookAt, focal)        camera.h:8-10      Camera(pos, look_at, focal)
+  Octree(min, max) / push_back(e)   octree.h:115,121   Octree(min, max) / push_back(e)
+  ImpSphere / ImpTriangle / ExpQuad entities.h:45,138,581  same names and constructor arguments
+  Material(color[, shader]), .specular_power           Material(color, shader, specular_power)
+  RayTracer(camera, light)          raytracer.h:18     RayTracer(camera, light)
+    .setScene(octree) / .run(w, h) / .start() / .stop() / .running() / .getImage()
+
+``RayTracer.run`` renders on the GPU through ``gi_render`` and returns when the frame is done (or
+``stop()`` was called from another thread); ``getImage()`` returns the RGB888 frame the reference's
+``Image`` would hold.  There is no CPU fallback: without ``libgi.so`` or a gfx950 device every
+render raises ``GIError``.
+
+Lower-level handles for benchmarks and multi-GPU: ``DeviceScene`` (a scene resident in HBM) with
+``render_device`` into caller-owned device buffers on a HIP stream.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import scenes as _scenes
+
+__all__ = [
+    "GIError", "lib", "Camera", "Material", "Octree", "ImpSphere", "ImpTriangle", "ExpQuad",
+    "RayTracer", "DeviceScene", "MODE_R", "MODE_X", "STAT_RAYS", "STAT_NODES", "STAT_PRIMS",
+    "STAT_PIXELS", "TILE",
+]
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libgi.so")
+
+MODE_R, MODE_X = 0, 1
+FLAG_STATS = 1
+STAT_RAYS, STAT_NODES, STAT_PRIMS, STAT_PIXELS = 0, 1, 2, 3
+STATS_N = 8
+TILE = 8
+ABI_VERSION = 1
+
+
+class GIError(RuntimeError):
+    pass
+
+
+# ---- C structures (include/gi.h) -------------------------------------------------------------
+class EntityDesc(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("has_material", ctypes.c_int32), ("args", ctypes.c_double * 11),
+                ("mat_color", ctypes.c_double * 3), ("mat_shader", ctypes.c_double * 3),
+                ("mat_specular_power", ctypes.c_double)]
+
+
+class SceneDesc(ctypes.Structure):
+    _fields_ = [("octree_min", ctypes.c_double * 3), ("octree_max", ctypes.c_double * 3),
+                ("n_entities", ctypes.c_int32), ("entities", ctypes.POINTER(EntityDesc))]
+
+
+class CameraDesc(ctypes.Structure):
+    _fields_ = [("pos", ctypes.c_double * 3), ("up", ctypes.c_double * 3), ("forward", ctypes.c_double * 3),
+                ("focal", ctypes.c_double)]
+
+
+class Opts(ctypes.Structure):
+    _fields_ = [("mode", ctypes.c_int32), ("spp", ctypes.c_int32), ("depth", ctypes.c_int32),
+                ("shard_count", ctypes.c_int32), ("shard_index", ctypes.c_int32), ("band_rows", ctypes.c_int32),
+                ("flags", ctypes.c_uint32), ("reserved", ctypes.c_int32), ("seed", ctypes.c_uint64),
+                ("stats", ctypes.c_void_p)]
+
+
+class SceneInfo(ctypes.Structure):
+    _fields_ = [("n_entities", ctypes.c_int32), ("n_nodes", ctypes.c_int32), ("n_leaves", ctypes.c_int32),
+                ("max_depth", ctypes.c_int32), ("n_reachable", ctypes.c_int32), ("n_dropped", ctypes.c_int32),
+                ("x_nodes", ctypes.c_int32), ("x_prims", ctypes.c_int32), ("device_bytes", ctypes.c_int64)]
+
+
+class Hit(ctypes.Structure):
+    _fields_ = [("entity", ctypes.c_int32), ("u", ctypes.c_int32), ("v", ctypes.c_int32),
+                ("point", ctypes.c_double * 3), ("normal", ctypes.c_double * 3)]
+
+
+TILE_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint8),
+                           ctypes.POINTER(ctypes.c_double))
+
+EXPORTS = ["gi_abi_version", "gi_last_error", "gi_camera_init", "gi_scene_create", "gi_scene_destroy",
+           "gi_scene_get_info", "gi_render", "gi_render_device", "gi_shard_tiles", "gi_unshard_device",
+           "gi_trace_ray"]
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib():
+    """Load libgi.so (built in-tree by ``2019global_amd/build.py``).  torch, when importable, is
+    imported first so that libgi binds to the same HIP runtime instance torch uses."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise GIError(f"{LIB_PATH} is missing: run `python 2019global_amd/build.py` (no CPU fallback)")
+        try:
+            import torch  # noqa: F401  (one HIP runtime per process)
+        except ImportError:
+            pass
+        L = ctypes.CDLL(LIB_PATH)
+        vp, i32, dp = ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double)
+        L.gi_abi_version.restype = i32
+        L.gi_last_error.restype = ctypes.c_char_p
+        L.gi_camera_init.argtypes = [dp, dp, ctypes.c_double, ctypes.POINTER(CameraDesc)]
+        L.gi_scene_create.argtypes = [ctypes.POINTER(SceneDesc), ctypes.POINTER(vp)]
+        L.gi_scene_destroy.argtypes = [vp]
+        L.gi_scene_destroy.restype = None
+        L.gi_scene_get_info.argtypes = [vp, ctypes.POINTER(SceneInfo)]
+        L.gi_render.argtypes = [vp, ctypes.POINTER(CameraDesc), dp, i32, i32, ctypes.POINTER(Opts), dp,
+                                ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_int), TILE_CB, vp]
+        L.gi_render_device.argtypes = [vp, ctypes.POINTER(CameraDesc), dp, i32, i32, ctypes.POINTER(Opts), vp, vp, vp]
+        L.gi_shard_tiles.argtypes = [i32, i32, i32]
+        L.gi_shard_tiles.restype = ctypes.c_int64
+        L.gi_unshard_device.argtypes = [i32, i32, i32, vp, vp, vp, vp, vp]
+        L.gi_trace_ray.argtypes = [vp, dp, dp, dp, ctypes.POINTER(Hit), dp]
+        if L.gi_abi_version() != ABI_VERSION:
+            raise GIError(f"libgi ABI {L.gi_abi_version()} != {ABI_VERSION}")
+        _lib = L
+        return L
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise GIError(f"{what} failed ({rc}): {lib().gi_last_error().decode()}")
+
+
+def _d3(v) -> ctypes.Array:
+    return (ctypes.c_double * 3)(*[float(x) for x in v])
+
+
+# ---- reference-shaped API ---------------------------------------------------------------------
+class Material:
+    """Material(color[, shader]) (material.h:13-20); specular_power (material.h:29)."""
+
+    def __init__(self, color, shader=(0.1, 0.7, 1.0), specular_power: float = 5.0):
+        self.color = tuple(float(c) for c in color)
+        self.shader_parameters = tuple(float(c) for c in shader)
+        self.specular_power = float(specular_power)
+
+
+class _Entity:
+    kind = 0
+
+    def __init__(self, args: Sequence[float], material: Optional[Material]):
+        self._args = tuple(float(a) for a in args)
+        self._material = material   # explicit override (entity->material = ...)
+
+    @property
+    def material(self) -> Optional[Material]:
+        return self._material
+
+    @material.setter
+    def material(self, m: Material) -> None:
+        self._material = m
+
+    def _desc(self, d: EntityDesc) -> None:
+        d.kind = self.kind
+        for i, a in enumerate(self._args):
+            d.args[i] = a
+        m = self._material
+        d.has_material = 1 if m is not None else 0
+        if m is not None:
+            for i in range(3):
+                d.mat_color[i] = m.color[i]
+                d.mat_shader[i] = m.shader_parameters[i]
+            d.mat_specular_power = m.specular_power
+
+
+class ImpSphere(_Entity):
+    """ImpSphere(pos, float radius, color) (entities.h:45)."""
+    kind = _scenes.IMP_SPHERE
+
+    def __init__(self, pos, radius, color):
+        super().__init__((*pos, radius, *color), None)
+
+
+class ImpTriangle(_Entity):
+    """ImpTriangle(p1, p2, p3) (entities.h:138); default material red (entities.h:21)."""
+    kind = _scenes.IMP_TRIANGLE
+
+    def __init__(self, p1, p2, p3):
+        super().__init__((*p1, *p2, *p3), None)
+
+
+class ExpQuad(_Entity):
+    """ExpQuad(pos, float width, float length, float alpha, color) (entities.h:581)."""
+    kind = _scenes.EXP_QUAD
+
+    def __init__(self, pos, width, length, alpha, color):
+        super().__init__((*pos, width, length, alpha, *color), None)
+
+
+class Octree:
+    """Octree(min, max) + push_back (octree.h:115-144).  The tree itself is built by libgi from the
+    push order (gi_scene_create), exactly as the reference builds it."""
+
+    def __init__(self, min=(-20, -20, -20), max=(20, 20, 20)):
+        self.min = tuple(float(v) for v in min)
+        self.max = tuple(float(v) for v in max)
+        self.entities = []
+
+    def push_back(self, e: _Entity) -> None:
+        self.entities.append(e)
+
+    @classmethod
+    def from_scene(cls, s: "_scenes.Scene") -> "Octree":
+        o = cls(s.octree_min, s.octree_max)
+        for e in s.entities:
+            ent = _Entity(e.args, None if e.material is None else
+                          Material(e.material.color, e.material.shader, e.material.specular_power))
+            ent.kind = e.kind
+            o.push_back(ent)
+        return o
+
+    def _scene_desc(self):
+        n = len(self.entities)
+        arr = (EntityDesc * max(n, 1))()
+        for i, e in enumerate(self.entities):
+            e._desc(arr[i])
+        d = SceneDesc()
+        d.octree_min = _d3(self.min)
+        d.octree_max = _d3(self.max)
+        d.n_entities = n
+        d.entities = ctypes.cast(arr, ctypes.POINTER(EntityDesc))
+        return d, arr
+
+
+class Camera:
+    """Camera(pos, lookAt, focal) (camera.h:8-10): up = (0,0,1), forward = normalize(lookAt - pos)."""
+
+    def __init__(self, pos, lookAt=(0.0, 0.0, 0.0), focal: float = 0.04):
+        self._c = CameraDesc()
+        _check(lib().gi_camera_init(_d3(pos), _d3(lookAt), float(focal), ctypes.byref(self._c)), "gi_camera_init")
+
+    @property
+    def pos(self):
+        return tuple(self._c.pos)
+
+    @property
+    def up(self):
+        return tuple(self._c.up)
+
+    @property
+    def forward(self):
+        return tuple(self._c.forward)
+
+    @property
+    def focalDist(self):
+        return self._c.focal
+
+
+class DeviceScene:
+    """A scene resident in HBM on the current HIP device (gi_scene_create)."""
+
+    def __init__(self, octree: Octree):
+        L = lib()
+        d, keep = octree._scene_desc()
+        h = ctypes.c_void_p()
+        _check(L.gi_scene_create(ctypes.byref(d), ctypes.byref(h)), "gi_scene_create")
+        self._h = h
+        del keep
+
+    @classmethod
+    def from_scene(cls, s: "_scenes.Scene") -> "DeviceScene":
+        return cls(Octree.from_scene(s))
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) and self._h.value:
+            lib().gi_scene_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def info(self) -> dict:
+        i = SceneInfo()
+        _check(lib().gi_scene_get_info(self._h, ctypes.byref(i)), "gi_scene_get_info")
+        return {f: getattr(i, f) for f, _ in SceneInfo._fields_}
+
+    @staticmethod
+    def opts(mode=MODE_R, spp=1, depth=1, seed=0, shard_count=1, shard_index=0, band_rows=0, stats_ptr=0) -> Opts:
+        o = Opts()
+        o.mode, o.spp, o.depth, o.seed = mode, spp, depth, seed
+        o.shard_count, o.shard_index, o.band_rows = shard_count, shard_index, band_rows
+        o.flags = FLAG_STATS if stats_ptr else 0
+        o.stats = stats_ptr or None
+        return o
+
+    def render(self, cam: Camera, light, w: int, h: int, mode=MODE_R, spp=1, depth=1, seed=0, band_rows=0,
+               cancel: Optional[ctypes.c_int] = None, callback=None):
+        """Host-buffer render (gi_render).  Returns (rgb float64 [h,w,3], rgb8 uint8 [h,w,3])."""
+        rgb = np.zeros((h, w, 3), np.float64)
+        rgb8 = np.zeros((h, w, 3), np.uint8)
+        cb = TILE_CB(callback) if callback is not None else TILE_CB()
+        o = self.opts(mode, spp, depth, seed, band_rows=band_rows)
+        _check(lib().gi_render(self._h, ctypes.byref(cam._c), _d3(light), w, h, ctypes.byref(o),
+                               rgb.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                               rgb8.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                               ctypes.byref(cancel) if cancel is not None else None, cb, None), "gi_render")
+        return rgb, rgb8
+
+    def render_device(self, cam: Camera, light, w: int, h: int, d_rgb: int, d_rgb8: int = 0, stream: int = 0,
+                      mode=MODE_R, spp=1, depth=1, seed=0, shard_count=1, shard_index=0, stats_ptr=0) -> None:
+        """Asynchronous render into device buffers (gi_render_device); pointers are ints."""
+        o = self.opts(mode, spp, depth, seed, shard_count, shard_index, stats_ptr=stats_ptr)
+        _check(lib().gi_render_device(self._h, ctypes.byref(cam._c), _d3(light), w, h, ctypes.byref(o),
+                                      d_rgb or None, d_rgb8 or None, stream or None), "gi_render_device")
+
+    def trace_ray(self, origin, direction, light):
+        hit = Hit()
+        rgb = (ctypes.c_double * 3)()
+        _check(lib().gi_trace_ray(self._h, _d3(origin), _d3(direction), _d3(light), ctypes.byref(hit), rgb),
+               "gi_trace_ray")
+        return hit, tuple(rgb)
+
+
+def shard_tiles(w: int, h: int, shard_count: int) -> int:
+    return int(lib().gi_shard_tiles(w, h, shard_count))
+
+
+def unshard_device(w, h, shard_count, d_packed, d_packed8, d_rgb, d_rgb8, stream=0) -> None:
+    _check(lib().gi_unshard_device(w, h, shard_count, d_packed or None, d_packed8 or None, d_rgb or None,
+                                   d_rgb8 or None, stream or None), "gi_unshard_device")
+
+
+class Image:
+    """What the reference's Image (image.h:7-29) holds after run(): RGB888 pixels."""
+
+    def __init__(self, rgb8: np.ndarray, rgb: Optional[np.ndarray] = None):
+        self.rgb8 = rgb8
+        self.radiance = rgb
+
+    def width(self) -> int:
+        return self.rgb8.shape[1]
+
+    def height(self) -> int:
+        return self.rgb8.shape[0]
+
+    def getPixel(self, x: int, y: int):
+        p = self.rgb8[y, x]
+        return (p[0] / 255.0, p[1] / 255.0, p[2] / 255.0)
+
+
+class RayTracer:
+    """RayTracer(camera, light) (raytracer.h:15-101) backed by the gfx950 kernels."""
+
+    def __init__(self, camera: Camera, light):
+        self._camera = camera
+        self._light = tuple(float(v) for v in light)
+        self._image = Image(np.zeros((0, 0, 3), np.uint8))
+        self._scene: Optional[Octree] = None
+        self._dev: Optional[DeviceScene] = None
+        self._cancel = ctypes.c_int(1)   # _running = false (raytracer.h:96)
+        self.band_rows = 64              # progressive granularity (reference: per pixel)
+
+    def setScene(self, scene: Octree) -> None:
+        self._scene = scene
+        self._dev = None   # rebuilt lazily on the next run()
+
+    def running(self) -> bool:
+        return self._cancel.value == 0
+
+    def stop(self) -> None:
+        self._cancel.value = 1
+
+    def start(self) -> None:
+        self._cancel.value = 0
+
+    def getImage(self) -> Image:
+        return self._image
+
+    def run(self, w: int, h: int) -> None:
+        self._image = Image(np.zeros((h, w, 3), np.uint8), np.zeros((h, w, 3)))   # raytracer.h:25
+        if self._scene is None:
+            raise GIError("setScene() was not called")
+        if self._dev is None:
+            self._dev = DeviceScene(self._scene)
+        img = self._image
+
+        def on_band(_user, y0, rows, p8, pf):
+            n = w * rows * 3
+            img.rgb8[y0:y0 + rows] = np.ctypeslib.as_array(p8, shape=(n,)).reshape(rows, w, 3)
+            img.radiance[y0:y0 + rows] = np.ctypeslib.as_array(pf, shape=(n,)).reshape(rows, w, 3)
+
+        rgb = np.zeros((h, w, 3))
+        rgb8 = np.zeros((h, w, 3), np.uint8)
+        o = DeviceScene.opts(MODE_R, band_rows=self.band_rows)
+        cb = TILE_CB(on_band)
+        rc = lib().gi_render(self._dev._h, ctypes.byref(self._camera._c), _d3(self._light), w, h, ctypes.byref(o),
+                             rgb.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                             rgb8.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), ctypes.byref(self._cancel), cb, None)
+        if rc not in (0, -4):   # -4: stopped, partial frame like the reference's loop exit
+            _check(rc, "gi_render")

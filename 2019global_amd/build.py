@@ -1,0 +1,64 @@
+"""Builds 2019global_amd/libgi.so in-tree (gfx950 only).
+
+Host translation units (scene builder, C-ABI) are compiled by g++ and the kernels by hipcc, both
+with ``-ffp-contract=off``: the Mode R parity contract is bit-level and the reference (x86-64,
+no FMA) never contracts a*b+c.  Run ``python -m 2019global_amd.build`` or ``__graft_entry__.build()``.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+INCLUDE = os.path.join(ROOT, "include")
+OUT = os.path.join(HERE, "libgi.so")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = "gfx950"
+
+HOST_SRCS = ["gi_build.cpp", "gi_capi.cpp"]
+DEV_SRCS = ["gi_kernels.hip"]
+HEADERS = ["gi_math.h", "gi_scene.h"]
+
+COMMON = ["-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", f"-I{INCLUDE}", f"-I{CSRC}"]
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+
+
+def _stale(out, deps):
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(verbose: bool = False, force: bool = False) -> str:
+    hipcc = shutil.which("hipcc") or os.path.join(ROCM, "bin", "hipcc")
+    objdir = os.path.join(HERE, "_obj")
+    os.makedirs(objdir, exist_ok=True)
+    hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "gi.h")]
+    objs = []
+    for s in HOST_SRCS:
+        src, obj = os.path.join(CSRC, s), os.path.join(objdir, s + ".o")
+        if force or _stale(obj, [src] + hdrs):
+            _run(["g++", "-O2", *COMMON, "-D__HIP_PLATFORM_AMD__", f"-I{ROCM}/include", "-c", src, "-o", obj], verbose)
+        objs.append(obj)
+    for s in DEV_SRCS:
+        src, obj = os.path.join(CSRC, s), os.path.join(objdir, s + ".o")
+        if force or _stale(obj, [src] + hdrs):
+            _run([hipcc, f"--offload-arch={ARCH}", "-O3", *COMMON, "-munsafe-fp-atomics", "-c", src, "-o", obj], verbose)
+        objs.append(obj)
+    if force or _stale(OUT, objs):
+        _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-o", OUT, *objs, f"-L{ROCM}/lib", "-lamdhip64"], verbose)
+    return OUT
+
+
+if __name__ == "__main__":
+    build(verbose=True, force="--force" in sys.argv)

@@ -1,0 +1,372 @@
+// gi_build.cpp — host-side scene construction for libgi (compiled by g++ -ffp-contract=off).
+//
+// Entities are built exactly as the reference constructors build them (own restatement):
+//   ImpSphere   entities.h:45-47, bbox :98-99 (member-init while pos == {0,0,0})
+//   ImpTriangle entities.h:138-148, bbox :251-275 (+0.01 on max.z, +1e-5 on flat axes, A.13)
+//   ExpQuad     entities.h:581-590 (float trig on the float alpha), bbox :623-624 (A.5)
+// then pushed into the reference octree with Octree::push_back semantics (octree.h:121-230,
+// bbox.h:25-39), including the silent drop (A.14) and entities kept only at the split node (A.6).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+
+#include "gi.h"
+#include "gi_scene.h"
+
+namespace gi {
+
+namespace {
+
+struct BEnt {
+    REnt rec;
+    V3 bmin, bmax;
+    std::vector<TriRec> tris;
+};
+
+REnt blank_rec(int kind) {
+    REnt r;
+    memset(&r, 0, sizeof r);
+    r.kind = kind;
+    r.color[0] = 1; r.color[1] = 0; r.color[2] = 0;   // Entity() : Material(dvec3(1,0,0)) (entities.h:21)
+    r.shader[0] = 0.1; r.shader[1] = 0.7; r.shader[2] = 1.0;   // material.h:27
+    r.spec_pow = 5.0;                                          // material.h:29
+    return r;
+}
+
+void set_color(REnt& r, const double* c) { r.color[0] = c[0]; r.color[1] = c[1]; r.color[2] = c[2]; }
+
+bool build_entity(const gi_entity_desc& d, BEnt& e, std::string& err) {
+    const double* a = d.args;
+    switch (d.kind) {
+    case GI_IMP_SPHERE: {
+        e.rec = blank_rec(K_IMP_SPHERE);
+        set_color(e.rec, a + 4);
+        e.rec.radius = (float)a[3];
+        e.rec.pos[0] = a[0]; e.rec.pos[1] = a[1]; e.rec.pos[2] = a[2];
+        const double r = e.rec.radius;
+        e.bmin = v3((float)(0.0 - r), (float)(0.0 - r), (float)(0.0 - r));
+        e.bmax = v3((float)(0.0 + r), (float)(0.0 + r), (float)(0.0 + r));
+        break;
+    }
+    case GI_IMP_TRIANGLE: {
+        e.rec = blank_rec(K_IMP_TRIANGLE);
+        TriRec t;
+        const V3 p1 = v3(a[0], a[1], a[2]), p2 = v3(a[3], a[4], a[5]), p3 = v3(a[6], a[7], a[8]);
+        make_tri(p1, p2, p3, t);
+        e.tris.push_back(t);
+        e.rec.pos[0] = t.pos[0]; e.rec.pos[1] = t.pos[1]; e.rec.pos[2] = t.pos[2];
+        e.bmin = v3(smin(smin(p1.x, p2.x), p3.x), smin(smin(p1.y, p2.y), p3.y), smin(smin(p1.z, p2.z), p3.z));
+        e.bmax = v3(smax(smax(p1.x, p2.x), p3.x), smax(smax(p1.y, p2.y), p3.y), smax(smax(p1.z, p2.z), p3.z) + 0.01);
+        if (e.bmax.x == e.bmin.x) e.bmax.x += 1e-5;
+        if (e.bmax.y == e.bmin.y) e.bmax.y += 1e-5;
+        if (e.bmax.z == e.bmin.z) e.bmax.z += 1e-5;
+        break;
+    }
+    case GI_EXP_QUAD: {
+        e.rec = blank_rec(K_EXP_QUAD);
+        set_color(e.rec, a + 6);
+        const V3 pos = v3(a[0], a[1], a[2]);
+        e.rec.pos[0] = pos.x; e.rec.pos[1] = pos.y; e.rec.pos[2] = pos.z;
+        const float w = (float)a[3], l = (float)a[4], al = (float)a[5];
+        e.rec.width = w; e.rec.length = l; e.rec.alpha = al;
+        const float hw = w / 2, hl = l / 2;
+        const double ca = (double)std::cos(al), sa = (double)std::sin(al);   // float overloads (cosf/sinf)
+        V3 q[4];
+        q[0] = v3((pos.x + hw) * ca, pos.y + hl, pos.z + (pos.x + hw) * sa);
+        q[1] = v3((pos.x - hw) * ca, pos.y + hl, pos.z + (pos.x - hw) * sa);
+        q[2] = v3((pos.x + hw) * ca, pos.y - hl, pos.z + (pos.x + hw) * sa);
+        q[3] = v3((pos.x - hw) * ca, pos.y - hl, pos.z + pos.z + (pos.x - hw) * sa);   // entities.h:586
+        TriRec t0, t1;
+        make_tri(q[1], q[2], q[0], t0);   // entities.h:588
+        make_tri(q[1], q[3], q[2], t1);   // entities.h:589
+        e.tris.push_back(t0);
+        e.tris.push_back(t1);
+        st3(e.rec.qv0, q[0]);
+        st3(e.rec.qv1, q[1]);
+        e.bmin = v3((float)(0.0 - hw), (float)(0.0 - hl), (float)0.0);
+        e.bmax = v3((float)(0.0 + hw), (float)(0.0 + hl), (float)(0.0 + (0.0 + hw) * sa));
+        break;
+    }
+    default:
+        err = "unsupported entity kind " + std::to_string(d.kind);
+        return false;
+    }
+    if (d.has_material) {
+        set_color(e.rec, d.mat_color);
+        e.rec.shader[0] = d.mat_shader[0]; e.rec.shader[1] = d.mat_shader[1]; e.rec.shader[2] = d.mat_shader[2];
+        e.rec.spec_pow = d.mat_specular_power;
+    }
+    return true;
+}
+
+// ---- reference octree ------------------------------------------------------------------------
+bool bb_overlap(V3 amin, V3 amax, V3 bmin, V3 bmax) {   // BoundingBox::intersect (bbox.h:25-39)
+    const V3 p1 = 0.5 * (amin + amax), p2 = 0.5 * (bmin + bmax);
+    const V3 d = p1 - p2;
+    const bool xo = std::fabs(d.x) < (0.5 * (amax.x - amin.x) + 0.5 * (bmax.x - bmin.x));
+    const bool yo = std::fabs(d.y) < (0.5 * (amax.y - amin.y) + 0.5 * (bmax.y - bmin.y));
+    const bool zo = std::fabs(d.z) < (0.5 * (amax.z - amin.z) + 0.5 * (bmax.z - bmin.z));
+    return xo && yo && zo;
+}
+bool le3(V3 a, V3 b) { return a.x <= b.x && a.y <= b.y && a.z <= b.z; }
+
+struct RBuild {
+    struct N {
+        V3 mn, mx;
+        std::vector<int32_t> ents;
+        int32_t child0 = -1;
+    };
+    std::vector<N> nodes;
+    const std::vector<BEnt>* ents;
+
+    void partition(int ni) {   // octree.h:176-211
+        if (nodes[ni].child0 >= 0) return;
+        const V3 mn = nodes[ni].mn, mx = nodes[ni].mx;
+        const V3 mid = (mn + mx) * 0.5;
+        bool all_in = true;
+        for (int32_t e : nodes[ni].ents) all_in = all_in && le3((*ents)[e].bmin, mid) && le3(mid, (*ents)[e].bmax);
+        if (all_in) return;
+        const V3 bx[8][2] = {
+            {mn, mid},
+            {v3(mn.x, mid.y, mn.z), v3(mid.x, mx.y, mid.z)},
+            {v3(mid.x, mn.y, mn.z), v3(mx.x, mid.y, mid.z)},
+            {v3(mid.x, mid.y, mn.z), v3(mx.x, mx.y, mid.z)},
+            {mid, mx},
+            {v3(mn.x, mid.y, mid.z), v3(mid.x, mx.y, mx.z)},
+            {v3(mid.x, mn.y, mid.z), v3(mx.x, mid.y, mx.z)},
+            {v3(mn.x, mn.y, mid.z), v3(mid.x, mid.y, mx.z)},
+        };
+        const int32_t c0 = (int32_t)nodes.size();
+        for (int c = 0; c < 8; ++c) {
+            N n;
+            n.mn = bx[c][0];
+            n.mx = bx[c][1];
+            nodes.push_back(n);
+        }
+        nodes[ni].child0 = c0;
+    }
+    void push_obj(int ni, int32_t e) {   // octree.h:216-230
+        nodes[ni].ents.push_back(e);
+        partition(ni);
+        if (nodes[ni].child0 < 0) return;
+        const BEnt& E = (*ents)[e];
+        for (int c = 0; c < 8; ++c) {
+            const int ci = nodes[ni].child0 + c;
+            if (le3(nodes[ci].mn, E.bmin) && le3(E.bmax, nodes[ci].mx)) push_obj(ci, e);
+            else if (bb_overlap(nodes[ci].mn, nodes[ci].mx, E.bmin, E.bmax)) nodes[ci].ents.push_back(e);
+        }
+    }
+};
+
+// ---- Mode X octree (build-defined: tight cells, every overlapping leaf holds the primitive) ---
+struct Box {
+    double mn[3], mx[3];
+};
+const int XLEAF_MAX = 4;
+const int XMAX_DEPTH = 16;
+
+struct XBuild {
+    const std::vector<Box>* pb;
+    std::vector<XNode>* out;
+    std::vector<int32_t>* idx;
+    double pad;
+    int max_depth = 0;
+
+    static bool overlap(const Box& a, const Box& b) {
+        for (int k = 0; k < 3; ++k)
+            if (a.mx[k] < b.mn[k] || b.mx[k] < a.mn[k]) return false;
+        return true;
+    }
+    Box tight(const Box& cell, const std::vector<int32_t>& prims) const {
+        Box u;
+        for (int k = 0; k < 3; ++k) { u.mn[k] = INFINITY; u.mx[k] = -INFINITY; }
+        for (int32_t p : prims)
+            for (int k = 0; k < 3; ++k) {
+                u.mn[k] = std::min(u.mn[k], (*pb)[p].mn[k]);
+                u.mx[k] = std::max(u.mx[k], (*pb)[p].mx[k]);
+            }
+        Box t;
+        for (int k = 0; k < 3; ++k) {
+            t.mn[k] = std::max(cell.mn[k], u.mn[k]) - pad;
+            t.mx[k] = std::min(cell.mx[k], u.mx[k]) + pad;
+        }
+        return t;
+    }
+    // builds node `ni` (already allocated) for `cell` holding `prims`
+    void build(int ni, const Box& cell, std::vector<int32_t>& prims, int depth) {
+        max_depth = std::max(max_depth, depth);
+        const Box tb = tight(cell, prims);
+        XNode& n0 = (*out)[ni];
+        for (int k = 0; k < 3; ++k) { n0.mn[k] = tb.mn[k]; n0.mx[k] = tb.mx[k]; }
+        n0.child_base = -1; n0.child_mask = 0; n0.prim_off = 0; n0.prim_cnt = 0;
+        std::vector<int32_t> kids[8];
+        Box cb[8];
+        bool split = (int)prims.size() > XLEAF_MAX && depth < XMAX_DEPTH;
+        if (split) {
+            double mid[3];
+            for (int k = 0; k < 3; ++k) mid[k] = 0.5 * (cell.mn[k] + cell.mx[k]);
+            bool progress = false;
+            for (int c = 0; c < 8; ++c) {
+                for (int k = 0; k < 3; ++k) {
+                    const bool hi = (c >> k) & 1;
+                    cb[c].mn[k] = hi ? mid[k] : cell.mn[k];
+                    cb[c].mx[k] = hi ? cell.mx[k] : mid[k];
+                }
+                Box test = cb[c];
+                for (int k = 0; k < 3; ++k) { test.mn[k] -= pad; test.mx[k] += pad; }
+                for (int32_t p : prims)
+                    if (overlap(test, (*pb)[p])) kids[c].push_back(p);
+                if (!kids[c].empty() && kids[c].size() < prims.size()) progress = true;
+            }
+            split = progress;
+        }
+        if (!split) {
+            XNode& n = (*out)[ni];
+            n.prim_off = (int32_t)idx->size();
+            n.prim_cnt = (int32_t)prims.size();
+            idx->insert(idx->end(), prims.begin(), prims.end());
+            return;
+        }
+        int mask = 0, cnt = 0;
+        for (int c = 0; c < 8; ++c)
+            if (!kids[c].empty()) { mask |= 1 << c; ++cnt; }
+        const int base = (int)out->size();
+        out->resize(out->size() + cnt);
+        (*out)[ni].child_base = base;
+        (*out)[ni].child_mask = mask;
+        std::vector<int32_t>().swap(prims);   // release before recursing
+        int k = 0;
+        for (int c = 0; c < 8; ++c)
+            if (!kids[c].empty()) build(base + k++, cb[c], kids[c], depth + 1);
+    }
+};
+
+}  // namespace
+
+bool build_host_scene(const gi_scene_desc& desc, HostScene& hs, std::string& err) {
+    std::vector<BEnt> ents((size_t)desc.n_entities);
+    for (int i = 0; i < desc.n_entities; ++i)
+        if (!build_entity(desc.entities[i], ents[i], err)) return false;
+
+    // entity + triangle records
+    hs.ents.clear();
+    hs.tris.clear();
+    for (BEnt& e : ents) {
+        e.rec.tri_first = (int32_t)hs.tris.size();
+        e.rec.tri_count = (int32_t)e.tris.size();
+        hs.tris.insert(hs.tris.end(), e.tris.begin(), e.tris.end());
+        hs.ents.push_back(e.rec);
+    }
+
+    // reference octree
+    RBuild rb;
+    rb.ents = &ents;
+    RBuild::N root;
+    root.mn = v3(desc.octree_min[0], desc.octree_min[1], desc.octree_min[2]);
+    root.mx = v3(desc.octree_max[0], desc.octree_max[1], desc.octree_max[2]);
+    rb.nodes.push_back(root);
+    hs.n_dropped = 0;
+    for (int32_t i = 0; i < desc.n_entities; ++i) {
+        if (!bb_overlap(rb.nodes[0].mn, rb.nodes[0].mx, ents[i].bmin, ents[i].bmax)) { ++hs.n_dropped; continue; }   // octree.h:123-125
+        rb.push_obj(0, i);
+    }
+    const size_t nn = rb.nodes.size();
+    hs.rnodes.assign(nn, RNode());
+    hs.leaf_ents.clear();
+    std::vector<int32_t> depth(nn, 0);
+    std::vector<char> reach((size_t)desc.n_entities, 0);
+    hs.n_leaves = 0;
+    hs.max_depth = 0;
+    for (size_t i = 0; i < nn; ++i) {
+        const RBuild::N& s = rb.nodes[i];
+        RNode& d = hs.rnodes[i];
+        st3(d.mn, s.mn);
+        st3(d.mx, s.mx);
+        d.child0 = s.child0;
+        if (i == 0) d.parent = -1;
+        d.ent_cnt = (int32_t)s.ents.size();
+        d.ent_off = -1;
+        if (s.child0 < 0) {
+            d.ent_off = (int32_t)hs.leaf_ents.size();
+            hs.leaf_ents.insert(hs.leaf_ents.end(), s.ents.begin(), s.ents.end());
+            for (int32_t e : s.ents) reach[e] = 1;
+            ++hs.n_leaves;
+        } else {
+            for (int c = 0; c < 8; ++c) {
+                hs.rnodes[s.child0 + c].parent = (int32_t)i;
+                depth[s.child0 + c] = depth[i] + 1;
+            }
+        }
+        hs.max_depth = std::max(hs.max_depth, depth[i]);
+    }
+    hs.n_reachable = 0;
+    for (char r : reach) hs.n_reachable += r;
+
+    // Mode X primitives (every entity, in push order; ExpQuad contributes its 2 triangles)
+    hs.xprims.clear();
+    std::vector<Box> pb;
+    for (int32_t i = 0; i < desc.n_entities; ++i) {
+        const REnt& r = hs.ents[i];
+        if (r.kind == K_IMP_SPHERE) {
+            XPrim p;
+            memset(&p, 0, sizeof p);
+            p.kind = 1; p.ent = i;
+            p.a[0] = r.pos[0]; p.a[1] = r.pos[1]; p.a[2] = r.pos[2];
+            p.b[0] = (double)r.radius;
+            hs.xprims.push_back(p);
+            Box b;
+            for (int k = 0; k < 3; ++k) { b.mn[k] = r.pos[k] - (double)r.radius; b.mx[k] = r.pos[k] + (double)r.radius; }
+            pb.push_back(b);
+        } else {
+            for (int t = 0; t < r.tri_count; ++t) {
+                const TriRec& tr = hs.tris[r.tri_first + t];
+                XPrim p;
+                memset(&p, 0, sizeof p);
+                p.kind = 0; p.ent = i;
+                const V3 p1 = ld3(tr.p1), e1 = ld3(tr.p2) - p1, e2 = ld3(tr.p3) - p1;
+                st3(p.a, p1); st3(p.b, e1); st3(p.c, e2);
+                for (int k = 0; k < 3; ++k) p.n[k] = tr.n[k];
+                hs.xprims.push_back(p);
+                Box b;
+                for (int k = 0; k < 3; ++k) {
+                    b.mn[k] = std::min(std::min(tr.p1[k], tr.p2[k]), tr.p3[k]);
+                    b.mx[k] = std::max(std::max(tr.p1[k], tr.p2[k]), tr.p3[k]);
+                }
+                pb.push_back(b);
+            }
+        }
+    }
+    hs.xnodes.clear();
+    hs.xprim_idx.clear();
+    hs.xnodes.resize(1);
+    Box rootb;
+    for (int k = 0; k < 3; ++k) { rootb.mn[k] = INFINITY; rootb.mx[k] = -INFINITY; }
+    for (const Box& b : pb)
+        for (int k = 0; k < 3; ++k) { rootb.mn[k] = std::min(rootb.mn[k], b.mn[k]); rootb.mx[k] = std::max(rootb.mx[k], b.mx[k]); }
+    if (pb.empty()) {
+        for (int k = 0; k < 3; ++k) { rootb.mn[k] = 0; rootb.mx[k] = 0; }
+    }
+    double ext = 1.0;
+    for (int k = 0; k < 3; ++k) ext = std::max(ext, std::max(std::fabs(rootb.mn[k]), std::fabs(rootb.mx[k])));
+    XBuild xb;
+    xb.pb = &pb;
+    xb.out = &hs.xnodes;
+    xb.idx = &hs.xprim_idx;
+    xb.pad = 1e-9 * ext;
+    std::vector<int32_t> all(pb.size());
+    for (size_t i = 0; i < pb.size(); ++i) all[i] = (int32_t)i;
+    if (pb.empty()) {
+        XNode& n = hs.xnodes[0];
+        memset(&n, 0, sizeof n);
+        n.mn[0] = n.mn[1] = n.mn[2] = 1.0;   // empty box: no ray enters
+        n.mx[0] = n.mx[1] = n.mx[2] = -1.0;
+        n.child_base = -1;
+    } else {
+        xb.build(0, rootb, all, 0);
+    }
+    hs.x_max_depth = xb.max_depth;
+    return true;
+}
+
+}  // namespace gi

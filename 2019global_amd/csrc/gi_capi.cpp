@@ -1,0 +1,282 @@
+// gi_capi.cpp — the extern "C" boundary (include/gi.h).  Host-side only: validates arguments,
+// builds the scene (gi_build.cpp), owns its HBM copy, and launches the gfx950 kernels
+// (gi_kernels.hip).  There is no CPU rendering path: without a gfx950 device every call fails.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "gi.h"
+#include "gi_scene.h"
+
+namespace gi {
+struct CamDev {
+    V3 pos, up, left, top_left;
+    double rx, ry;
+};
+bool build_host_scene(const gi_scene_desc& desc, HostScene& hs, std::string& err);
+long long shard_tiles(int w, int h, int shard_count);
+hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w, int h, int y0, const gi_opts& o,
+                         double* rgb, uint8_t* rgb8, hipStream_t stream);
+hipError_t launch_unshard(int w, int h, int shard_count, const double* packed, const uint8_t* packed8, double* rgb,
+                          uint8_t* rgb8, hipStream_t stream);
+hipError_t launch_trace_ray(const DevScene& sc, V3 o, V3 d, V3 light, int32_t* out_i, double* out_d, hipStream_t stream);
+}  // namespace gi
+
+using namespace gi;
+
+struct gi_scene {
+    HostScene host;
+    DevScene dev;
+    std::vector<void*> allocs;
+    int device = -1;
+    int64_t bytes = 0;
+    bool mode_x_ok = true;
+};
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+int hip_fail(hipError_t e, const char* what) {
+    return fail(GI_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+template <typename T>
+hipError_t upload(gi_scene* s, const std::vector<T>& v, const T** out) {
+    *out = nullptr;
+    const size_t bytes = std::max<size_t>(v.size() * sizeof(T), 16);
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) return e;
+    s->allocs.push_back(p);
+    s->bytes += (int64_t)bytes;
+    if (!v.empty()) {
+        e = hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+        if (e != hipSuccess) return e;
+    }
+    *out = static_cast<const T*>(p);
+    return hipSuccess;
+}
+
+// raytracer.h:26-30: camera basis and the frame's top-left (vertical offset uses w)
+CamDev make_cam(const gi_camera& c, int w) {
+    CamDev d;
+    d.pos = v3(c.pos[0], c.pos[1], c.pos[2]);
+    d.up = v3(c.up[0], c.up[1], c.up[2]);
+    const V3 fwd = v3(c.forward[0], c.forward[1], c.forward[2]);
+    d.rx = 0.0002;
+    d.ry = 0.0002;
+    d.left = normalize(cross(d.up, fwd));
+    d.top_left = (((d.pos + c.focal * fwd) + ((d.left * (double)w) * 0.5) * d.rx) + ((d.up * (double)w) * 0.5) * d.ry) - d.pos;
+    return d;
+}
+
+int check_opts(const gi_scene* s, int w, int h, const gi_opts* o) {
+    if (!s || !o) return fail(GI_ERR_ARG, "null scene or opts");
+    if (w <= 0 || h <= 0 || (int64_t)w * h > (int64_t)1 << 34) return fail(GI_ERR_ARG, "bad frame size");
+    if (o->mode != GI_MODE_R && o->mode != GI_MODE_X) return fail(GI_ERR_ARG, "bad mode");
+    if (o->shard_count < 1 || o->shard_index < 0 || o->shard_index >= o->shard_count) return fail(GI_ERR_ARG, "bad shard");
+    if (o->mode == GI_MODE_X) {
+        if (o->spp < 1 || o->depth < 1 || o->depth > 0xFFFF) return fail(GI_ERR_ARG, "mode X needs spp >= 1, 1 <= depth <= 65535");
+        if (!s->mode_x_ok) return fail(GI_ERR_SCENE, "mode X needs integer specular_power in [0, 64]");
+    }
+    if ((o->flags & GI_FLAG_STATS) && !o->stats) return fail(GI_ERR_ARG, "GI_FLAG_STATS without stats buffer");
+    return GI_OK;
+}
+
+int bind_device(const gi_scene* s) {
+    int cur = -1;
+    hipError_t e = hipGetDevice(&cur);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+    if (cur != s->device) {
+        e = hipSetDevice(s->device);
+        if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    }
+    return GI_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int gi_abi_version(void) { return GI_ABI_VERSION; }
+const char* gi_last_error(void) { return g_err.c_str(); }
+
+int gi_camera_init(const double pos[3], const double look_at[3], double focal, gi_camera* out) {
+    if (!pos || !look_at || !out) return fail(GI_ERR_ARG, "null argument");
+    // Camera(pos, lookAt, focal) (camera.h:8-10): up = (0,0,1); forward = normalize(lookAt - pos)
+    const V3 p = v3(pos[0], pos[1], pos[2]);
+    const V3 f = normalize(v3(look_at[0], look_at[1], look_at[2]) - p);
+    st3(out->pos, p);
+    out->up[0] = 0; out->up[1] = 0; out->up[2] = 1.0;
+    st3(out->forward, f);
+    out->focal = focal;
+    return GI_OK;
+}
+
+int gi_scene_create(const gi_scene_desc* desc, gi_scene** out) {
+    if (!desc || !out || desc->n_entities < 0 || (desc->n_entities > 0 && !desc->entities))
+        return fail(GI_ERR_ARG, "bad scene descriptor");
+    *out = nullptr;
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev <= 0) return fail(GI_ERR_DEVICE, "no HIP device (libgi renders only on gfx950)");
+    int dev = 0;
+    if ((e = hipGetDevice(&dev)) != hipSuccess) return hip_fail(e, "hipGetDevice");
+    hipDeviceProp_t prop;
+    if ((e = hipGetDeviceProperties(&prop, dev)) != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(GI_ERR_DEVICE, std::string("device is ") + prop.gcnArchName + ", libgi is built for gfx950 only");
+
+    gi_scene* s = new gi_scene();
+    s->device = dev;
+    std::string err;
+    if (!build_host_scene(*desc, s->host, err)) {
+        delete s;
+        return fail(GI_ERR_SCENE, err);
+    }
+    for (const REnt& r : s->host.ents)
+        if (!(r.spec_pow >= 0 && r.spec_pow <= 64 && r.spec_pow == std::floor(r.spec_pow))) s->mode_x_ok = false;
+    DevScene& d = s->dev;
+    memset(&d, 0, sizeof d);
+    const HostScene& h = s->host;
+    if ((e = upload(s, h.rnodes, &d.rnodes)) != hipSuccess || (e = upload(s, h.leaf_ents, &d.leaf_ents)) != hipSuccess ||
+        (e = upload(s, h.ents, &d.ents)) != hipSuccess || (e = upload(s, h.tris, &d.tris)) != hipSuccess ||
+        (e = upload(s, h.xnodes, &d.xnodes)) != hipSuccess || (e = upload(s, h.xprim_idx, &d.xprim_idx)) != hipSuccess ||
+        (e = upload(s, h.xprims, &d.xprims)) != hipSuccess) {
+        gi_scene_destroy(s);
+        return hip_fail(e, "scene upload");
+    }
+    d.n_rnodes = (int32_t)h.rnodes.size();
+    d.n_ents = (int32_t)h.ents.size();
+    d.n_xnodes = (int32_t)h.xnodes.size();
+    d.n_xprims = (int32_t)h.xprims.size();
+    d.x_max_depth = h.x_max_depth;
+    *out = s;
+    return GI_OK;
+}
+
+void gi_scene_destroy(gi_scene* s) {
+    if (!s) return;
+    for (void* p : s->allocs) (void)hipFree(p);
+    delete s;
+}
+
+int gi_scene_get_info(const gi_scene* s, gi_scene_info* info) {
+    if (!s || !info) return fail(GI_ERR_ARG, "null argument");
+    info->n_entities = (int32_t)s->host.ents.size();
+    info->n_nodes = (int32_t)s->host.rnodes.size();
+    info->n_leaves = s->host.n_leaves;
+    info->max_depth = s->host.max_depth;
+    info->n_reachable = s->host.n_reachable;
+    info->n_dropped = s->host.n_dropped;
+    info->x_nodes = (int32_t)s->host.xnodes.size();
+    info->x_prims = (int32_t)s->host.xprims.size();
+    info->device_bytes = s->bytes;
+    return GI_OK;
+}
+
+int64_t gi_shard_tiles(int w, int h, int shard_count) {
+    if (w <= 0 || h <= 0 || shard_count < 1) return -1;
+    return shard_tiles(w, h, shard_count);
+}
+
+int gi_render_device(gi_scene* s, const gi_camera* cam, const double light[3], int w, int h, const gi_opts* o,
+                     double* d_rgb, uint8_t* d_rgb8, void* stream) {
+    int rc = check_opts(s, w, h, o);
+    if (rc) return rc;
+    if (!cam || !light) return fail(GI_ERR_ARG, "null camera or light");
+    if ((rc = bind_device(s))) return rc;
+    const hipError_t e = launch_render(s->dev, make_cam(*cam, w), v3(light[0], light[1], light[2]), w, h, 0, *o, d_rgb,
+                                       d_rgb8, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(e, "render launch");
+    return GI_OK;
+}
+
+int gi_render(gi_scene* s, const gi_camera* cam, const double light[3], int w, int h, const gi_opts* o, double* rgb,
+              uint8_t* rgb8, const volatile int* cancel, gi_tile_cb cb, void* user) {
+    int rc = check_opts(s, w, h, o);
+    if (rc) return rc;
+    if (!cam || !light) return fail(GI_ERR_ARG, "null camera or light");
+    if (o->shard_count != 1) return fail(GI_ERR_ARG, "gi_render renders whole frames; use gi_render_device to shard");
+    if ((rc = bind_device(s))) return rc;
+    // progressive bands of whole tile rows (the reference fills rows in order, raytracer.h:32-33,
+    // and the Viewer repaints what is done, viewer.h:18-21); cancel is polled between bands.
+    int band = o->band_rows > 0 ? o->band_rows : h;
+    band = ((band + GI_TILE - 1) / GI_TILE) * GI_TILE;
+    band = std::min(band, ((h + GI_TILE - 1) / GI_TILE) * GI_TILE);
+    const size_t band_px = (size_t)w * (size_t)band;
+    double* d_rgb = nullptr;
+    uint8_t* d_rgb8 = nullptr;
+    hipError_t e;
+    if ((e = hipMalloc((void**)&d_rgb, band_px * 3 * sizeof(double))) != hipSuccess) return hip_fail(e, "hipMalloc");
+    if ((e = hipMalloc((void**)&d_rgb8, band_px * 3)) != hipSuccess) {
+        (void)hipFree(d_rgb);
+        return hip_fail(e, "hipMalloc");
+    }
+    std::vector<double> scratch(rgb ? 0 : band_px * 3);
+    std::vector<uint8_t> scratch8(rgb8 ? 0 : band_px * 3);
+    const CamDev cd = make_cam(*cam, w);
+    const V3 L = v3(light[0], light[1], light[2]);
+    rc = GI_OK;
+    for (int y0 = 0; y0 < h; y0 += band) {
+        if (cancel && *cancel) { rc = fail(GI_ERR_CANCELLED, "cancelled"); break; }
+        const int rows = std::min(band, h - y0);
+        e = launch_render(s->dev, cd, L, w, rows, y0, *o, d_rgb, d_rgb8, nullptr);
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+        if (e != hipSuccess) { rc = hip_fail(e, "render"); break; }
+        double* hr = rgb ? rgb + (size_t)y0 * w * 3 : scratch.data();
+        uint8_t* hr8 = rgb8 ? rgb8 + (size_t)y0 * w * 3 : scratch8.data();
+        const size_t n = (size_t)w * rows * 3;
+        if ((rgb || cb) && (e = hipMemcpy(hr, d_rgb, n * sizeof(double), hipMemcpyDeviceToHost)) != hipSuccess) { rc = hip_fail(e, "copy back"); break; }
+        if ((rgb8 || cb) && (e = hipMemcpy(hr8, d_rgb8, n, hipMemcpyDeviceToHost)) != hipSuccess) { rc = hip_fail(e, "copy back"); break; }
+        if (cb) cb(user, y0, rows, hr8, hr);
+    }
+    (void)hipFree(d_rgb);
+    (void)hipFree(d_rgb8);
+    return rc;
+}
+
+int gi_unshard_device(int w, int h, int shard_count, const double* d_packed, const uint8_t* d_packed8, double* d_rgb,
+                      uint8_t* d_rgb8, void* stream) {
+    if (w <= 0 || h <= 0 || shard_count < 1) return fail(GI_ERR_ARG, "bad unshard arguments");
+    if ((d_rgb && !d_packed) || (d_rgb8 && !d_packed8)) return fail(GI_ERR_ARG, "missing packed input");
+    const hipError_t e = launch_unshard(w, h, shard_count, d_packed, d_packed8, d_rgb, d_rgb8, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(e, "unshard launch");
+    return GI_OK;
+}
+
+int gi_trace_ray(gi_scene* s, const double origin[3], const double dir[3], const double light[3], gi_hit* hit,
+                 double rgb[3]) {
+    if (!s || !origin || !dir || !light || !hit || !rgb) return fail(GI_ERR_ARG, "null argument");
+    int rc = bind_device(s);
+    if (rc) return rc;
+    int32_t* d_i = nullptr;
+    double* d_d = nullptr;
+    hipError_t e;
+    if ((e = hipMalloc((void**)&d_i, 4 * sizeof(int32_t))) != hipSuccess) return hip_fail(e, "hipMalloc");
+    if ((e = hipMalloc((void**)&d_d, 9 * sizeof(double))) != hipSuccess) { (void)hipFree(d_i); return hip_fail(e, "hipMalloc"); }
+    const V3 o = v3(origin[0], origin[1], origin[2]);
+    const V3 d = normalize(v3(dir[0], dir[1], dir[2]));   // Ray ctor (ray.h:6)
+    e = launch_trace_ray(s->dev, o, d, v3(light[0], light[1], light[2]), d_i, d_d, nullptr);
+    int32_t hi[3] = {-1, 0, 0};
+    double hd[9] = {0};
+    if (e == hipSuccess) e = hipMemcpy(hi, d_i, 3 * sizeof(int32_t), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(hd, d_d, 9 * sizeof(double), hipMemcpyDeviceToHost);
+    (void)hipFree(d_i);
+    (void)hipFree(d_d);
+    if (e != hipSuccess) return hip_fail(e, "trace_ray");
+    hit->entity = hi[0];
+    hit->u = hi[1];
+    hit->v = hi[2];
+    for (int k = 0; k < 3; ++k) { hit->point[k] = hd[k]; hit->normal[k] = hd[3 + k]; rgb[k] = hd[6 + k]; }
+    return GI_OK;
+}
+
+}  // extern "C"

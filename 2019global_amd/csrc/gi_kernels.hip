@@ -1,0 +1,540 @@
+// gi_kernels.hip — gfx950 (CDNA4) kernels for the per-pixel radiance path.
+//
+// Work decomposition: one wave64 renders one 8x8 pixel tile (lane = pixel), four waves per
+// 256-thread workgroup.  Tiles are dealt round-robin over shard ranks (tile t belongs to rank
+// t % shard_count), so the same kernel serves 1 GPU and N-GPU tile sharding.
+//
+// Mode R (reference semantics):
+//   The reference builds the full candidate list of Octree::intersect (octree.h:233-256, DFS over
+//   children 0..7, ExpBox node test) and keeps the LAST candidate whose intersect() succeeds
+//   (raytracer.h:53-74, A.1).  The last hit in DFS order is the first hit in reverse DFS order,
+//   so the kernel walks the same tree children 7..0 with a parent-pointer (stackless) traversal,
+//   scans each leaf list backwards, and stops at the first success.  Same node tests, same
+//   primitive math (gi_math.h), fewer of them.
+// Mode X (build-defined): per-pixel sample loop, closest-hit + shadow any-hit through
+//   the tight Mode X octree, front-to-back child order by ray-direction octant.
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off (bit-level parity needs no FMA
+// contraction; f64 div/sqrt are correctly rounded on gfx950).
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+
+#include "gi.h"
+#include "gi_scene.h"
+
+namespace gi {
+
+struct CamDev {
+    V3 pos, up, left, top_left;
+    double rx, ry;
+};
+
+namespace {
+
+constexpr int kTile = GI_TILE;
+constexpr int kWavesPerBlock = 4;
+
+// ---------------------------------------------------------------------------------------------
+// Mode R device pieces
+// ---------------------------------------------------------------------------------------------
+__device__ bool ent_hit(const DevScene& sc, const REnt& e, V3 o, V3 d, V3& P, V3& N, uint32_t& nprim) {
+    if (e.kind == K_IMP_SPHERE) {
+        ++nprim;
+        return sphere_hit(ld3(e.pos), e.radius, o, d, P, N);
+    }
+    if (e.kind == K_IMP_TRIANGLE) {
+        ++nprim;
+        return tri_hit(sc.tris[e.tri_first], o, d, P, N);
+    }
+    // ExpQuad::intersect (entities.h:596-620): nearest by <= over its triangles, ties -> later
+    bool flag = false;
+    double md = DBL_MAX;
+    V3 mi = v3(DBL_MAX, DBL_MAX, DBL_MAX), cn = v3(0, 0, 0);
+    for (int t = 0; t < e.tri_count; ++t) {
+        V3 p, n;
+        ++nprim;
+        if (tri_hit(sc.tris[e.tri_first + t], o, d, p, n)) {
+            const double dd = sq3(p - o);
+            if (dd <= md) { mi = p; cn = n; md = dd; }
+            flag = true;
+        }
+    }
+    P = mi;
+    N = cn;
+    return flag;
+}
+
+// getTextureCoord (entities.h:108-130, 277-303, 630-641) with the device's f64 acos/sin/cos
+__device__ void tex_coord(const DevScene& sc, const REnt& e, V3 ip, int32_t& x, int32_t& y) {
+    if (e.kind == K_IMP_SPHERE) {
+        const double r = e.radius;
+        const double unit_v = 2.0 * REF_PI * r / 320.0;
+        const V3 to = ip - ld3(e.pos);
+        const double cos_vert = dot(to, v3(0, 0, r)) / (r * r);
+        const double ang = acos(cos_vert);
+        y = x86_trunc((r * ang) / unit_v);
+        const double small_r = r * sin(ang);
+        const double cos_hori = dot(v3(to.x, to.y, 0), v3(0, small_r, 0)) / (small_r * small_r);
+        const double unit_h = 2.0 * REF_PI * small_r / 320.0;
+        x = x86_trunc(small_r * acos(cos_hori) / unit_h);
+    } else if (e.kind == K_IMP_TRIANGLE) {
+        const TriRec& t = sc.tris[e.tri_first];
+        const V3 p1 = ld3(t.p1), p2 = ld3(t.p2), p3 = ld3(t.p3);
+        const V3 p21 = p2 - p1, p31 = p3 - p1, p32 = p3 - p2, i1 = ip - p1;
+        const double p21l = gsqrt(sq3(p21));
+        const double i1l = gsqrt(sq3(i1));
+        const double theta = acos(dot(p21, i1) / (p21l * i1l));
+        const double ixl = i1l * sin(theta);
+        const double vl = gsqrt(sq3(0.5 * (p21 + p31)));
+        const double hl = gsqrt(sq3(0.5 * ((-p32) + (-p31))));
+        const double uv = vl / 160.0, uh = hl / 160.0;
+        y = x86_trunc(i1l / uh);
+        x = x86_trunc(ixl / uv);
+    } else {
+        const double uv = (double)e.width / 160.0, uh = (double)e.length / 160.0;
+        const V3 rv = ld3(e.qv0) - ld3(e.qv1);
+        const V3 i1 = ip - ld3(e.qv1);
+        const double i1l = gsqrt(sq3(i1));
+        const double theta = acos(dot(i1, rv) / ((double)e.width * i1l));
+        y = x86_trunc(i1l * sin(theta) / uh);
+        x = x86_trunc(i1l * cos(theta) / uv);
+    }
+}
+
+// Material::blinn_phong_texture (material.h:48-62)
+__device__ V3 shade_ref(const REnt& e, V3 dir, V3 light, V3 ip, V3 n, int32_t u, int32_t v) {
+    const V3 tc = texel(ld3(e.color), u, v);
+    const V3 tdc = tc * 0.5;
+    const V3 la = tc * e.shader[0];
+    const V3 ld = (smax(0.0, dot(n, normalize(light - ip))) * tdc) * e.shader[1];
+    const V3 bis = normalize(normalize(-dir) + normalize(light - ip));
+    const double p = pow(smax(0.0, dot(n, bis)), e.spec_pow);
+    const V3 ls = (p * v3(1, 1, 1)) * e.shader[2];
+    const V3 out = (la + ld) + ls;
+    return v3(smin(out.x, 1.0), smin(out.y, 1.0), smin(out.z, 1.0));
+}
+
+struct RResult {
+    int32_t ent;
+    V3 P, N;
+};
+
+// scan one leaf list backwards; true when the last hitting candidate of this leaf is found
+__device__ bool scan_leaf_rev(const DevScene& sc, const RNode& nd, V3 o, V3 d, RResult& r, uint32_t& nprim) {
+    for (int k = nd.ent_cnt - 1; k >= 0; --k) {
+        const int32_t e = sc.leaf_ents[nd.ent_off + k];
+        V3 P, N;
+        if (ent_hit(sc, sc.ents[e], o, d, P, N, nprim)) {
+            if (sq3(P - o) < DBL_MAX) {   // raytracer.h:63-65 with min_dist_square == DBL_MAX
+                r.ent = e;
+                r.P = P;
+                r.N = N;
+                return true;
+            }
+        }
+    }
+    return false;
+}
+
+// Last hitting candidate of Octree::intersect's list = first hit of the reverse DFS.
+__device__ void trace_mode_r(const DevScene& sc, V3 o, V3 d, RResult& r, uint32_t& nnode, uint32_t& nprim) {
+    r.ent = -1;
+    const RNode* nodes = sc.rnodes;
+    const RNode root = nodes[0];
+    if (root.child0 < 0) {
+        scan_leaf_rev(sc, root, o, d, r, nprim);
+        return;
+    }
+    int parent = 0, parent_child0 = root.child0, slot = 7;
+    for (;;) {
+        if (slot < 0) {
+            if (parent == 0) return;
+            const int pp = nodes[parent].parent;
+            const int pc0 = nodes[pp].child0;
+            slot = parent - pc0 - 1;
+            parent = pp;
+            parent_child0 = pc0;
+            continue;
+        }
+        const int c = parent_child0 + slot;
+        const RNode nd = nodes[c];
+        if (nd.ent_cnt == 0) { --slot; continue; }   // octree.h:241
+        ++nnode;
+        if (!box_hit(ld3(nd.mn), ld3(nd.mx), o, d)) { --slot; continue; }
+        if (nd.child0 < 0) {
+            if (scan_leaf_rev(sc, nd, o, d, r, nprim)) return;
+            --slot;
+            continue;
+        }
+        parent = c;
+        parent_child0 = nd.child0;
+        slot = 7;
+    }
+}
+
+__device__ __forceinline__ void wave_add_stats(unsigned long long* stats, uint64_t a, uint64_t b, uint64_t c, uint64_t px) {
+    for (int off = 32; off > 0; off >>= 1) {
+        a += __shfl_xor(a, off);
+        b += __shfl_xor(b, off);
+        c += __shfl_xor(c, off);
+        px += __shfl_xor(px, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(stats + GI_STAT_RAYS, (unsigned long long)a);
+        atomicAdd(stats + GI_STAT_NODES, (unsigned long long)b);
+        atomicAdd(stats + GI_STAT_PRIMS, (unsigned long long)c);
+        atomicAdd(stats + GI_STAT_PIXELS, (unsigned long long)px);
+    }
+}
+
+struct TileMap {
+    int w, h, tiles_x;
+    int y0;   // absolute row of the band's first row (progressive gi_render bands)
+    long long n_tiles, n_local;
+    int shard_count, shard_index;
+};
+
+// pixel of this lane; returns false when the lane has no pixel
+__device__ __forceinline__ bool lane_pixel(const TileMap& m, long long& out_idx, int& x, int& y) {
+    const int lane = threadIdx.x & 63;
+    const long long lt = (long long)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (lt >= m.n_local) return false;
+    const long long t = (long long)m.shard_index + lt * m.shard_count;
+    if (t >= m.n_tiles) { out_idx = -1; return false; }
+    const int ty = (int)(t / m.tiles_x), tx = (int)(t % m.tiles_x);
+    x = tx * kTile + (lane & 7);
+    y = ty * kTile + (lane >> 3);
+    if (m.shard_count == 1) out_idx = (long long)y * m.w + x;
+    else out_idx = lt * (kTile * kTile) + lane;
+    return x < m.w && y < m.h;
+}
+
+__device__ __forceinline__ V3 primary_dir(const CamDev& c, double fx, double fy) {
+    // raytracer.h:41: top_left - left*x*res.x - up*y*res.y
+    return (c.top_left - (c.left * fx) * c.rx) - (c.up * fy) * c.ry;
+}
+
+template <bool STATS>
+__global__ __launch_bounds__(256) void k_mode_r(DevScene sc, CamDev cam, V3 light, TileMap m, double* rgb,
+                                                 uint8_t* rgb8, unsigned long long* stats) {
+    long long idx = -1;
+    int x = 0, y = 0;
+    const bool ok = lane_pixel(m, idx, x, y);
+    y += m.y0;
+    uint32_t nnode = 0, nprim = 0;
+    if (ok) {
+        const V3 o = cam.pos;
+        const V3 d = normalize(primary_dir(cam, (double)x, (double)y));   // Ray ctor (ray.h:6)
+        RResult r;
+        trace_mode_r(sc, o, d, r, nnode, nprim);
+        double c0 = 0, c1 = 0, c2 = 0;
+        if (r.ent >= 0) {
+            const REnt e = sc.ents[r.ent];
+            int32_t u, v;
+            tex_coord(sc, e, r.P, u, v);
+            const V3 col = shade_ref(e, d, light, r.P, r.N, u, v);
+            c0 = col.x; c1 = col.y; c2 = col.z;
+        }
+        if (rgb) { rgb[3 * idx] = c0; rgb[3 * idx + 1] = c1; rgb[3 * idx + 2] = c2; }
+        if (rgb8) quantize(c0, c1, c2, rgb8 + 3 * idx);
+    } else if (idx >= 0 && m.shard_count > 1) {   // padding lanes of a packed tile
+        if (rgb) { rgb[3 * idx] = 0; rgb[3 * idx + 1] = 0; rgb[3 * idx + 2] = 0; }
+        if (rgb8) { rgb8[3 * idx] = 0; rgb8[3 * idx + 1] = 0; rgb8[3 * idx + 2] = 0; }
+    }
+    if (STATS) {
+        const long long lt = (long long)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+        if (lt < m.n_local) wave_add_stats(stats, ok ? 1 : 0, nnode, nprim, ok ? 1 : 0);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Mode X
+// ---------------------------------------------------------------------------------------------
+constexpr int kXStack = 128;
+
+__device__ __forceinline__ double x_prim_t(const XPrim& p, V3 o, V3 d, double tmin) {
+    if (p.kind == 0) {   // Möller–Trumbore, two-sided
+        const V3 e1 = ld3(p.b), e2 = ld3(p.c);
+        const V3 pv = cross(d, e2);
+        const double det = dot(e1, pv);
+        if (det == 0.0) return INFINITY;
+        const double inv = 1.0 / det;
+        const V3 tv = o - ld3(p.a);
+        const double u = dot(tv, pv) * inv;
+        if (u < 0.0 || u > 1.0) return INFINITY;
+        const V3 qv = cross(tv, e1);
+        const double v = dot(d, qv) * inv;
+        if (v < 0.0 || u + v > 1.0) return INFINITY;
+        const double t = dot(e2, qv) * inv;
+        return (t > tmin) ? t : INFINITY;
+    }
+    const V3 oc = o - ld3(p.a);
+    const double b = dot(oc, d);
+    const double r = p.b[0];
+    const double c2 = dot(oc, oc) - r * r;
+    const double disc = b * b - c2;
+    if (disc < 0.0) return INFINITY;
+    const double sq = gsqrt(disc);
+    double t = -b - sq;
+    if (t > tmin) return t;
+    t = -b + sq;
+    return (t > tmin) ? t : INFINITY;
+}
+
+__device__ __forceinline__ double slab_enter(const XNode& n, V3 o, V3 inv, double tmax) {
+    const double tx0 = (n.mn[0] - o.x) * inv.x, tx1 = (n.mx[0] - o.x) * inv.x;
+    const double ty0 = (n.mn[1] - o.y) * inv.y, ty1 = (n.mx[1] - o.y) * inv.y;
+    const double tz0 = (n.mn[2] - o.z) * inv.z, tz1 = (n.mx[2] - o.z) * inv.z;
+    const double tn = fmax(fmax(fmin(tx0, tx1), fmin(ty0, ty1)), fmax(fmin(tz0, tz1), 0.0));
+    const double tf = fmin(fmin(fmax(tx0, tx1), fmax(ty0, ty1)), fmin(fmax(tz0, tz1), tmax));
+    return (tn <= tf) ? tn : INFINITY;
+}
+
+// closest hit (any_hit=false) or occlusion test before tmax (any_hit=true).  Returns prim index.
+template <bool ANY>
+__device__ int x_trace(const DevScene& sc, V3 o, V3 d, double tmax, double& tbest, uint32_t& nnode, uint32_t& nprim) {
+    const V3 inv = v3(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+    const int dmask = (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
+    int stack[kXStack];
+    int sp = 0;
+    stack[sp++] = 0;
+    int best = -1;
+    tbest = tmax;
+    while (sp > 0) {
+        const int ni = stack[--sp];
+        const XNode nd = sc.xnodes[ni];
+        ++nnode;
+        const double te = slab_enter(nd, o, inv, tbest);
+        if (!(te <= tbest)) continue;
+        if (nd.child_mask == 0) {
+            for (int k = 0; k < nd.prim_cnt; ++k) {
+                const int pi = sc.xprim_idx[nd.prim_off + k];
+                ++nprim;
+                const double t = x_prim_t(sc.xprims[pi], o, d, MX_TMIN);
+                if (ANY) {
+                    if (t < tmax) { tbest = t; return pi; }
+                } else if (t < tbest || (t == tbest && pi < best)) {
+                    tbest = t;
+                    best = pi;
+                }
+            }
+            continue;
+        }
+        // push existing children far-to-near so the nearest (octant dmask first) pops first
+        for (int k = 7; k >= 0; --k) {
+            const int c = k ^ dmask;
+            if (!((nd.child_mask >> c) & 1)) continue;
+            const int rank = __popc(nd.child_mask & ((1 << c) - 1));
+            if (sp < kXStack) stack[sp++] = nd.child_base + rank;
+        }
+    }
+    return best;
+}
+
+__device__ void x_texcoord(const DevScene& sc, const REnt& e, V3 ip, int32_t& x, int32_t& y) {
+    if (e.kind == K_IMP_SPHERE) {
+        const double r = e.radius;
+        const double unit_v = 2.0 * REF_PI * r / 320.0;
+        const V3 to = ip - ld3(e.pos);
+        const double cv = dot(to, v3(0, 0, r)) / (r * r);
+        y = x86_trunc((r * mx_acos(cv)) / unit_v);
+        const double small_r = r * mx_sin_acos(cv);
+        const double ch = dot(v3(to.x, to.y, 0), v3(0, small_r, 0)) / (small_r * small_r);
+        const double unit_h = 2.0 * REF_PI * small_r / 320.0;
+        x = x86_trunc(small_r * mx_acos(ch) / unit_h);
+    } else if (e.kind == K_IMP_TRIANGLE) {
+        const TriRec& t = sc.tris[e.tri_first];
+        const V3 p1 = ld3(t.p1), p2 = ld3(t.p2), p3 = ld3(t.p3);
+        const V3 p21 = p2 - p1, p31 = p3 - p1, p32 = p3 - p2, i1 = ip - p1;
+        const double p21l = gsqrt(sq3(p21)), i1l = gsqrt(sq3(i1));
+        const double c = dot(p21, i1) / (p21l * i1l);
+        const double ixl = i1l * mx_sin_acos(c);
+        const double vl = gsqrt(sq3(0.5 * (p21 + p31)));
+        const double hl = gsqrt(sq3(0.5 * ((-p32) + (-p31))));
+        y = x86_trunc(i1l / (hl / 160.0));
+        x = x86_trunc(ixl / (vl / 160.0));
+    } else {
+        const double uv = (double)e.width / 160.0, uh = (double)e.length / 160.0;
+        const V3 rv = ld3(e.qv0) - ld3(e.qv1), i1 = ip - ld3(e.qv1);
+        const double i1l = gsqrt(sq3(i1));
+        const double c = dot(i1, rv) / ((double)e.width * i1l);
+        y = x86_trunc(i1l * mx_sin_acos(c) / uh);
+        x = x86_trunc(i1l * mx_cos_acos(c) / uv);
+    }
+}
+
+template <bool STATS>
+__global__ __launch_bounds__(256) void k_mode_x(DevScene sc, CamDev cam, V3 light, TileMap m, int spp, int depth,
+                                                 uint64_t seed, double* rgb, uint8_t* rgb8,
+                                                 unsigned long long* stats) {
+    long long idx = -1;
+    int x = 0, y = 0;
+    const bool ok = lane_pixel(m, idx, x, y);
+    y += m.y0;
+    uint32_t nnode = 0, nprim = 0, nrays = 0;
+    if (ok) {
+        const uint64_t pix = (uint64_t)y * (uint64_t)m.w + (uint64_t)x;
+        const uint64_t key = mx_key(seed, pix);
+        double s0 = 0, s1 = 0, s2 = 0;
+        for (int smp = 0; smp < spp; ++smp) {
+            double jx = 0.0, jy = 0.0;
+            if (spp > 1) { jx = mx_u01k(key, smp, 0xFFFF, 0); jy = mx_u01k(key, smp, 0xFFFF, 1); }
+            V3 o = cam.pos;
+            V3 d = normalize(primary_dir(cam, (double)x + jx, (double)y + jy));
+            V3 L = v3(0, 0, 0), T = v3(1, 1, 1);
+            for (int b = 0; b < depth; ++b) {
+                double t;
+                const int pi = x_trace<false>(sc, o, d, INFINITY, t, nnode, nprim);
+                ++nrays;
+                if (pi < 0) break;
+                const XPrim p = sc.xprims[pi];
+                const REnt e = sc.ents[p.ent];
+                const V3 P = o + t * d;
+                V3 N = p.kind == 0 ? ld3(p.n) : normalize(P - ld3(p.a));
+                if (!(dot(d, N) < 0)) N = -N;
+                int32_t tu, tv;
+                x_texcoord(sc, e, P, tu, tv);
+                const V3 tc = texel(ld3(e.color), tu, tv);
+                const V3 lv = light - P;
+                const double ldist = gsqrt(dot(lv, lv));
+                const V3 Ld = normalize(lv);
+                double ts;
+                const bool vis = x_trace<true>(sc, P, Ld, ldist, ts, nnode, nprim) < 0;
+                ++nrays;
+                const V3 la = tc * e.shader[0];
+                V3 loc = la;
+                if (vis) {
+                    const V3 ldf = (smax(0.0, dot(N, Ld)) * (tc * 0.5)) * e.shader[1];
+                    const V3 bis = normalize(normalize(-d) + Ld);
+                    const double sp = mx_powi(smax(0.0, dot(N, bis)), (int)e.spec_pow);
+                    const V3 ls = v3(sp, sp, sp) * e.shader[2];
+                    loc = (la + ldf) + ls;
+                }
+                loc = v3(smin(loc.x, 1.0), smin(loc.y, 1.0), smin(loc.z, 1.0));
+                L = L + vmul(T, loc);
+                if (b == depth - 1) break;
+                T = vmul(T, tc * 0.5);
+                if (T.x == 0.0 && T.y == 0.0 && T.z == 0.0) break;
+                double sx = 0, sy = 0, r2 = 0;
+                for (int k = 0; k < 16; ++k) {
+                    const double ax = 2.0 * mx_u01k(key, smp, b, 2 + 2 * k) - 1.0;
+                    const double ay = 2.0 * mx_u01k(key, smp, b, 3 + 2 * k) - 1.0;
+                    const double q = ax * ax + ay * ay;
+                    if (q < 1.0) { sx = ax; sy = ay; r2 = q; break; }
+                }
+                const double sz = gsqrt(1.0 - r2);
+                const double sg = N.z >= 0.0 ? 1.0 : -1.0;
+                const double aa = -1.0 / (sg + N.z);
+                const double bb = N.x * N.y * aa;
+                const V3 t1 = v3(1.0 + sg * N.x * N.x * aa, sg * bb, -sg * N.x);
+                const V3 t2 = v3(bb, sg + N.y * N.y * aa, -N.y);
+                d = normalize((t1 * sx + t2 * sy) + N * sz);
+                o = P;
+            }
+            s0 = s0 + L.x; s1 = s1 + L.y; s2 = s2 + L.z;
+        }
+        const double c0 = smin(s0 / (double)spp, 1.0), c1 = smin(s1 / (double)spp, 1.0), c2 = smin(s2 / (double)spp, 1.0);
+        if (rgb) { rgb[3 * idx] = c0; rgb[3 * idx + 1] = c1; rgb[3 * idx + 2] = c2; }
+        if (rgb8) quantize(c0, c1, c2, rgb8 + 3 * idx);
+    } else if (idx >= 0 && m.shard_count > 1) {
+        if (rgb) { rgb[3 * idx] = 0; rgb[3 * idx + 1] = 0; rgb[3 * idx + 2] = 0; }
+        if (rgb8) { rgb8[3 * idx] = 0; rgb8[3 * idx + 1] = 0; rgb8[3 * idx + 2] = 0; }
+    }
+    if (STATS) {
+        const long long lt = (long long)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+        if (lt < m.n_local) wave_add_stats(stats, nrays, nnode, nprim, ok ? 1 : 0);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// unshard: packed per-rank tiles -> row-major frame
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_unshard(TileMap m, const double* packed, const uint8_t* packed8, double* rgb,
+                                                  uint8_t* rgb8) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;   // global pixel slot in tile order
+    const long long t = i / (kTile * kTile);
+    if (t >= m.n_tiles) return;
+    const int lane = (int)(i % (kTile * kTile));
+    const int ty = (int)(t / m.tiles_x), tx = (int)(t % m.tiles_x);
+    const int x = tx * kTile + (lane & 7), y = ty * kTile + (lane >> 3);
+    if (x >= m.w || y >= m.h) return;
+    const long long r = t % m.shard_count, lt = t / m.shard_count;
+    const long long src = (r * m.n_local + lt) * (kTile * kTile) + lane;
+    const long long dst = (long long)y * m.w + x;
+    if (rgb) { rgb[3 * dst] = packed[3 * src]; rgb[3 * dst + 1] = packed[3 * src + 1]; rgb[3 * dst + 2] = packed[3 * src + 2]; }
+    if (rgb8) { rgb8[3 * dst] = packed8[3 * src]; rgb8[3 * dst + 1] = packed8[3 * src + 1]; rgb8[3 * dst + 2] = packed8[3 * src + 2]; }
+}
+
+__global__ void k_trace_ray(DevScene sc, V3 o, V3 d, V3 light, int32_t* out_i, double* out_d) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    RResult r;
+    uint32_t nn = 0, np = 0;
+    trace_mode_r(sc, o, d, r, nn, np);
+    out_i[0] = r.ent;
+    out_i[1] = out_i[2] = 0;
+    for (int k = 0; k < 9; ++k) out_d[k] = 0;
+    if (r.ent >= 0) {
+        const REnt e = sc.ents[r.ent];
+        int32_t u, v;
+        tex_coord(sc, e, r.P, u, v);
+        const V3 col = shade_ref(e, d, light, r.P, r.N, u, v);
+        out_i[1] = u; out_i[2] = v;
+        out_d[0] = r.P.x; out_d[1] = r.P.y; out_d[2] = r.P.z;
+        out_d[3] = r.N.x; out_d[4] = r.N.y; out_d[5] = r.N.z;
+        out_d[6] = col.x; out_d[7] = col.y; out_d[8] = col.z;
+    }
+}
+
+TileMap make_map(int w, int h, int shard_count, int shard_index, int y0 = 0) {
+    TileMap m;
+    m.w = w;
+    m.h = h;
+    m.y0 = y0;
+    m.tiles_x = (w + kTile - 1) / kTile;
+    const long long tiles_y = (h + kTile - 1) / kTile;
+    m.n_tiles = (long long)m.tiles_x * tiles_y;
+    m.shard_count = shard_count;
+    m.shard_index = shard_index;
+    m.n_local = (m.n_tiles + shard_count - 1) / shard_count;
+    return m;
+}
+
+}  // namespace
+
+long long shard_tiles(int w, int h, int shard_count) { return make_map(w, h, shard_count, 0).n_local; }
+
+hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w, int h, int y0, const gi_opts& o,
+                         double* rgb, uint8_t* rgb8, hipStream_t stream) {
+    const TileMap m = make_map(w, h, o.shard_count, o.shard_index, y0);
+    if (m.n_local == 0) return hipSuccess;
+    const dim3 grid((unsigned)((m.n_local + kWavesPerBlock - 1) / kWavesPerBlock)), block(64 * kWavesPerBlock);
+    unsigned long long* st = reinterpret_cast<unsigned long long*>(o.stats);
+    const bool stats = (o.flags & GI_FLAG_STATS) && st;
+    if (o.mode == GI_MODE_R) {
+        if (stats) hipLaunchKernelGGL(k_mode_r<true>, grid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st);
+        else hipLaunchKernelGGL(k_mode_r<false>, grid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st);
+    } else {
+        if (stats)
+            hipLaunchKernelGGL(k_mode_x<true>, grid, block, 0, stream, sc, cam, light, m, o.spp, o.depth, o.seed, rgb, rgb8, st);
+        else
+            hipLaunchKernelGGL(k_mode_x<false>, grid, block, 0, stream, sc, cam, light, m, o.spp, o.depth, o.seed, rgb, rgb8, st);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_unshard(int w, int h, int shard_count, const double* packed, const uint8_t* packed8, double* rgb,
+                          uint8_t* rgb8, hipStream_t stream) {
+    const TileMap m = make_map(w, h, shard_count, 0);
+    const long long n = m.n_tiles * kTile * kTile;
+    hipLaunchKernelGGL(k_unshard, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, m, packed, packed8, rgb, rgb8);
+    return hipGetLastError();
+}
+
+hipError_t launch_trace_ray(const DevScene& sc, V3 o, V3 d, V3 light, int32_t* out_i, double* out_d, hipStream_t stream) {
+    hipLaunchKernelGGL(k_trace_ray, dim3(1), dim3(64), 0, stream, sc, o, d, light, out_i, out_d);
+    return hipGetLastError();
+}
+
+}  // namespace gi

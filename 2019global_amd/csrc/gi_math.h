@@ -1,0 +1,235 @@
+// gi_math.h — fp64/fp32 vector math with the reference's exact operation order, shared by the host
+// scene builder (g++) and the gfx950 kernels (hipcc).  Both sides compile with -ffp-contract=off,
+// so every expression rounds exactly like the reference's glm 0.9.8.2 code:
+//   dot       (x*x' + y*y') + z*z'                 glm/detail/func_geometric.inl:54-61
+//   cross     (y*z'-y'*z, z*x'-z'*x, x*y'-x'*y)    func_geometric.inl:74-85
+//   normalize v * (1 / sqrt(dot(v,v)))              func_geometric.inl:88-96, func_exponential.inl:128-133
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define GI_HD __host__ __device__ __forceinline__
+#else
+#define GI_HD inline
+#include <cmath>
+#endif
+
+namespace gi {
+
+struct V3 {
+    double x, y, z;
+};
+GI_HD V3 v3(double x, double y, double z) { V3 r; r.x = x; r.y = y; r.z = z; return r; }
+GI_HD V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+GI_HD V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+GI_HD V3 operator-(V3 a) { return v3(-a.x, -a.y, -a.z); }
+GI_HD V3 operator*(V3 a, double s) { return v3(a.x * s, a.y * s, a.z * s); }
+GI_HD V3 operator*(double s, V3 a) { return v3(s * a.x, s * a.y, s * a.z); }
+GI_HD V3 vmul(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
+GI_HD double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+GI_HD V3 cross(V3 x, V3 y) { return v3(x.y * y.z - y.y * x.z, x.z * y.x - y.z * x.x, x.x * y.y - y.x * x.y); }
+GI_HD double gsqrt(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_sqrt(x);   // correctly rounded f64 sqrt on gfx950
+#else
+    return std::sqrt(x);
+#endif
+}
+GI_HD V3 normalize(V3 v) { return v * (1.0 / gsqrt(dot(v, v))); }
+GI_HD double length(V3 v) { return gsqrt(dot(v, v)); }
+// pow(v.x,2)+pow(v.y,2)+pow(v.z,2) as the reference writes it (g++ folds pow(x,2) to x*x)
+GI_HD double sq3(V3 v) { return v.x * v.x + v.y * v.y + v.z * v.z; }
+GI_HD double smin(double a, double b) { return (b < a) ? b : a; }   // std::min
+GI_HD double smax(double a, double b) { return (a < b) ? b : a; }   // std::max
+GI_HD float sminf(float a, float b) { return (b < a) ? b : a; }
+GI_HD float fabsf_(float a) { return a < 0.0f ? -a : (a == 0.0f ? 0.0f : a); }
+
+// x86-64 cvttsd2si semantics for the reference's int() casts: NaN/out of range -> INT_MIN (A.9).
+// (gfx950's v_cvt_i32_f64 clamps instead, so this is explicit.)
+GI_HD int32_t x86_trunc(double d) {
+    if (!(d > -2147483649.0 && d < 2147483648.0)) return (int32_t)0x80000000u;
+    return (int32_t)d;
+}
+
+const double REF_PI = 3.1415926535;   // entities.h:16
+
+// ImpTriangle derived members (entities.h:139-148), member-initialisation order.
+struct TriRec {            // 144 bytes
+    double p1[3], p2[3], p3[3];
+    double n[3];           // normalize(cross(edge1, edge2))
+    double pos[3];         // 0.5*(0.5*(p1+p2)+p3)
+    float e1f[3], e2f[3];  // glm::vec3(edge1/edge2) as cast into the fp32 mat3
+};
+
+GI_HD V3 ld3(const double* p) { return v3(p[0], p[1], p[2]); }
+GI_HD void st3(double* p, V3 v) { p[0] = v.x; p[1] = v.y; p[2] = v.z; }
+
+GI_HD void make_tri(V3 p1, V3 p2, V3 p3, TriRec& t) {
+    st3(t.p1, p1); st3(t.p2, p2); st3(t.p3, p3);
+    const V3 e1 = p2 - p1, e2 = p3 - p1;
+    st3(t.n, normalize(cross(e1, e2)));
+    st3(t.pos, 0.5 * (0.5 * (p1 + p2) + p3));
+    t.e1f[0] = (float)e1.x; t.e1f[1] = (float)e1.y; t.e1f[2] = (float)e1.z;
+    t.e2f[0] = (float)e2.x; t.e2f[1] = (float)e2.y; t.e2f[2] = (float)e2.z;
+}
+
+// ImpTriangle::intersect (entities.h:150-249).  fp32 solve: glm::mat3(e1, e2, -dir) transposed,
+// glm's cofactor inverse (func_matrix.inl:272-294) and vec3 * mat3 (type_mat3x3.inl:437-443);
+// only sol.z is used.  No t > 0 test (A.3).
+GI_HD bool tri_hit(V3 p1, V3 p2, V3 p3, V3 n, V3 pos, const float* e1f, const float* e2f, V3 o, V3 d,
+                   V3& P, V3& N) {
+    if (dot(n, d) == 0) return false;
+    const float m00 = e1f[0], m01 = e2f[0], m02 = (float)(-d.x);
+    const float m10 = e1f[1], m11 = e2f[1], m12 = (float)(-d.y);
+    const float m20 = e1f[2], m21 = e2f[2], m22 = (float)(-d.z);
+    const float det = m00 * (m11 * m22 - m21 * m12) - m10 * (m01 * m22 - m21 * m02) + m20 * (m01 * m12 - m11 * m02);
+    const float ood = 1.0f / det;
+    const float i20 = (m10 * m21 - m20 * m11) * ood;
+    const float i21 = (-(m00 * m21 - m20 * m01)) * ood;
+    const float i22 = (m00 * m11 - m10 * m01) * ood;
+    const V3 right = o - pos;
+    const float solz = i20 * (float)right.x + i21 * (float)right.y + i22 * (float)right.z;
+    const V3 point = o + (double)solz * d;
+    const V3 d1 = normalize(cross(p1 - point, p2 - point));
+    const V3 d2 = normalize(cross(p2 - point, p3 - point));
+    const V3 d3 = normalize(cross(p3 - point, p1 - point));
+    // glm::length(d_k) < 1e-3 branches (:201-230): a normalised vector has length ~1, inf or NaN;
+    // test the squared length first so the sqrt only runs when the branch can fire.
+    const double q1 = dot(d1, d1), q2 = dot(d2, d2), q3 = dot(d3, d3);
+    const bool short_d = (q1 < 1e-5 && gsqrt(q1) < 1.0e-3) || (q2 < 1e-5 && gsqrt(q2) < 1.0e-3) ||
+                         (q3 < 1e-5 && gsqrt(q3) < 1.0e-3);
+    const bool inside = sq3(d1 - d2) < 1.0e-3 && sq3(d2 - d3) < 1.0e-3;   // :232-237
+    if (!(short_d || inside)) return false;
+    P = point;
+    N = dot(d, n) < 0 ? n : -n;
+    return true;
+}
+
+GI_HD bool tri_hit(const TriRec& t, V3 o, V3 d, V3& P, V3& N) {
+    return tri_hit(ld3(t.p1), ld3(t.p2), ld3(t.p3), ld3(t.n), ld3(t.pos), t.e1f, t.e2f, o, d, P, N);
+}
+
+// A triangle built on the fly from three corners (ExpBox faces, entities.h:319-324).
+GI_HD bool tri_hit_corners(V3 p1, V3 p2, V3 p3, V3 o, V3 d) {
+    const V3 e1 = p2 - p1, e2 = p3 - p1;
+    const V3 n = normalize(cross(e1, e2));
+    const V3 pos = 0.5 * (0.5 * (p1 + p2) + p3);
+    const float e1f[3] = {(float)e1.x, (float)e1.y, (float)e1.z};
+    const float e2f[3] = {(float)e2.x, (float)e2.y, (float)e2.z};
+    V3 P, N;
+    return tri_hit(p1, p2, p3, n, pos, e1f, e2f, o, d, P, N);
+}
+
+// ExpBox(min,max).intersect (entities.h:379-440) as Octree::Node::intersect uses it: true iff any
+// of the 12 face triangles hits; each ExpRectangle(p1,p2,p3) face is t1=(p1,p2,p3) then
+// t2=(p1,p2,p4) with p4 = -p3 (default member init runs before pos is set, A.4).
+GI_HD bool box_hit(V3 mn, V3 mx, V3 o, V3 d) {
+    const V3 dlb = mn, drb = v3(mx.x, mn.y, mn.z), dlt = v3(mn.x, mx.y, mn.z), drt = v3(mx.x, mx.y, mn.z);
+    const V3 ulb = v3(mn.x, mn.y, mx.z), urb = v3(mx.x, mn.y, mx.z), ult = v3(mn.x, mx.y, mx.z), urt = mx;
+    // faces in ExpBox::faces order (entities.h:400-405); || short-circuits like an OR of bools
+    return tri_hit_corners(dlb, urb, ulb, o, d) || tri_hit_corners(dlb, urb, -ulb, o, d) ||
+           tri_hit_corners(dlb, ult, dlt, o, d) || tri_hit_corners(dlb, ult, -dlt, o, d) ||
+           tri_hit_corners(dlb, drt, dlt, o, d) || tri_hit_corners(dlb, drt, -dlt, o, d) ||
+           tri_hit_corners(urt, ulb, ult, o, d) || tri_hit_corners(urt, ulb, -ult, o, d) ||
+           tri_hit_corners(urt, drb, drt, o, d) || tri_hit_corners(urt, drb, -drt, o, d) ||
+           tri_hit_corners(urt, dlt, drt, o, d) || tri_hit_corners(urt, dlt, -drt, o, d);
+}
+
+// ImpSphere::intersect (entities.h:53-96): the quadratic in the dominant-axis parameterisation
+// with its fp32/fp64 mix; a line test on |root| (A.2).
+GI_HD bool sphere_hit(V3 pos, float radius, V3 o, V3 d, V3& P, V3& N) {
+    const V3 np = pos - o;
+    float a1 = 1, a2 = 1, a3 = 1;
+    if (d.x != 0) { a2 = (float)(d.y / d.x); a3 = (float)(d.z / d.x); }
+    else if (d.y != 0) { a1 = (float)(d.x / d.y); a3 = (float)(d.z / d.y); }
+    else if (d.z != 0) { a2 = (float)(d.y / d.z); a1 = (float)(d.x / d.z); }
+    else return false;
+    const double A1 = a1, A2 = a2, A3 = a3;
+    const float a = (float)(A1 * A1 + A2 * A2 + A3 * A3);
+    const float b = (float)(-2.0 * (np.x * A1 + np.y * A2 + np.z * A3));
+    const double R = radius;
+    const float c = (float)(np.x * np.x + np.y * np.y + np.z * np.z - R * R);
+    const double B = b;
+    const float ac4 = (4.0f * a) * c;
+    const double disc = B * B - (double)ac4;
+    if (disc < 0) return false;
+    const double s = gsqrt(disc);
+    const float a2f = 2.0f * a;
+    const float v1 = (float)((-B + s) / (double)a2f);
+    const float v2 = (float)((-B - s) / (double)a2f);
+    const float base = sminf(fabsf_(v1), fabsf_(v2));
+    const V3 ip = v3((double)(base * a1), (double)(base * a2), (double)(base * a3)) + o;
+    P = ip;
+    N = normalize(ip - pos);
+    return true;
+}
+
+// ---- Mode X (build-defined) ----------------------------------------------------
+// Only + - * / sqrt and comparisons, so host oracle and device agree bit for bit.
+const double MX_TMIN = 1e-7;
+const double MX_PI = 0x1.921fb54442d18p+1, MX_PIO2 = 0x1.921fb54442d18p+0;
+
+GI_HD uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+// counter-based uniform in [0,1): key (seed, pixel, sample, bounce, dim)
+GI_HD uint64_t mx_key(uint64_t seed, uint64_t pixel) { return mix64(seed + 0x9E3779B97F4A7C15ULL * (pixel + 1)); }
+GI_HD double mx_u01k(uint64_t key, uint32_t sample, uint32_t bounce, uint32_t dim) {
+    const uint64_t k = mix64(key ^ (((uint64_t)sample << 32) | ((uint64_t)(bounce & 0xFFFF) << 16) | (uint64_t)(dim & 0xFFFF)));
+    return (double)(k >> 11) * 0x1.0p-53;
+}
+
+GI_HD double mx_asin_small(double y) {   // |y| <= 0.5: 30-term Taylor series, Horner
+    const double C[30] = {
+        0x1.0000000000000p+0, 0x1.5555555555555p-3, 0x1.3333333333333p-4, 0x1.6db6db6db6db7p-5,
+        0x1.f1c71c71c71c7p-6, 0x1.6e8ba2e8ba2e9p-6, 0x1.1c4ec4ec4ec4fp-6, 0x1.c99999999999ap-7,
+        0x1.7a87878787878p-7, 0x1.3fde50d79435ep-7, 0x1.12ef3cf3cf3cfp-7, 0x1.df3bd37a6f4dfp-8,
+        0x1.a6863d70a3d71p-8, 0x1.782dda12f684cp-8, 0x1.51ba308d3dcb1p-8, 0x1.31683bdef7bdfp-8,
+        0x1.15ee9d45d1746p-8, 0x1.fcaf8fb6db6dbp-9, 0x1.d3d2a8e0dd67dp-9, 0x1.b026f57b13b14p-9,
+        0x1.90cb77f60c7cep-9, 0x1.750de64d7d05fp-9, 0x1.5c5f56efaaaabp-9, 0x1.464c0950f7d47p-9,
+        0x1.3275586c5f2f0p-9, 0x1.208d3570ae5a6p-9, 0x1.1052bc5fa960ap-9, 0x1.018f963c229bfp-9,
+        0x1.e82be60d9127ep-10, 0x1.cf7dea5b6e830p-10};
+    const double z = y * y;
+    double p = C[29];
+    for (int k = 28; k >= 0; --k) p = p * z + C[k];
+    return y * p;
+}
+GI_HD double mx_acos(double x) {
+    if (!(x >= -1.0 && x <= 1.0)) return __builtin_nan("");
+    if (x >= -0.5 && x <= 0.5) return MX_PIO2 - mx_asin_small(x);
+    if (x > 0.5) return 2.0 * mx_asin_small(gsqrt((1.0 - x) * 0.5));
+    return MX_PI - 2.0 * mx_asin_small(gsqrt((1.0 + x) * 0.5));
+}
+GI_HD double mx_sin_acos(double c) { return gsqrt(1.0 - c * c); }
+GI_HD double mx_cos_acos(double c) { return (c >= -1.0 && c <= 1.0) ? c : __builtin_nan(""); }
+GI_HD double mx_powi(double x, int p) {
+    double r = 1.0, b = x;
+    while (p) {
+        if (p & 1) r = r * b;
+        b = b * b;
+        p >>= 1;
+    }
+    return r;
+}
+
+// Texture (material.h:65-106): 32x32 int checker, colour truncated to int (A.7); a negative
+// index (out-of-bounds UB in the reference, A.9) wraps into [0,32).
+GI_HD V3 texel(V3 color, int32_t u, int32_t v) {
+    int i = u % 32, j = v % 32;
+    if (i < 0) i += 32;
+    if (j < 0) j += 32;
+    if ((i <= 16 && j <= 16) || (i > 16 && j > 16)) return v3(1, 1, 1);
+    return v3((double)x86_trunc(color.x), (double)x86_trunc(color.y), (double)x86_trunc(color.z));
+}
+
+// Image::setPixel quantisation (image.h:14-16): (int)(255*c); an out-of-range channel makes the
+// QColor invalid, which QImage stores as black.
+GI_HD void quantize(double r, double g, double b, uint8_t* q) {
+    const int32_t R = x86_trunc(255 * r), G = x86_trunc(255 * g), B = x86_trunc(255 * b);
+    if (R < 0 || R > 255 || G < 0 || G > 255 || B < 0 || B > 255) { q[0] = q[1] = q[2] = 0; return; }
+    q[0] = (uint8_t)R; q[1] = (uint8_t)G; q[2] = (uint8_t)B;
+}
+
+}  // namespace gi

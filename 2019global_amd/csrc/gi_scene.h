@@ -1,0 +1,86 @@
+// gi_scene.h — device-resident scene layout (HBM) and the host-side builder interface.
+//
+// Mode R keeps the reference octree exactly (octree.h:12-163, including SURVEY A.4-A.6, A.14):
+//   RNode[]   64 B/node: AABB (fp64) + child0 / parent / leaf list range.  Children of a node are
+//             8 consecutive records in octant order 0..7 (octree.h:195-209).
+//   leaf_ents int32 entity indices, each leaf's list in push order.
+//   REnt[]    entity records (kind, material, sphere/quad parameters) + TriRec[] triangles.
+// Mode X uses its own tight octree over primitives (XNode[], xprim_idx[], XPrim[]).
+#pragma once
+#include <stdint.h>
+#include <vector>
+
+#include "gi_math.h"
+
+namespace gi {
+
+enum EntKind : int32_t { K_IMP_SPHERE = 1, K_IMP_TRIANGLE = 2, K_EXP_QUAD = 3 };
+
+struct RNode {             // 64 bytes
+    double mn[3], mx[3];
+    int32_t child0;        // -1: leaf
+    int32_t parent;        // -1: root
+    int32_t ent_off;       // leaves: offset into leaf_ents
+    int32_t ent_cnt;       // size of the node's _entities (interior: only emptiness is used, octree.h:241)
+};
+static_assert(sizeof(RNode) == 64, "RNode layout");
+
+struct REnt {              // 160 bytes
+    int32_t kind, tri_first, tri_count, pad0;
+    double pos[3];         // ImpSphere centre / ExpQuad pos
+    float radius, width, length, alpha;
+    double qv0[3], qv1[3]; // ExpQuad vertices[0], [1] (texture frame, entities.h:634-635)
+    double color[3], shader[3];
+    double spec_pow;
+};
+static_assert(sizeof(REnt) == 160, "REnt layout");
+
+// Mode X primitive: triangle (v0, e1, e2, n) or sphere (c, r)
+struct XPrim {             // 112 bytes
+    double a[3];           // triangle v0 | sphere centre
+    double b[3];           // triangle e1 | sphere (r, 0, 0)
+    double c[3];           // triangle e2
+    double n[3];           // triangle geometric normal normalize(cross(e1,e2))
+    int32_t kind;          // 0 triangle, 1 sphere
+    int32_t ent;
+    int32_t pad[2];
+};
+static_assert(sizeof(XPrim) == 112, "XPrim layout");
+
+struct XNode {             // 64 bytes
+    double mn[3], mx[3];   // conservative AABB of the cell
+    int32_t child_base;    // interior: index of the first existing child (children contiguous)
+    int32_t child_mask;    // interior: bit c set if octant c exists; 0 for a leaf
+    int32_t prim_off;      // leaf: range in xprim_idx
+    int32_t prim_cnt;
+};
+static_assert(sizeof(XNode) == 64, "XNode layout");
+
+struct HostScene {
+    // Mode R
+    std::vector<RNode> rnodes;
+    std::vector<int32_t> leaf_ents;
+    std::vector<REnt> ents;
+    std::vector<TriRec> tris;
+    int32_t max_depth = 0, n_leaves = 0, n_reachable = 0, n_dropped = 0;
+    // Mode X
+    std::vector<XNode> xnodes;
+    std::vector<int32_t> xprim_idx;
+    std::vector<XPrim> xprims;
+    int32_t x_max_depth = 0;
+};
+
+// Device view passed to kernels by value.
+struct DevScene {
+    const RNode* rnodes;
+    const int32_t* leaf_ents;
+    const REnt* ents;
+    const TriRec* tris;
+    const XNode* xnodes;
+    const int32_t* xprim_idx;
+    const XPrim* xprims;
+    int32_t n_rnodes, n_ents, n_xnodes, n_xprims;
+    int32_t x_max_depth, pad;
+};
+
+}  // namespace gi

@@ -1,0 +1,169 @@
+/* gi.h — C-ABI of the MI355X-native (gfx950) per-pixel radiance path for preon7/2019global.
+ *
+ * This is the drop-in boundary for the reference's render driver.  The reference has no ABI: its
+ * path is the header-only class RayTracer (include/raytracer.h:15-101) whose run(w, h)
+ * (raytracer.h:23-87) loops over pixels and, per pixel, queries Octree::intersect
+ * (octree.h:147-169), calls Entity::intersect / getTextureCoord (entities.h:26, 32) and
+ * Material::blinn_phong_texture (material.h:48-62), and stores through Image::setPixel
+ * (image.h:14-16).  The entry points below replace, one for one:
+ *
+ *   gi_scene_create      Octree(min,max) (octree.h:115) + Octree::push_back per entity
+ *                        (octree.h:121-144) + the entity constructors (entities.h:45, 138, 581, ...)
+ *   gi_camera_init       Camera(pos, lookAt, focal) (camera.h:8-10)
+ *   gi_render            RayTracer::run(w, h) (raytracer.h:23-87), host buffers, progressive tiles,
+ *                        cancel flag = RayTracer::stop() (raytracer.h:90)
+ *   gi_render_device     the same frame into device-resident buffers on a HIP stream (bench,
+ *                        multi-GPU tile sharding)
+ *   gi_trace_ray         one iteration of raytracer.h:41-84 for an arbitrary ray
+ *   gi_unshard_device    reassembles a frame from per-rank packed tiles after the RCCL gather
+ *
+ * Conventions: all pointers are plain C pointers; buffers are caller-owned; sizes are in elements;
+ * every function returns 0 on success and a negative gi_status on error, with a thread-local
+ * message from gi_last_error().  No exception crosses this boundary.  Rendering never falls back
+ * to the CPU: without a usable gfx950 device gi_scene_create fails with GI_ERR_DEVICE.
+ */
+#ifndef GI_H_
+#define GI_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GI_ABI_VERSION 1
+
+typedef enum gi_status {
+    GI_OK = 0,
+    GI_ERR_ARG = -1,      /* invalid argument */
+    GI_ERR_DEVICE = -2,   /* HIP error / no device */
+    GI_ERR_SCENE = -3,    /* unsupported entity or material */
+    GI_ERR_CANCELLED = -4 /* *cancel became non-zero; frame partially rendered */
+} gi_status;
+
+/* Entity kinds.  args[] holds the reference constructor's arguments in constructor order. */
+typedef enum gi_entity_kind {
+    GI_IMP_SPHERE = 1,   /* ImpSphere(pos, float radius, color)              entities.h:45  args: px py pz r cr cg cb            */
+    GI_IMP_TRIANGLE = 2, /* ImpTriangle(p1, p2, p3) (material: red)          entities.h:138 args: p1 p2 p3 (9)                   */
+    GI_EXP_QUAD = 3,     /* ExpQuad(pos, float w, float l, float alpha, col) entities.h:581 args: px py pz w l alpha cr cg cb    */
+    GI_EXP_SPHERE = 4,   /* reserved */
+    GI_EXP_CUBE = 5,     /* reserved */
+    GI_EXP_CONE = 6      /* reserved */
+} gi_entity_kind;
+
+typedef struct gi_entity_desc {
+    int32_t kind;               /* gi_entity_kind */
+    int32_t has_material;       /* 1: entity->material = Material(mat_color, mat_shader); specular_power set */
+    double args[11];
+    double mat_color[3];
+    double mat_shader[3];       /* Material::shader_parameters (material.h:27) */
+    double mat_specular_power;  /* Material::specular_power (material.h:29) */
+} gi_entity_desc;
+
+typedef struct gi_scene_desc {
+    double octree_min[3];       /* Octree(min, max) */
+    double octree_max[3];
+    int32_t n_entities;         /* push_back order = candidate order */
+    const gi_entity_desc* entities;
+} gi_scene_desc;
+
+/* Camera as the reference stores it (camera.h:16-20). */
+typedef struct gi_camera {
+    double pos[3];
+    double up[3];
+    double forward[3];          /* normalised */
+    double focal;
+} gi_camera;
+
+typedef enum gi_mode {
+    GI_MODE_R = 0,  /* the reference's semantics bit for bit (depth 1, 1 spp) */
+    GI_MODE_X = 1   /* build-defined depth/spp integrator (DESIGN.md "Mode X") */
+} gi_mode;
+
+#define GI_FLAG_STATS 1u   /* accumulate work counters into opts->stats (device pointer) */
+
+typedef struct gi_opts {
+    int32_t mode;          /* gi_mode */
+    int32_t spp;           /* Mode X samples per pixel (>= 1) */
+    int32_t depth;         /* Mode X path length (>= 1) */
+    int32_t shard_count;   /* >= 1: number of ranks the frame is split over */
+    int32_t shard_index;   /* this rank, 0 <= shard_index < shard_count */
+    int32_t band_rows;     /* gi_render only: rows per progressive band (0 = whole frame) */
+    uint32_t flags;        /* GI_FLAG_* */
+    int32_t reserved;
+    uint64_t seed;         /* Mode X RNG seed */
+    uint64_t* stats;       /* device pointer to GI_STATS_N uint64 counters (GI_FLAG_STATS) */
+} gi_opts;
+
+/* stats[] slots */
+#define GI_STAT_RAYS 0        /* rays traced (primary + bounce + shadow) */
+#define GI_STAT_NODES 1       /* octree node records fetched & tested */
+#define GI_STAT_PRIMS 2       /* primitive records fetched & tested */
+#define GI_STAT_PIXELS 3
+#define GI_STATS_N 8
+
+#define GI_TILE 8             /* shard granularity: 8x8 pixel tiles, dealt round-robin to ranks */
+
+typedef struct gi_scene gi_scene;
+
+typedef struct gi_scene_info {
+    int32_t n_entities;
+    int32_t n_nodes;          /* reference octree nodes (Mode R) */
+    int32_t n_leaves;
+    int32_t max_depth;
+    int32_t n_reachable;      /* entities referenced by at least one leaf */
+    int32_t n_dropped;        /* entities whose bbox misses the root (A.14) */
+    int32_t x_nodes;          /* Mode X octree nodes */
+    int32_t x_prims;          /* Mode X primitives */
+    int64_t device_bytes;     /* scene bytes resident in HBM */
+} gi_scene_info;
+
+typedef struct gi_hit {
+    int32_t entity;           /* -1: no hit */
+    int32_t u, v;             /* getTextureCoord */
+    double point[3], normal[3];
+} gi_hit;
+
+/* progressive-display callback: rgb8 rows [y0, y0+rows) of the frame are final */
+typedef void (*gi_tile_cb)(void* user, int y0, int rows, const uint8_t* rgb8_rows, const double* rgb_rows);
+
+int gi_abi_version(void);
+const char* gi_last_error(void);
+
+int gi_camera_init(const double pos[3], const double look_at[3], double focal, gi_camera* out);
+
+/* Builds the reference octree and the Mode X acceleration structure on the host and uploads the
+ * scene to the current HIP device (the scene is bound to that device). */
+int gi_scene_create(const gi_scene_desc* desc, gi_scene** out);
+void gi_scene_destroy(gi_scene* scene);
+int gi_scene_get_info(const gi_scene* scene, gi_scene_info* info);
+
+/* Renders a w x h frame into host buffers (rgb: w*h*3 fp64, rgb8: w*h*3 RGB888; either may be
+ * NULL).  Polls *cancel (if non-NULL) between bands; calls cb (if non-NULL) after each band. */
+int gi_render(gi_scene* scene, const gi_camera* cam, const double light[3], int w, int h,
+              const gi_opts* opts, double* rgb, uint8_t* rgb8, const volatile int* cancel,
+              gi_tile_cb cb, void* user);
+
+/* Device-resident variant, asynchronous on `stream` (hipStream_t; NULL = default stream).
+ * shard_count == 1: d_rgb / d_rgb8 are row-major frames.  shard_count > 1: they hold this rank's
+ * tiles packed as [gi_shard_tiles(w,h,n)][GI_TILE*GI_TILE][3], tile t = shard_index + k*n. */
+int gi_render_device(gi_scene* scene, const gi_camera* cam, const double light[3], int w, int h,
+                     const gi_opts* opts, double* d_rgb, uint8_t* d_rgb8, void* stream);
+
+/* Tiles per rank (the packed buffer of every rank has this many tiles, padded). */
+int64_t gi_shard_tiles(int w, int h, int shard_count);
+
+/* d_packed: shard_count consecutive per-rank packed buffers (as gathered); writes row-major frames. */
+int gi_unshard_device(int w, int h, int shard_count, const double* d_packed, const uint8_t* d_packed8,
+                      double* d_rgb, uint8_t* d_rgb8, void* stream);
+
+/* One ray through the Mode R per-pixel body (raytracer.h:43-82) on the device: origin, dir (the
+ * Ray ctor normalises it), light.  rgb receives the shaded colour (0 if no hit). */
+int gi_trace_ray(gi_scene* scene, const double origin[3], const double dir[3], const double light[3],
+                 gi_hit* hit, double rgb[3]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GI_H_ */

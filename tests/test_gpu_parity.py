@@ -1,0 +1,253 @@
+"""GPU (gfx950): the HIP path through the C-ABI against (a) the golden vectors of the COMPILED
+REFERENCE (Mode R) and (b) the CPU oracle on the same seeded inputs (Mode R and Mode X).
+
+Tolerances (north_star: per-pixel error <= 1e-5 relative per channel):
+  * Mode R radiance: |gpu - ref| <= 1e-5 * max(|ref|, 1e-300) per channel.  Everything except the
+    device's f64 acos/sin/cos/pow is the reference's exact op sequence, so most pixels are
+    bit-identical; the count is reported.  RGB888 (Image::setPixel) must match exactly.
+  * Mode X radiance: bit-identical to the oracle (only correctly rounded ops, no contraction).
+"""
+import json
+import os
+import re
+import glob
+
+import numpy as np
+import pytest
+
+import oracle_util as U
+
+pytestmark = pytest.mark.gpu
+
+gi = U.pkg()
+S = U.scenes()
+GOLD = U.GOLDEN
+REL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need a device"
+    return torch
+
+
+def _scene(name):
+    if name == "main":
+        return S.main_scene()
+    if name == "sphere":
+        return S.sphere_scene()
+    if name == "cornell":
+        return S.cornell_scene()
+    if name.startswith("soup"):
+        return S.soup_scene(int(name[4:]))
+    raise KeyError(name)
+
+
+_dev_cache = {}
+
+
+def dev_scene(name):
+    if name not in _dev_cache:
+        _dev_cache[name] = gi.DeviceScene.from_scene(_scene(name))
+    return _dev_cache[name]
+
+
+def cam_of(sc):
+    return gi.Camera(sc.cam_pos, sc.cam_look, sc.focal)
+
+
+def assert_rel(gpu, ref, what):
+    gpu = np.asarray(gpu, np.float64)
+    ref = np.asarray(ref, np.float64)
+    err = np.abs(gpu - ref)
+    tol = REL * np.maximum(np.abs(ref), 1e-300)
+    bad = ~(err <= tol)
+    same_nan = np.isnan(gpu) & np.isnan(ref)
+    bad &= ~same_nan
+    assert not bad.any(), f"{what}: {int(bad.sum())} channels beyond {REL} relative; max rel err " \
+                          f"{float(np.nanmax(err / np.maximum(np.abs(ref), 1e-300)))}"
+
+
+FRAMES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLD, "*.npz"))
+                if re.search(r"_\d+x\d+", os.path.basename(p)))
+
+
+@pytest.mark.parametrize("name", FRAMES)
+def test_mode_r_vs_reference_golden(torch_cuda, name):
+    z = np.load(os.path.join(GOLD, name + ".npz"))
+    meta = json.loads(str(z["meta"]))
+    sc = _scene(meta["scene"])
+    assert sc.digest() == meta["scene_sha256"]
+    w, h = meta["w"], meta["h"]
+    rgb, rgb8 = dev_scene(meta["scene"]).render(cam_of(sc), sc.light, w, h)
+    g = rgb[z["y"], z["x"]]
+    g8 = rgb8[z["y"], z["x"]]
+    assert_rel(g, z["rgb"], name)
+    assert (g8 == z["q"]).all(), f"{name}: {(g8 != z['q']).any(1).sum()} RGB888 pixels differ"
+    if "run_q" in z.files:
+        assert (rgb8 == z["run_q"]).all()   # RayTracer::run's own frame
+    exact = U.bits_equal(g, z["rgb"]).all(1).mean()
+    print(f"{name}: {exact * 100:.3f}% pixels bit-identical to the reference")
+
+
+def test_mode_r_random_scene_vs_oracle(torch_cuda):
+    rng = np.random.default_rng(5)
+    s = S.Scene(entities=[])
+    for _ in range(8):
+        s.imp_sphere(tuple(rng.uniform(-4, 8, 3)), float(rng.uniform(0.5, 3)), tuple(rng.integers(0, 2, 3)))
+    for _ in range(60):
+        c = rng.uniform(-3, 9, 3)
+        v = c + rng.uniform(-2, 2, (3, 3))
+        s.imp_triangle(tuple(v[0]), tuple(v[1]), tuple(v[2]), tuple(rng.integers(0, 2, 3)))
+    s.exp_quad((1.0, 0.5, -0.5), 3, 2, 0.7, (1, 1, 0))
+    w, h = 160, 120
+    o = U.oracle_render(s.to_scn(), w, h)
+    d = gi.DeviceScene.from_scene(s)
+    info = d.info()
+    assert info["n_nodes"] > 1   # the octree splits: node tests are exercised
+    rgb, rgb8 = d.render(cam_of(s), s.light, w, h)
+    assert_rel(rgb.reshape(-1, 3), o["rgb"], "random scene")
+    assert (rgb8.reshape(-1, 3) == o["q"]).all()
+
+
+def test_scene_info_matches_reference_tree(torch_cuda):
+    for name in ("cornell", "soup1000", "soup100000"):
+        st = json.load(open(os.path.join(GOLD, f"tree_{name}.json")))
+        info = dev_scene(name).info()
+        assert (info["n_nodes"], info["n_leaves"], info["max_depth"], info["n_reachable"]) == \
+               (st["n_nodes"], st["n_leaves"], st["max_depth"], st["n_reachable"])
+
+
+def test_trace_ray_matches_frame(torch_cuda):
+    sc = S.cornell_scene()
+    z = np.load(os.path.join(GOLD, "cornell_128x128.npz"))
+    d = dev_scene("cornell")
+    # camera ray of pixel (x, y) exactly as raytracer.h:41 builds it
+    c = cam_of(sc)
+    pos, up, fwd = np.array(c.pos), np.array(c.up), np.array(c.forward)
+    for k in range(0, len(z["x"]), 997):
+        x, y = int(z["x"][k]), int(z["y"][k])
+        left = np.cross(up, fwd)
+        left = left * (1.0 / np.sqrt((left[0] * left[0] + left[1] * left[1]) + left[2] * left[2]))
+        # only used as a spot check: the kernel normalises; compare hit entity and colour
+        w = 128
+        tl = (((pos + c.focalDist * fwd) + ((left * w) * 0.5) * 0.0002) + ((up * w) * 0.5) * 0.0002) - pos
+        dirv = (tl - (left * x) * 0.0002) - (up * y) * 0.0002
+        hit, rgb = d.trace_ray(c.pos, tuple(dirv), sc.light)
+        assert hit.entity == z["hit"][k]
+        assert_rel(rgb, z["rgb"][k], f"trace_ray px {x},{y}")
+
+
+def test_progressive_bands_equal_whole_frame(torch_cuda):
+    sc = S.cornell_scene()
+    d = dev_scene("cornell")
+    a, a8 = d.render(cam_of(sc), sc.light, 200, 136)
+    b, b8 = d.render(cam_of(sc), sc.light, 200, 136, band_rows=16)
+    assert U.bits_equal(a, b).all() and (a8 == b8).all()
+    ax, _ = d.render(cam_of(sc), sc.light, 64, 40, mode=gi.MODE_X, spp=2, depth=3, seed=9)
+    bx, _ = d.render(cam_of(sc), sc.light, 64, 40, mode=gi.MODE_X, spp=2, depth=3, seed=9, band_rows=8)
+    assert U.bits_equal(ax, bx).all()
+
+
+def test_cancel_before_start(torch_cuda):
+    import ctypes
+    sc = S.cornell_scene()
+    with pytest.raises(gi.GIError, match="-4"):
+        dev_scene("cornell").render(cam_of(sc), sc.light, 64, 64, cancel=ctypes.c_int(1))
+
+
+def test_raytracer_api_matches_run_golden(torch_cuda):
+    z = np.load(os.path.join(GOLD, "main_200x200.npz"))
+    sc = S.main_scene()
+    cam = gi.Camera(sc.cam_pos, sc.cam_look, sc.focal)
+    rt = gi.RayTracer(cam, sc.light)
+    tree = gi.Octree(sc.octree_min, sc.octree_max)
+    tree.push_back(gi.ExpQuad((0.0, 0.0, 0.0), 2, 3, 90.0 * np.pi / 180.0, (1, 2, 3)))
+    tree.push_back(gi.ImpSphere((3.0, 4.0, 4.0), 2, (1, 0, 0)))
+    tree.push_back(gi.ImpSphere((4.0, -4.0, 4.0), 2, (0, 0, 1)))
+    rt.setScene(tree)
+    rt.start()
+    rt.run(200, 200)
+    img = rt.getImage()
+    assert img.width() == 200 and img.height() == 200
+    assert (img.rgb8 == z["run_q"]).all()
+
+
+@pytest.mark.parametrize("scene,w,h,spp,depth", [("cornell", 48, 40, 4, 4), ("main", 40, 40, 2, 3),
+                                                  ("sphere", 32, 32, 3, 2), ("soup1000", 40, 40, 2, 8)])
+def test_mode_x_bit_exact_vs_oracle(torch_cuda, scene, w, h, spp, depth):
+    sc = _scene(scene)
+    o = U.oracle_render(sc.to_scn(), w, h, mode=1, spp=spp, depth=depth, seed=2019)
+    rgb, rgb8 = dev_scene(scene).render(cam_of(sc), sc.light, w, h, mode=gi.MODE_X, spp=spp, depth=depth, seed=2019)
+    same = U.bits_equal(rgb.reshape(-1, 3), o["rgb"]).all(1)
+    assert same.all(), f"{(~same).sum()} of {same.size} pixels differ from the oracle"
+    assert (rgb8.reshape(-1, 3) == o["q"]).all()
+
+
+def test_mode_x_cornell_window_full_depth(torch_cuda):
+    # C3 frame (1920x1080, depth 8) on a window, 2 spp: parity at the config's geometry
+    sc = S.cornell_scene()
+    win = (900, 880, 940, 920)
+    o = U.oracle_render(sc.to_scn(), 1920, 1080, mode=1, spp=2, depth=8, seed=1, window=win)
+    rgb, _ = dev_scene("cornell").render(cam_of(sc), sc.light, 1920, 1080, mode=gi.MODE_X, spp=2, depth=8, seed=1)
+    g = rgb[win[1]:win[3], win[0]:win[2]].reshape(-1, 3)
+    assert U.bits_equal(g, o["rgb"]).all()
+    assert (o["hit"] >= 0).mean() > 0.5
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+@pytest.mark.parametrize("mode", [gi.MODE_R, gi.MODE_X])
+def test_sharded_render_equals_single(torch_cuda, n, mode):
+    torch = torch_cuda
+    sc = S.cornell_scene()
+    d = dev_scene("cornell")
+    w, h = 203, 117
+    kw = dict(mode=mode, spp=2, depth=4, seed=3) if mode == gi.MODE_X else {}
+    full = torch.zeros(h * w * 3, dtype=torch.float64, device="cuda")
+    full8 = torch.zeros(h * w * 3, dtype=torch.uint8, device="cuda")
+    d.render_device(cam_of(sc), sc.light, w, h, full.data_ptr(), full8.data_ptr(), **kw)
+    per = gi.shard_tiles(w, h, n) * gi.TILE * gi.TILE * 3
+    packed = torch.zeros(n * per, dtype=torch.float64, device="cuda")
+    packed8 = torch.zeros(n * per, dtype=torch.uint8, device="cuda")
+    for r in range(n):
+        d.render_device(cam_of(sc), sc.light, w, h, packed.data_ptr() + r * per * 8, packed8.data_ptr() + r * per,
+                        shard_count=n, shard_index=r, **kw)
+    out = torch.zeros_like(full)
+    out8 = torch.zeros_like(full8)
+    gi.unshard_device(w, h, n, packed.data_ptr(), packed8.data_ptr(), out.data_ptr(), out8.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int64), full.view(torch.int64))
+    assert torch.equal(out8, full8)
+
+
+def test_stats_counters(torch_cuda):
+    torch = torch_cuda
+    sc = S.cornell_scene()
+    d = dev_scene("cornell")
+    w, h = 128, 128
+    st = torch.zeros(8, dtype=torch.int64, device="cuda")
+    buf = torch.zeros(w * h * 3, dtype=torch.float64, device="cuda")
+    d.render_device(cam_of(sc), sc.light, w, h, buf.data_ptr(), stats_ptr=st.data_ptr())
+    torch.cuda.synchronize()
+    s = st.cpu().numpy()
+    assert s[gi.STAT_RAYS] == w * h and s[gi.STAT_PIXELS] == w * h
+    z = np.load(os.path.join(GOLD, "cornell_128x128.npz"))
+    # reverse-DFS first hit never tests more nodes than the reference's full DFS
+    assert 0 < s[gi.STAT_NODES] <= int(z["nnode"].sum())
+
+
+def test_soup100k_full_frame_properties(torch_cuda):
+    # C4 at full 1920x1080: the golden window sample above pins values; here the whole frame is
+    # rendered and checked for size-independent properties: sharding invariance and determinism.
+    torch = torch_cuda
+    sc = S.soup_scene(100000)
+    d = dev_scene("soup100000")
+    w, h = 1920, 1080
+    a = torch.zeros(w * h * 3, dtype=torch.float64, device="cuda")
+    b = torch.zeros_like(a)
+    d.render_device(cam_of(sc), sc.light, w, h, a.data_ptr())
+    d.render_device(cam_of(sc), sc.light, w, h, b.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(a.view(torch.int64), b.view(torch.int64))
+    assert float(a.max()) <= 1.0 and float(a.min()) >= 0.0

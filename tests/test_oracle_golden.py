@@ -1,0 +1,142 @@
+"""CPU: pins the oracle (oracle/gi_oracle.cpp, this repo's restatement of the reference per-pixel
+loop) against golden vectors produced by the COMPILED REFERENCE (tests/golden/make_golden.py).
+Mode R is required to match bit for bit: radiance, hit entity, (u,v), candidate-list length and
+node-test count.  Where oracle/_ref exists (build container), also re-checks live against it."""
+import glob
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle_util as U
+
+S = U.scenes()
+GOLD = U.GOLDEN
+
+
+def _scene(name):
+    if name == "main":
+        return S.main_scene()
+    if name == "sphere":
+        return S.sphere_scene()
+    if name == "cornell":
+        return S.cornell_scene()
+    if name.startswith("soup"):
+        return S.soup_scene(int(name[4:]))
+    raise KeyError(name)
+
+
+FRAMES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLD, "*.npz"))
+                if re.search(r"_\d+x\d+", os.path.basename(p)))
+
+
+def load_frame(name):
+    z = np.load(os.path.join(GOLD, name + ".npz"))
+    meta = json.loads(str(z["meta"]))
+    return z, meta
+
+
+def render_pixels(scn, w, h, xs, ys, **kw):
+    """oracle at exactly the golden pixel set (bounding window, then gather)."""
+    x0, x1, y0, y1 = xs.min(), xs.max() + 1, ys.min(), ys.max() + 1
+    o = U.oracle_render(scn, w, h, window=(x0, y0, x1, y1), **kw)
+    idx = (ys - y0) * (x1 - x0) + (xs - x0)
+    return {k: v[idx] for k, v in o.items()}
+
+
+def test_frames_present():
+    assert len(FRAMES) >= 6, FRAMES
+
+
+@pytest.mark.parametrize("name", FRAMES)
+def test_mode_r_bit_exact_vs_reference_golden(name):
+    z, meta = load_frame(name)
+    sc = _scene(meta["scene"])
+    assert sc.digest() == meta["scene_sha256"], "scene generator drifted from the fixture"
+    if meta["scene"] == "soup100000" and len(z["x"]) > 9000:
+        pytest.skip("large")
+    o = render_pixels(sc.to_scn(), meta["w"], meta["h"], z["x"], z["y"])
+    assert U.bits_equal(o["rgb"], z["rgb"]).all(), "fp64 radiance differs from the reference"
+    assert (o["hit"] == z["hit"]).all()
+    assert (o["uv"] == z["uv"]).all()
+    assert (o["ncand"] == z["ncand"]).all()
+    assert (o["nnode"] == z["nnode"]).all()
+    assert (o["q"] == z["q"]).all()
+    if "run_q" in z.files:   # RayTracer::run's own QImage (Qt) agrees with the restated quantisation
+        q = z["q"].reshape(meta["h"], meta["w"], 3)
+        assert (z["run_q"] == q).all()
+
+
+def test_main_scene_checksum_anchor():
+    # SURVEY Appendix B regression anchor: main.cpp scene 500x500 -> sum(3R+5G+7B) = 111049727
+    o = U.oracle_render(S.main_scene().to_scn(), 500, 500)
+    q = o["q"].astype(np.int64)
+    assert int((3 * q[:, 0] + 5 * q[:, 1] + 7 * q[:, 2]).sum()) == 111049727
+    assert int((q.sum(1) > 0).sum()) == 53182
+
+
+@pytest.mark.parametrize("scene", ["main", "sphere", "cornell", "soup1000"])
+def test_octree_structure_vs_reference(scene):
+    import hashlib
+    st = json.load(open(os.path.join(GOLD, f"tree_{scene}.json")))
+    dump = U.oracle_tree(_scene(scene).to_scn())
+    assert hashlib.sha256(dump.encode()).hexdigest() == st["sha256"]
+
+
+def test_cornell_tree_stats():
+    st = json.load(open(os.path.join(GOLD, "tree_cornell.json")))
+    # Cornell 81 nodes / 71 leaves / depth 4 / 22 of 34 reachable (A.6)
+    assert (st["n_nodes"], st["n_leaves"], st["max_depth"], st["n_reachable"]) == (81, 71, 4, 22)
+
+
+@pytest.mark.parametrize("scene", ["main", "cornell"])
+def test_entity_intersect_kat(scene):
+    z = np.load(os.path.join(GOLD, f"rays_{scene}.npz"))
+    sc = _scene(scene)
+    o = U.oracle_rays(sc.to_scn(), z["rays"], len(sc.entities))
+    assert (o["hit"] == z["hit"]).all()
+    assert U.bits_equal(o["pn"], z["pn"]).all()
+    assert (o["uv"] == z["uv"]).all()
+
+
+def test_expbox_node_test_kat():
+    z = np.load(os.path.join(GOLD, "boxes.npz"))
+    assert (U.oracle_boxes(z["recs"]) == z["hit"]).all()
+
+
+def test_main_cpp_kat_values():
+    kat = json.load(open(os.path.join(GOLD, "kat.json")))
+    # main.cpp:90-104 entity_test through the oracle's sphere routine (a sphere scene + one ray)
+    s = S.Scene(entities=[])
+    s.imp_sphere((2.0, 0.0, 0.0), 10, (0, 1, 0))
+    o = U.oracle_rays(s.to_scn(), np.array([[-10.0, 0, 0, 1, 0.5, 0.5]]), 1)
+    assert o["hit"][0, 0] == kat["entity_test.hit"][0]
+    assert np.array_equal(o["pn"][0, 0, :3], kat["entity_test.point"])
+    assert np.array_equal(o["pn"][0, 0, 3:], kat["entity_test.normal"])
+
+
+def test_soup_generator_digest():
+    d = json.load(open(os.path.join(GOLD, "soup_digest.json")))
+    assert S.soup_digest(1000, 2019) == d["soup1000_vertices_sha256"]
+
+
+@pytest.mark.skipif(not U.have_ref(), reason="compiled reference only in the build container")
+def test_live_reference_random_scene():
+    # a seeded random scene of all supported entity kinds, compared live with the reference
+    rng = np.random.default_rng(11)
+    s = S.Scene(entities=[])
+    for _ in range(6):
+        s.imp_sphere(tuple(rng.uniform(-4, 8, 3)), float(rng.uniform(0.5, 3)), tuple(rng.integers(0, 2, 3)))
+    for _ in range(20):
+        c = rng.uniform(-3, 9, 3)
+        v = c + rng.uniform(-2, 2, (3, 3))
+        s.imp_triangle(tuple(v[0]), tuple(v[1]), tuple(v[2]), tuple(rng.integers(0, 2, 3)))
+    s.exp_quad((1.0, 0.5, -0.5), 3, 2, 0.7, (1, 1, 0))
+    scn = s.to_scn()
+    r = U.ref_render(scn, 96, 96)
+    o = U.oracle_render(scn, 96, 96)
+    assert U.bits_equal(r["rgb"], o["rgb"]).all()
+    assert (r["hit"] == o["hit"]).all() and (r["nnode"] == o["nnode"]).all()
+    assert U.ref_tree(scn) == U.oracle_tree(scn)
