@@ -6,6 +6,7 @@ no FMA) never contracts a*b+c.  Run ``python -m 2019global_amd.build`` or ``__gr
 """
 from __future__ import annotations
 
+import glob
 import os
 import shutil
 import subprocess
@@ -57,6 +58,8 @@ def build(verbose: bool = False, force: bool = False) -> str:
         objs.append(obj)
     if force or _stale(OUT, objs):
         _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-o", OUT, *objs, f"-L{ROCM}/lib", "-lamdhip64"], verbose)
+        for leftover in glob.glob(OUT + ".0.*"):   # hipcc's unbundling temporaries
+            os.remove(leftover)
     return OUT
 
 

@@ -164,10 +164,64 @@ struct Box {
     double mn[3], mx[3];
 };
 const int XLEAF_MAX = 4;
-const int XMAX_DEPTH = 16;
+const int XMAX_DEPTH = 12;
+
+// Separating-axis triangle/box overlap (Akenine-Moller 2001): 3 box normals, the triangle plane
+// and the 9 edge x axis products.  Conservative: callers pass a padded box.
+bool tri_box_overlap(const double* c, const double* hs, const XPrim& p) {
+    double v[3][3];
+    for (int k = 0; k < 3; ++k) {
+        v[0][k] = p.a[k] - c[k];
+        v[1][k] = p.a[k] + p.b[k] - c[k];
+        v[2][k] = p.a[k] + p.c[k] - c[k];
+    }
+    for (int k = 0; k < 3; ++k) {   // box normals
+        const double mn = std::min(std::min(v[0][k], v[1][k]), v[2][k]);
+        const double mx = std::max(std::max(v[0][k], v[1][k]), v[2][k]);
+        if (mn > hs[k] || mx < -hs[k]) return false;
+    }
+    double e[3][3];
+    for (int k = 0; k < 3; ++k) {
+        e[0][k] = v[1][k] - v[0][k];
+        e[1][k] = v[2][k] - v[1][k];
+        e[2][k] = v[0][k] - v[2][k];
+    }
+    for (int i = 0; i < 3; ++i)        // edge i x box axis j
+        for (int j = 0; j < 3; ++j) {
+            double a[3] = {0, 0, 0};
+            const int j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+            a[j1] = -e[i][j2];
+            a[j2] = e[i][j1];
+            const double p0 = a[0] * v[0][0] + a[1] * v[0][1] + a[2] * v[0][2];
+            const double p1 = a[0] * v[1][0] + a[1] * v[1][1] + a[2] * v[1][2];
+            const double p2 = a[0] * v[2][0] + a[1] * v[2][1] + a[2] * v[2][2];
+            const double r = hs[0] * std::fabs(a[0]) + hs[1] * std::fabs(a[1]) + hs[2] * std::fabs(a[2]);
+            const double mn = std::min(std::min(p0, p1), p2), mx = std::max(std::max(p0, p1), p2);
+            if (mn > r * (1 + 1e-12) || mx < -r * (1 + 1e-12)) return false;
+        }
+    // triangle plane
+    const double n[3] = {e[0][1] * e[1][2] - e[0][2] * e[1][1], e[0][2] * e[1][0] - e[0][0] * e[1][2],
+                         e[0][0] * e[1][1] - e[0][1] * e[1][0]};
+    const double d = n[0] * v[0][0] + n[1] * v[0][1] + n[2] * v[0][2];
+    const double r = hs[0] * std::fabs(n[0]) + hs[1] * std::fabs(n[1]) + hs[2] * std::fabs(n[2]);
+    return std::fabs(d) <= r * (1 + 1e-12);
+}
+
+bool prim_box_overlap(const XPrim& p, const double* mn, const double* mx) {
+    double c[3], hs[3];
+    for (int k = 0; k < 3; ++k) { c[k] = 0.5 * (mn[k] + mx[k]); hs[k] = 0.5 * (mx[k] - mn[k]); }
+    if (p.kind == 0) return tri_box_overlap(c, hs, p);
+    double d2 = 0;   // sphere: squared distance from the centre to the box
+    for (int k = 0; k < 3; ++k) {
+        const double q = std::max(mn[k] - p.a[k], std::max(0.0, p.a[k] - mx[k]));
+        d2 += q * q;
+    }
+    return d2 <= p.b[0] * p.b[0] * (1 + 1e-12);
+}
 
 struct XBuild {
     const std::vector<Box>* pb;
+    const std::vector<XPrim>* prims;
     std::vector<XNode>* out;
     std::vector<int32_t>* idx;
     double pad;
@@ -216,7 +270,7 @@ struct XBuild {
                 Box test = cb[c];
                 for (int k = 0; k < 3; ++k) { test.mn[k] -= pad; test.mx[k] += pad; }
                 for (int32_t p : prims)
-                    if (overlap(test, (*pb)[p])) kids[c].push_back(p);
+                    if (overlap(test, (*pb)[p]) && prim_box_overlap((*this->prims)[p], test.mn, test.mx)) kids[c].push_back(p);
                 if (!kids[c].empty() && kids[c].size() < prims.size()) progress = true;
             }
             split = progress;
@@ -351,6 +405,7 @@ bool build_host_scene(const gi_scene_desc& desc, HostScene& hs, std::string& err
     for (int k = 0; k < 3; ++k) ext = std::max(ext, std::max(std::fabs(rootb.mn[k]), std::fabs(rootb.mx[k])));
     XBuild xb;
     xb.pb = &pb;
+    xb.prims = &hs.xprims;
     xb.out = &hs.xnodes;
     xb.idx = &hs.xprim_idx;
     xb.pad = 1e-9 * ext;
@@ -366,6 +421,58 @@ bool build_host_scene(const gi_scene_desc& desc, HostScene& hs, std::string& err
         xb.build(0, rootb, all, 0);
     }
     hs.x_max_depth = xb.max_depth;
+
+    // wide traversal nodes: one XWNode per interior cell holding its children's boxes in fp32
+    double pad32 = 1e-5 * ext;
+    auto lo32 = [&](double v) {
+        float f = (float)(v - pad32);
+        if ((double)f > v - pad32) f = std::nextafter(f, -INFINITY);
+        return f;
+    };
+    auto hi32 = [&](double v) {
+        float f = (float)(v + pad32);
+        if ((double)f < v + pad32) f = std::nextafter(f, INFINITY);
+        return f;
+    };
+    const size_t nx = hs.xnodes.size();
+    std::vector<int32_t> ref(nx, 0);
+    int32_t nwide = 0, nleaf = 0;
+    for (size_t i = 0; i < nx; ++i) {
+        if (hs.xnodes[i].child_mask != 0) ref[i] = nwide++;
+        else ref[i] = ~(nleaf++);
+    }
+    hs.xleaves.assign((size_t)nleaf, XLeaf{0, 0});
+    for (size_t i = 0; i < nx; ++i)
+        if (hs.xnodes[i].child_mask == 0) hs.xleaves[~ref[i]] = XLeaf{hs.xnodes[i].prim_off, hs.xnodes[i].prim_cnt};
+    const bool root_leaf = hs.xnodes[0].child_mask == 0;
+    hs.xwnodes.assign(root_leaf ? 1 : (size_t)nwide, XWNode());
+    auto empty_slot = [](XWNode& w, int c) {
+        for (int k = 0; k < 3; ++k) { w.lo[k][c] = INFINITY; w.hi[k][c] = -INFINITY; }
+        w.child[c] = XEMPTY;
+    };
+    for (XWNode& w : hs.xwnodes) {
+        for (int c = 0; c < 8; ++c) empty_slot(w, c);
+        for (int c = 0; c < 8; ++c) w.pad[c] = 0;
+    }
+    auto fill_slot = [&](XWNode& w, int c, const XNode& n, int32_t r) {
+        for (int k = 0; k < 3; ++k) { w.lo[k][c] = lo32(n.mn[k]); w.hi[k][c] = hi32(n.mx[k]); }
+        w.child[c] = r;
+    };
+    if (root_leaf) {
+        fill_slot(hs.xwnodes[0], 0, hs.xnodes[0], ref[0]);
+    } else {
+        for (size_t i = 0; i < nx; ++i) {
+            const XNode& n = hs.xnodes[i];
+            if (n.child_mask == 0) continue;
+            XWNode& w = hs.xwnodes[ref[i]];
+            int rank = 0;
+            for (int c = 0; c < 8; ++c)
+                if ((n.child_mask >> c) & 1) {
+                    const int ci = n.child_base + rank++;
+                    fill_slot(w, c, hs.xnodes[ci], ref[ci]);
+                }
+        }
+    }
     return true;
 }
 

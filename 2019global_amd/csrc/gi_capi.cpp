@@ -148,14 +148,15 @@ int gi_scene_create(const gi_scene_desc* desc, gi_scene** out) {
     const HostScene& h = s->host;
     if ((e = upload(s, h.rnodes, &d.rnodes)) != hipSuccess || (e = upload(s, h.leaf_ents, &d.leaf_ents)) != hipSuccess ||
         (e = upload(s, h.ents, &d.ents)) != hipSuccess || (e = upload(s, h.tris, &d.tris)) != hipSuccess ||
-        (e = upload(s, h.xnodes, &d.xnodes)) != hipSuccess || (e = upload(s, h.xprim_idx, &d.xprim_idx)) != hipSuccess ||
+        (e = upload(s, h.xwnodes, &d.xwnodes)) != hipSuccess || (e = upload(s, h.xleaves, &d.xleaves)) != hipSuccess ||
+        (e = upload(s, h.xprim_idx, &d.xprim_idx)) != hipSuccess ||
         (e = upload(s, h.xprims, &d.xprims)) != hipSuccess) {
         gi_scene_destroy(s);
         return hip_fail(e, "scene upload");
     }
     d.n_rnodes = (int32_t)h.rnodes.size();
     d.n_ents = (int32_t)h.ents.size();
-    d.n_xnodes = (int32_t)h.xnodes.size();
+    d.n_xwnodes = (int32_t)h.xwnodes.size();
     d.n_xprims = (int32_t)h.xprims.size();
     d.x_max_depth = h.x_max_depth;
     *out = s;

@@ -252,7 +252,19 @@ __global__ __launch_bounds__(256) void k_mode_r(DevScene sc, CamDev cam, V3 ligh
 // ---------------------------------------------------------------------------------------------
 // Mode X
 // ---------------------------------------------------------------------------------------------
-constexpr int kXStack = 128;
+// worst case 7 pushes per level x XMAX_DEPTH (12) + 1; a line crosses at most 4 octants
+constexpr int kXStack = 96;
+
+struct F3 {
+    float x, y, z;
+};
+__device__ __forceinline__ F3 f3(float x, float y, float z) { F3 r; r.x = x; r.y = y; r.z = z; return r; }
+// smallest float >= v (conservative culling bound)
+__device__ __forceinline__ float up32(double v) {
+    float f = (float)v;
+    if ((double)f < v) f = __int_as_float(__float_as_int(f) + (f >= 0.0f ? 1 : -1));
+    return f;
+}
 
 __device__ __forceinline__ double x_prim_t(const XPrim& p, V3 o, V3 d, double tmin) {
     if (p.kind == 0) {   // Möller–Trumbore, two-sided
@@ -281,56 +293,6 @@ __device__ __forceinline__ double x_prim_t(const XPrim& p, V3 o, V3 d, double tm
     if (t > tmin) return t;
     t = -b + sq;
     return (t > tmin) ? t : INFINITY;
-}
-
-__device__ __forceinline__ double slab_enter(const XNode& n, V3 o, V3 inv, double tmax) {
-    const double tx0 = (n.mn[0] - o.x) * inv.x, tx1 = (n.mx[0] - o.x) * inv.x;
-    const double ty0 = (n.mn[1] - o.y) * inv.y, ty1 = (n.mx[1] - o.y) * inv.y;
-    const double tz0 = (n.mn[2] - o.z) * inv.z, tz1 = (n.mx[2] - o.z) * inv.z;
-    const double tn = fmax(fmax(fmin(tx0, tx1), fmin(ty0, ty1)), fmax(fmin(tz0, tz1), 0.0));
-    const double tf = fmin(fmin(fmax(tx0, tx1), fmax(ty0, ty1)), fmin(fmax(tz0, tz1), tmax));
-    return (tn <= tf) ? tn : INFINITY;
-}
-
-// closest hit (any_hit=false) or occlusion test before tmax (any_hit=true).  Returns prim index.
-template <bool ANY>
-__device__ int x_trace(const DevScene& sc, V3 o, V3 d, double tmax, double& tbest, uint32_t& nnode, uint32_t& nprim) {
-    const V3 inv = v3(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
-    const int dmask = (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
-    int stack[kXStack];
-    int sp = 0;
-    stack[sp++] = 0;
-    int best = -1;
-    tbest = tmax;
-    while (sp > 0) {
-        const int ni = stack[--sp];
-        const XNode nd = sc.xnodes[ni];
-        ++nnode;
-        const double te = slab_enter(nd, o, inv, tbest);
-        if (!(te <= tbest)) continue;
-        if (nd.child_mask == 0) {
-            for (int k = 0; k < nd.prim_cnt; ++k) {
-                const int pi = sc.xprim_idx[nd.prim_off + k];
-                ++nprim;
-                const double t = x_prim_t(sc.xprims[pi], o, d, MX_TMIN);
-                if (ANY) {
-                    if (t < tmax) { tbest = t; return pi; }
-                } else if (t < tbest || (t == tbest && pi < best)) {
-                    tbest = t;
-                    best = pi;
-                }
-            }
-            continue;
-        }
-        // push existing children far-to-near so the nearest (octant dmask first) pops first
-        for (int k = 7; k >= 0; --k) {
-            const int c = k ^ dmask;
-            if (!((nd.child_mask >> c) & 1)) continue;
-            const int rank = __popc(nd.child_mask & ((1 << c) - 1));
-            if (sp < kXStack) stack[sp++] = nd.child_base + rank;
-        }
-    }
-    return best;
 }
 
 __device__ void x_texcoord(const DevScene& sc, const REnt& e, V3 ip, int32_t& x, int32_t& y) {
@@ -365,6 +327,18 @@ __device__ void x_texcoord(const DevScene& sc, const REnt& e, V3 ip, int32_t& x,
     }
 }
 
+// Mode X path state machine.  A lane owns one pixel and walks its spp samples in order; every
+// loop iteration a lane either makes ONE traversal step of its current ray (pop a node: cull,
+// push children, or test a leaf's primitives) or, once its ray has finished, runs the shading
+// handler that consumes the hit and spawns the lane's next ray (shadow ray, next bounce, or the
+// next sample's primary ray).  Lanes never wait for each other at sample/bounce boundaries
+// (the nested-loop form reconverged at every loop exit: ~16% VALU lane utilisation measured).
+// The handler runs once at least half of the live lanes have a finished ray, or when none is
+// still traversing, so it executes with a well-filled EXEC mask.  The per-path operation
+// sequence is exactly the oracle's (pixel_mode_x in oracle/gi_oracle.cpp), so results are
+// bit-identical whatever the schedule.
+enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_DONE = 2, PH_START = 3 };
+
 template <bool STATS>
 __global__ __launch_bounds__(256) void k_mode_x(DevScene sc, CamDev cam, V3 light, TileMap m, int spp, int depth,
                                                  uint64_t seed, double* rgb, uint8_t* rgb8,
@@ -374,67 +348,175 @@ __global__ __launch_bounds__(256) void k_mode_x(DevScene sc, CamDev cam, V3 ligh
     const bool ok = lane_pixel(m, idx, x, y);
     y += m.y0;
     uint32_t nnode = 0, nprim = 0, nrays = 0;
-    if (ok) {
-        const uint64_t pix = (uint64_t)y * (uint64_t)m.w + (uint64_t)x;
-        const uint64_t key = mx_key(seed, pix);
-        double s0 = 0, s1 = 0, s2 = 0;
-        for (int smp = 0; smp < spp; ++smp) {
-            double jx = 0.0, jy = 0.0;
-            if (spp > 1) { jx = mx_u01k(key, smp, 0xFFFF, 0); jy = mx_u01k(key, smp, 0xFFFF, 1); }
-            V3 o = cam.pos;
-            V3 d = normalize(primary_dir(cam, (double)x + jx, (double)y + jy));
-            V3 L = v3(0, 0, 0), T = v3(1, 1, 1);
-            for (int b = 0; b < depth; ++b) {
-                double t;
-                const int pi = x_trace<false>(sc, o, d, INFINITY, t, nnode, nprim);
+    const uint64_t pix = (uint64_t)y * (uint64_t)m.w + (uint64_t)x;
+    const uint64_t key = mx_key(seed, pix);
+
+    int phase = ok ? PH_START : PH_DONE;
+    int smp = 0, b = 0;
+    // current ray
+    V3 o = cam.pos, d = v3(1, 0, 0);
+    int dmask = 0, best = -1, sp = 0;
+    double tbest = INFINITY, tmax = INFINITY;
+    float tbest_f = INFINITY;
+    F3 of = f3(0, 0, 0), ivf = f3(1, 1, 1);
+    int stk_ref[kXStack];
+    float stk_t[kXStack];
+    // path
+    V3 L = v3(0, 0, 0), T = v3(1, 1, 1);
+    double s0 = 0, s1 = 0, s2 = 0;
+    // carried across the shadow ray
+    V3 P = v3(0, 0, 0), nextd = v3(0, 0, 0), lit = v3(0, 0, 0), dark = v3(0, 0, 0), Tn = v3(0, 0, 0);
+    bool has_next = false;
+
+    while (phase != PH_DONE) {
+        const bool trav = sp > 0;
+        const unsigned long long m_live = __ballot(1);
+        const unsigned long long m_trav = __ballot(trav);
+        const int n_wait = __popcll(m_live & ~m_trav);
+        const bool handle = !trav && (2 * n_wait >= __popcll(m_live) || m_trav == 0);
+        if (trav) {
+            // ---- one traversal step --------------------------------------------------------
+            --sp;
+            const int ref = stk_ref[sp];
+            if (stk_t[sp] <= tbest_f) {   // pruned on pop when a closer hit arrived since the push
+                if (ref < 0) {            // leaf: fp64 primitive tests (these decide the result)
+                    const XLeaf lf = sc.xleaves[~ref];
+                    for (int k = 0; k < lf.cnt; ++k) {
+                        const int pi = sc.xprim_idx[lf.off + k];
+                        ++nprim;
+                        const double t = x_prim_t(sc.xprims[pi], o, d, MX_TMIN);
+                        if (phase == PH_SHADOW) {
+                            if (t < tmax) { best = pi; sp = 0; break; }   // any hit occludes
+                        } else if (t < tbest || (t == tbest && pi < best)) {
+                            tbest = t;
+                            best = pi;
+                            tbest_f = up32(t);
+                        }
+                    }
+                } else {                  // interior: cull the 8 children in fp32, push hits
+                    ++nnode;
+                    const XWNode* nd = sc.xwnodes + ref;
+#pragma unroll
+                    for (int k = 7; k >= 0; --k) {   // far-to-near: octant dmask pops first
+                        const int c = k ^ dmask;
+                        const int ch = nd->child[c];
+                        const float tx0 = (nd->lo[0][c] - of.x) * ivf.x, tx1 = (nd->hi[0][c] - of.x) * ivf.x;
+                        const float ty0 = (nd->lo[1][c] - of.y) * ivf.y, ty1 = (nd->hi[1][c] - of.y) * ivf.y;
+                        const float tz0 = (nd->lo[2][c] - of.z) * ivf.z, tz1 = (nd->hi[2][c] - of.z) * ivf.z;
+                        const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+                        const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tbest_f));
+                        if (ch != XEMPTY && tn <= tf) {
+                            stk_ref[sp] = ch;
+                            stk_t[sp] = tn;
+                            ++sp;
+                        }
+                    }
+                }
+            }
+        } else if (handle) {
+            // ---- the lane's ray is finished: consume it, spawn the next one --------------------
+            bool end_path = false;
+            if (phase == PH_CLOSEST) {
                 ++nrays;
-                if (pi < 0) break;
-                const XPrim p = sc.xprims[pi];
-                const REnt e = sc.ents[p.ent];
-                const V3 P = o + t * d;
-                V3 N = p.kind == 0 ? ld3(p.n) : normalize(P - ld3(p.a));
-                if (!(dot(d, N) < 0)) N = -N;
-                int32_t tu, tv;
-                x_texcoord(sc, e, P, tu, tv);
-                const V3 tc = texel(ld3(e.color), tu, tv);
-                const V3 lv = light - P;
-                const double ldist = gsqrt(dot(lv, lv));
-                const V3 Ld = normalize(lv);
-                double ts;
-                const bool vis = x_trace<true>(sc, P, Ld, ldist, ts, nnode, nprim) < 0;
-                ++nrays;
-                const V3 la = tc * e.shader[0];
-                V3 loc = la;
-                if (vis) {
+                if (best < 0) {
+                    end_path = true;
+                } else {
+                    const XPrim p = sc.xprims[best];
+                    const REnt e = sc.ents[p.ent];
+                    P = o + tbest * d;
+                    V3 N = p.kind == 0 ? ld3(p.n) : normalize(P - ld3(p.a));
+                    if (!(dot(d, N) < 0)) N = -N;
+                    int32_t tu, tv;
+                    x_texcoord(sc, e, P, tu, tv);
+                    const V3 tc = texel(ld3(e.color), tu, tv);
+                    const V3 lv = light - P;
+                    const double ldist = gsqrt(dot(lv, lv));
+                    const V3 Ld = normalize(lv);
+                    const V3 la = tc * e.shader[0];
                     const V3 ldf = (smax(0.0, dot(N, Ld)) * (tc * 0.5)) * e.shader[1];
                     const V3 bis = normalize(normalize(-d) + Ld);
-                    const double sp = mx_powi(smax(0.0, dot(N, bis)), (int)e.spec_pow);
-                    const V3 ls = v3(sp, sp, sp) * e.shader[2];
-                    loc = (la + ldf) + ls;
+                    const double spw = mx_powi(smax(0.0, dot(N, bis)), (int)e.spec_pow);
+                    const V3 ls = v3(spw, spw, spw) * e.shader[2];
+                    const V3 lo = (la + ldf) + ls;
+                    lit = v3(smin(lo.x, 1.0), smin(lo.y, 1.0), smin(lo.z, 1.0));
+                    dark = v3(smin(la.x, 1.0), smin(la.y, 1.0), smin(la.z, 1.0));
+                    has_next = false;
+                    if (b != depth - 1) {
+                        Tn = vmul(T, tc * 0.5);
+                        if (!(Tn.x == 0.0 && Tn.y == 0.0 && Tn.z == 0.0)) {
+                            double sx = 0, sy = 0, r2 = 0;
+                            for (int k = 0; k < 16; ++k) {
+                                const double ax = 2.0 * mx_u01k(key, smp, b, 2 + 2 * k) - 1.0;
+                                const double ay = 2.0 * mx_u01k(key, smp, b, 3 + 2 * k) - 1.0;
+                                const double q = ax * ax + ay * ay;
+                                if (q < 1.0) { sx = ax; sy = ay; r2 = q; break; }
+                            }
+                            const double sz = gsqrt(1.0 - r2);
+                            const double sg = N.z >= 0.0 ? 1.0 : -1.0;
+                            const double aa = -1.0 / (sg + N.z);
+                            const double bb = N.x * N.y * aa;
+                            const V3 t1 = v3(1.0 + sg * N.x * N.x * aa, sg * bb, -sg * N.x);
+                            const V3 t2 = v3(bb, sg + N.y * N.y * aa, -N.y);
+                            nextd = normalize((t1 * sx + t2 * sy) + N * sz);
+                            has_next = true;
+                        }
+                    }
+                    // shadow ray toward the point light
+                    phase = PH_SHADOW;
+                    o = P;
+                    d = Ld;
+                    tmax = ldist;
+                    tbest = ldist;
+                    tbest_f = up32(ldist);
                 }
-                loc = v3(smin(loc.x, 1.0), smin(loc.y, 1.0), smin(loc.z, 1.0));
+            } else if (phase == PH_SHADOW) {
+                ++nrays;
+                const V3 loc = best < 0 ? lit : dark;
                 L = L + vmul(T, loc);
-                if (b == depth - 1) break;
-                T = vmul(T, tc * 0.5);
-                if (T.x == 0.0 && T.y == 0.0 && T.z == 0.0) break;
-                double sx = 0, sy = 0, r2 = 0;
-                for (int k = 0; k < 16; ++k) {
-                    const double ax = 2.0 * mx_u01k(key, smp, b, 2 + 2 * k) - 1.0;
-                    const double ay = 2.0 * mx_u01k(key, smp, b, 3 + 2 * k) - 1.0;
-                    const double q = ax * ax + ay * ay;
-                    if (q < 1.0) { sx = ax; sy = ay; r2 = q; break; }
+                if (!has_next) {
+                    end_path = true;
+                } else {
+                    T = Tn;
+                    o = P;
+                    d = nextd;
+                    ++b;
+                    phase = PH_CLOSEST;
+                    tmax = INFINITY;
+                    tbest = INFINITY;
+                    tbest_f = INFINITY;
                 }
-                const double sz = gsqrt(1.0 - r2);
-                const double sg = N.z >= 0.0 ? 1.0 : -1.0;
-                const double aa = -1.0 / (sg + N.z);
-                const double bb = N.x * N.y * aa;
-                const V3 t1 = v3(1.0 + sg * N.x * N.x * aa, sg * bb, -sg * N.x);
-                const V3 t2 = v3(bb, sg + N.y * N.y * aa, -N.y);
-                d = normalize((t1 * sx + t2 * sy) + N * sz);
-                o = P;
             }
-            s0 = s0 + L.x; s1 = s1 + L.y; s2 = s2 + L.z;
+            if (end_path) {
+                s0 = s0 + L.x; s1 = s1 + L.y; s2 = s2 + L.z;
+                ++smp;
+                phase = smp < spp ? PH_START : PH_DONE;
+            }
+            if (phase == PH_START) {
+                double jx = 0.0, jy = 0.0;
+                if (spp > 1) { jx = mx_u01k(key, smp, 0xFFFF, 0); jy = mx_u01k(key, smp, 0xFFFF, 1); }
+                o = cam.pos;
+                d = normalize(primary_dir(cam, (double)x + jx, (double)y + jy));
+                L = v3(0, 0, 0);
+                T = v3(1, 1, 1);
+                b = 0;
+                phase = PH_CLOSEST;
+                tmax = INFINITY;
+                tbest = INFINITY;
+                tbest_f = INFINITY;
+            }
+            if (phase != PH_DONE) {   // start traversing the new ray
+                const V3 inv = v3(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+                of = f3((float)o.x, (float)o.y, (float)o.z);
+                ivf = f3((float)inv.x, (float)inv.y, (float)inv.z);
+                dmask = (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
+                best = -1;
+                stk_ref[0] = 0;   // root wide node
+                stk_t[0] = 0.0f;
+                sp = 1;
+            }
         }
+    }
+    if (ok) {
         const double c0 = smin(s0 / (double)spp, 1.0), c1 = smin(s1 / (double)spp, 1.0), c2 = smin(s2 / (double)spp, 1.0);
         if (rgb) { rgb[3 * idx] = c0; rgb[3 * idx + 1] = c1; rgb[3 * idx + 2] = c2; }
         if (rgb8) quantize(c0, c1, c2, rgb8 + 3 * idx);

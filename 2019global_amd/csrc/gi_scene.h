@@ -56,6 +56,20 @@ struct XNode {             // 64 bytes
 };
 static_assert(sizeof(XNode) == 64, "XNode layout");
 
+// Mode X traversal node: the 8 children of one octree cell, each child's tight box in fp32
+// rounded outward and padded (conservative culling; the fp64 primitive tests decide hits).
+constexpr int32_t XEMPTY = (int32_t)0x80000000;
+struct XWNode {            // 256 bytes, 2 cache lines
+    float lo[3][8];        // child box minima, SoA over the 8 octants
+    float hi[3][8];
+    int32_t child[8];      // >= 0: wide node; < 0 (not XEMPTY): ~leaf index; XEMPTY: no child
+    int32_t pad[8];
+};
+static_assert(sizeof(XWNode) == 256, "XWNode layout");
+struct XLeaf {
+    int32_t off, cnt;      // range in xprim_idx
+};
+
 struct HostScene {
     // Mode R
     std::vector<RNode> rnodes;
@@ -65,6 +79,8 @@ struct HostScene {
     int32_t max_depth = 0, n_leaves = 0, n_reachable = 0, n_dropped = 0;
     // Mode X
     std::vector<XNode> xnodes;
+    std::vector<XWNode> xwnodes;
+    std::vector<XLeaf> xleaves;
     std::vector<int32_t> xprim_idx;
     std::vector<XPrim> xprims;
     int32_t x_max_depth = 0;
@@ -76,10 +92,11 @@ struct DevScene {
     const int32_t* leaf_ents;
     const REnt* ents;
     const TriRec* tris;
-    const XNode* xnodes;
+    const XWNode* xwnodes;
+    const XLeaf* xleaves;
     const int32_t* xprim_idx;
     const XPrim* xprims;
-    int32_t n_rnodes, n_ents, n_xnodes, n_xprims;
+    int32_t n_rnodes, n_ents, n_xwnodes, n_xprims;
     int32_t x_max_depth, pad;
 };
 

@@ -1,0 +1,256 @@
+#!/usr/bin/env python3
+"""bench.py — Mray/s and ms/frame of the gfx950 radiance path on the BASELINE.json metric config.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload C3|C2|C4|C5|R-C4|R-main]
+
+N > 1 is launched by the driver as `torch.distributed.run --nproc-per-node N bench.py --gpus N ...`:
+one rank per GPU (RCCL over xGMI).  The frame's 8x8 pixel tiles are dealt round-robin to the
+ranks (tile t -> rank t % N), each rank renders its tiles into a packed buffer in HBM, and one
+ncclGather (torch.distributed.gather on the nccl backend) brings them to rank 0, which
+reassembles the frame with gi_unshard_device.  A step = one whole frame: render + gather +
+unshard; the frame is fixed as N grows ("scaling": "strong").
+
+Default workload C3 (BASELINE.json configs[2]): Cornell box (34 ImpTriangles), 1920x1080,
+depth 8, 64 spp, Mode X (the build-defined integrator: the reference itself renders depth 1 only).
+`value` = total rays traced (primary + bounce + shadow, all ranks) per second, inputs resident in
+HBM.  The ray count per frame is exact: a counting launch (GI_FLAG_STATS) of the same
+deterministic frame runs before the timed region.
+
+roofline: the dominant kernel (k_mode_x) against HBM: achieved = algorithmic bytes per launch
+(node records x 64 B + primitive records x 112 B + 27 B/pixel output) /
+average launch time from HIP events on the launch stream; traffic = HBM bytes per launch from the
+committed rocprofv3 PMC summary when present (profiles/), else null.
+cpu_baseline: this repo's CPU port of the same integrator (oracle, test infrastructure), OpenMP,
+on a bounded window of the same frame; reference_cpu: the compiled reference itself (depth 1, the
+only depth it has) on a strided sample of the same frame, when oracle/_ref is present.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import glob
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+NODE_BYTES = {0: 64, 1: 64}    # RNode / XNode records
+PRIM_BYTES = {0: 144, 1: 112}  # Mode R: TriRec (sphere/quad records are <= 160 B; triangle scenes) / XPrim
+
+WORKLOADS = {
+    # name: (scene, w, h, mode, spp, depth, description)
+    "C3": ("cornell", 1920, 1080, 1, 64, 8, "Cornell box (34 tris), 1920x1080, depth=8, 64 spp (configs[2])"),
+    "C2": ("cornell", 512, 512, 1, 1, 4, "Cornell box (34 tris), 512x512, depth=4 (configs[1])"),
+    "C4": ("soup100000", 1920, 1080, 1, 1, 8, "100k-triangle random mesh + octree, 1920x1080, depth=8 (configs[3])"),
+    "C5": ("soup100000", 3840, 2160, 1, 256, 8, "100k-triangle mesh, 3840x2160, depth=8, 256 spp (configs[4])"),
+    "R-C4": ("soup100000", 1920, 1080, 0, 1, 1, "reference semantics (Mode R), 100k-triangle mesh, 1920x1080"),
+    "R-C3": ("cornell", 1920, 1080, 0, 1, 1, "reference semantics (Mode R), Cornell box, 1920x1080"),
+    "R-main": ("main", 500, 500, 0, 1, 1, "reference semantics (Mode R), main.cpp scene, 500x500"),
+}
+
+
+def make_scene(name):
+    from importlib import import_module
+    S = import_module("2019global_amd.scenes")
+    if name.startswith("soup"):
+        return S.soup_scene(int(name[4:]))
+    return {"cornell": S.cornell_scene, "main": S.main_scene, "sphere": S.sphere_scene}[name]()
+
+
+def pmc_traffic(workload: str):
+    """HBM bytes per launch of the dominant kernel from the committed PMC summary, if any."""
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+        try:
+            d = json.load(open(p))
+        except Exception:
+            continue
+        if d.get("workload") == workload and d.get("hbm_bytes_per_launch"):
+            best = d["hbm_bytes_per_launch"]
+    return best
+
+
+def cpu_baseline(scn_text, w, h, mode, spp, depth, seed):
+    """The oracle (this repo's CPU port) on a bounded window of the same frame."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_util as U
+    threads = max(1, min(16, os.cpu_count() or 1))
+    if mode == 1:
+        cx, cy = w // 2, int(h * 0.8)
+        win = (max(0, cx - 128), max(0, cy - 48), min(w, cx + 128), min(h, cy + 48))
+    else:
+        win = (0, 0, w, h)
+    t = time.perf_counter()
+    o = U.oracle_render(scn_text, w, h, mode=mode, spp=spp, depth=depth, seed=seed, window=win, threads=threads)
+    dt = time.perf_counter() - t
+    rays = int(o["ncand"].sum()) if mode == 1 else (win[2] - win[0]) * (win[3] - win[1])
+    return {"value": round(rays / dt / 1e6, 4), "unit": "Mray/s", "cores": threads, "kind": "port",
+            "sample": f"window x[{win[0]},{win[2]}) y[{win[1]},{win[3]}) of the same frame, {rays} rays, "
+                      f"{dt:.2f} s wall, OpenMP"}
+
+
+def reference_cpu(scn_text, w, h):
+    """The compiled reference (oracle/_ref/ref_harness `time`: RayTracer::run's per-pixel body,
+    depth 1, 1 thread) on a strided sample of the same frame."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(exe):
+        return None
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        sp = os.path.join(td, "s.scn")
+        open(sp, "w").write(scn_text)
+        stride = max(1, (w * h) // 20000)
+        try:
+            out = subprocess.run([exe, "time", sp, str(w), str(h), str(stride)], capture_output=True, text=True,
+                                 timeout=120, check=True).stdout
+        except Exception as e:   # never fail the bench on the optional reference leg
+            return {"error": str(e)[:200]}
+    r = json.loads(out)
+    return {"value": round(r["mray_s"], 6), "unit": "Mray/s", "cores": 1, "kind": "reference",
+            "sample": f"depth 1 (the reference's only depth), every {stride}th pixel, {r['rays']} rays"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="C3", choices=sorted(WORKLOADS))
+    ap.add_argument("--seed", type=int, default=2019)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from importlib import import_module
+    gi = import_module("2019global_amd")
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    scene_name, w, h, mode, spp, depth, desc = WORKLOADS[args.workload]
+    sc = make_scene(scene_name)
+    dev = gi.DeviceScene.from_scene(sc)
+    cam = gi.Camera(sc.cam_pos, sc.cam_look, sc.focal)
+    stream = torch.cuda.current_stream()
+    sptr = stream.cuda_stream
+    kw = dict(mode=mode, spp=spp, depth=depth, seed=args.seed, shard_count=world, shard_index=rank)
+
+    if world == 1:
+        buf = torch.empty(w * h * 3, dtype=torch.float64, device="cuda")
+        buf8 = torch.empty(w * h * 3, dtype=torch.uint8, device="cuda")
+        per = w * h * 3
+    else:
+        per = gi.shard_tiles(w, h, world) * gi.TILE * gi.TILE * 3
+        buf = torch.empty(per, dtype=torch.float64, device="cuda")
+        buf8 = torch.empty(per, dtype=torch.uint8, device="cuda")
+        if rank == 0:
+            gath = [torch.empty(per, dtype=torch.float64, device="cuda") for _ in range(world)]
+            gath8 = [torch.empty(per, dtype=torch.uint8, device="cuda") for _ in range(world)]
+            allp = torch.empty(world * per, dtype=torch.float64, device="cuda")
+            allp8 = torch.empty(world * per, dtype=torch.uint8, device="cuda")
+            frame = torch.empty(w * h * 3, dtype=torch.float64, device="cuda")
+            frame8 = torch.empty(w * h * 3, dtype=torch.uint8, device="cuda")
+
+    # exact work counts of this rank's share of the frame (same deterministic frame, untimed)
+    stats = torch.zeros(8, dtype=torch.int64, device="cuda")
+    dev.render_device(cam, sc.light, w, h, buf.data_ptr(), buf8.data_ptr(), sptr, stats_ptr=stats.data_ptr(), **kw)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.all_reduce(stats)
+    st = stats.cpu().tolist()
+    rays_frame = st[gi.STAT_RAYS]
+
+    ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+
+    def step(i=None):
+        if i is not None:
+            ev0[i].record(stream)
+        dev.render_device(cam, sc.light, w, h, buf.data_ptr(), buf8.data_ptr(), sptr, **kw)
+        if i is not None:
+            ev1[i].record(stream)
+        if world > 1:
+            dist.gather(buf, gath if rank == 0 else None, dst=0)
+            dist.gather(buf8, gath8 if rank == 0 else None, dst=0)
+            if rank == 0:
+                torch.cat(gath, out=allp)
+                torch.cat(gath8, out=allp8)
+                gi.unshard_device(w, h, world, allp.data_ptr(), allp8.data_ptr(), frame.data_ptr(), frame8.data_ptr(), sptr)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in zip(ev0, ev1)) / max(1, args.steps)
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = t.tolist()
+
+    if rank == 0:
+        ms_frame = elapsed / args.steps * 1e3
+        value = rays_frame * args.steps / elapsed / 1e6
+        # algorithmic bytes per launch of the dominant kernel (this rank's launch; N=1: the frame)
+        alg = (st[gi.STAT_NODES] * NODE_BYTES[mode] + st[gi.STAT_PRIMS] * PRIM_BYTES[mode] +
+               st[gi.STAT_PIXELS] * 27) / world
+        achieved = alg / (kern_ms * 1e-3) / 1e9
+        traffic = pmc_traffic(args.workload) if world == 1 else None
+        out = {
+            "metric": "Mray/s + ms/frame at 1920x1080, depth 8; %HBM roofline",
+            "value": round(value, 3),
+            "unit": "Mray/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_frame, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (procedural scene, no external data)",
+            "config": {"workload": f"{args.workload}: {desc}", "mode": "X" if mode == 1 else "R", "width": w,
+                       "height": h, "spp": spp, "depth": depth, "seed": args.seed,
+                       "rays_per_frame": rays_frame, "parallelism": f"tile-shard{world}"},
+            "roofline": {"bound": "hbm", "kernel": "k_mode_x" if mode == 1 else "k_mode_r",
+                         "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "traffic": traffic, "alg_bytes_per_launch": int(alg),
+                         "kernel_ms": round(kern_ms, 3),
+                         "node_visits": st[gi.STAT_NODES], "prim_tests": st[gi.STAT_PRIMS]},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            scn = sc.to_scn()
+            out["cpu_baseline"] = cpu_baseline(scn, w, h, mode, spp, depth, args.seed)
+            ref = reference_cpu(scn, w, h)
+            if ref is not None:
+                out["reference_cpu"] = ref
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
