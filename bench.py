@@ -147,19 +147,14 @@ def main():
     sptr = stream.cuda_stream
     kw = dict(mode=mode, spp=spp, depth=depth, seed=args.seed, shard_count=world, shard_index=rank)
 
+    shard = import_module("2019global_amd.shard")
     if world == 1:
         buf = torch.empty(w * h * 3, dtype=torch.float64, device="cuda")
         buf8 = torch.empty(w * h * 3, dtype=torch.uint8, device="cuda")
-        per = w * h * 3
     else:
-        per = gi.shard_tiles(w, h, world) * gi.TILE * gi.TILE * 3
-        buf = torch.empty(per, dtype=torch.float64, device="cuda")
-        buf8 = torch.empty(per, dtype=torch.uint8, device="cuda")
+        fg = shard.FrameGather(torch, dist, w, h, world, rank, "cuda")
+        buf, buf8 = fg.buf, fg.buf8
         if rank == 0:
-            gath = [torch.empty(per, dtype=torch.float64, device="cuda") for _ in range(world)]
-            gath8 = [torch.empty(per, dtype=torch.uint8, device="cuda") for _ in range(world)]
-            allp = torch.empty(world * per, dtype=torch.float64, device="cuda")
-            allp8 = torch.empty(world * per, dtype=torch.uint8, device="cuda")
             frame = torch.empty(w * h * 3, dtype=torch.float64, device="cuda")
             frame8 = torch.empty(w * h * 3, dtype=torch.uint8, device="cuda")
 
@@ -181,13 +176,11 @@ def main():
         dev.render_device(cam, sc.light, w, h, buf.data_ptr(), buf8.data_ptr(), sptr, **kw)
         if i is not None:
             ev1[i].record(stream)
-        if world > 1:
-            dist.gather(buf, gath if rank == 0 else None, dst=0)
-            dist.gather(buf8, gath8 if rank == 0 else None, dst=0)
+        if world > 1:   # one ncclGather of the packed tiles to rank 0, then reassembly on its GPU
+            fg.gather()
             if rank == 0:
-                torch.cat(gath, out=allp)
-                torch.cat(gath8, out=allp8)
-                gi.unshard_device(w, h, world, allp.data_ptr(), allp8.data_ptr(), frame.data_ptr(), frame8.data_ptr(), sptr)
+                gi.unshard_device(w, h, world, fg.packed_all.data_ptr(), fg.packed_all8.data_ptr(), frame.data_ptr(),
+                                  frame8.data_ptr(), sptr)
 
     for _ in range(args.warmup):
         step()

@@ -251,3 +251,25 @@ def test_soup100k_full_frame_properties(torch_cuda):
     torch.cuda.synchronize()
     assert torch.equal(a.view(torch.int64), b.view(torch.int64))
     assert float(a.max()) <= 1.0 and float(a.min()) >= 0.0
+
+
+def test_unshard_matches_host_layout(torch_cuda):
+    torch = torch_cuda
+    from importlib import import_module
+    SH = import_module("2019global_amd.shard")
+    sc = S.cornell_scene()
+    d = dev_scene("cornell")
+    w, h, n = 77, 50, 3
+    full = torch.zeros(h * w * 3, dtype=torch.float64, device="cuda")
+    d.render_device(cam_of(sc), sc.light, w, h, full.data_ptr())
+    per = gi.shard_tiles(w, h, n) * 64 * 3
+    f = None
+    for r in range(n):
+        pk = torch.zeros(per, dtype=torch.float64, device="cuda")
+        d.render_device(cam_of(sc), sc.light, w, h, pk.data_ptr(), shard_count=n, shard_index=r)
+        torch.cuda.synchronize()
+        f = full.cpu().numpy().reshape(-1, 3)
+        pp = SH.packed_pixels(w, h, n, r)
+        got = pk.cpu().numpy().reshape(-1, 3)
+        assert U.bits_equal(got[pp >= 0], f[pp[pp >= 0]]).all()
+        assert (got[pp < 0] == 0).all()
