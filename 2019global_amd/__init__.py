@@ -91,7 +91,7 @@ TILE_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ct
 
 EXPORTS = ["gi_abi_version", "gi_last_error", "gi_camera_init", "gi_scene_create", "gi_scene_destroy",
            "gi_scene_get_info", "gi_render", "gi_render_device", "gi_shard_tiles", "gi_unshard_device",
-           "gi_trace_ray"]
+           "gi_trace_ray", "gi_kat_expbox"]
 
 _lib = None
 _lock = threading.Lock()
@@ -126,6 +126,7 @@ def lib():
         L.gi_shard_tiles.restype = ctypes.c_int64
         L.gi_unshard_device.argtypes = [i32, i32, i32, vp, vp, vp, vp, vp]
         L.gi_trace_ray.argtypes = [vp, dp, dp, dp, ctypes.POINTER(Hit), dp]
+        L.gi_kat_expbox.argtypes = [i32, dp, ctypes.POINTER(ctypes.c_int32)]
         if L.gi_abi_version() != ABI_VERSION:
             raise GIError(f"libgi ABI {L.gi_abi_version()} != {ABI_VERSION}")
         _lib = L
@@ -328,6 +329,15 @@ class DeviceScene:
         _check(lib().gi_trace_ray(self._h, _d3(origin), _d3(direction), _d3(light), ctypes.byref(hit), rgb),
                "gi_trace_ray")
         return hit, tuple(rgb)
+
+
+def kat_expbox(recs: np.ndarray) -> np.ndarray:
+    """Device ExpBox node test over (min, max, origin, dir) records (gi_kat_expbox)."""
+    recs = np.ascontiguousarray(recs, np.float64)
+    out = np.zeros(recs.shape[0], np.int32)
+    _check(lib().gi_kat_expbox(recs.shape[0], recs.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                               out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))), "gi_kat_expbox")
+    return out
 
 
 def shard_tiles(w: int, h: int, shard_count: int) -> int:

@@ -24,6 +24,7 @@ hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w,
 hipError_t launch_unshard(int w, int h, int shard_count, const double* packed, const uint8_t* packed8, double* rgb,
                           uint8_t* rgb8, hipStream_t stream);
 hipError_t launch_trace_ray(const DevScene& sc, V3 o, V3 d, V3 light, int32_t* out_i, double* out_d, hipStream_t stream);
+hipError_t launch_box_kat(int n, const double* recs, int32_t* out, hipStream_t stream);
 }  // namespace gi
 
 using namespace gi;
@@ -278,6 +279,24 @@ int gi_trace_ray(gi_scene* s, const double origin[3], const double dir[3], const
     hit->v = hi[2];
     for (int k = 0; k < 3; ++k) { hit->point[k] = hd[k]; hit->normal[k] = hd[3 + k]; rgb[k] = hd[6 + k]; }
     return GI_OK;
+}
+
+int gi_kat_expbox(int n, const double* recs, int32_t* out) {
+    if (n < 0 || (n > 0 && (!recs || !out))) return fail(GI_ERR_ARG, "bad arguments");
+    if (n == 0) return GI_OK;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(GI_ERR_DEVICE, "no HIP device");
+    double* d_r = nullptr;
+    int32_t* d_o = nullptr;
+    hipError_t e;
+    if ((e = hipMalloc((void**)&d_r, (size_t)n * 12 * sizeof(double))) != hipSuccess) return hip_fail(e, "hipMalloc");
+    if ((e = hipMalloc((void**)&d_o, (size_t)n * sizeof(int32_t))) != hipSuccess) { (void)hipFree(d_r); return hip_fail(e, "hipMalloc"); }
+    e = hipMemcpy(d_r, recs, (size_t)n * 12 * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = launch_box_kat(n, d_r, d_o, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(out, d_o, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost);
+    (void)hipFree(d_r);
+    (void)hipFree(d_o);
+    return e == hipSuccess ? GI_OK : hip_fail(e, "gi_kat_expbox");
 }
 
 }  // extern "C"

@@ -549,6 +549,14 @@ __global__ __launch_bounds__(256) void k_unshard(TileMap m, const double* packed
     if (rgb8) { rgb8[3 * dst] = packed8[3 * src]; rgb8[3 * dst + 1] = packed8[3 * src + 1]; rgb8[3 * dst + 2] = packed8[3 * src + 2]; }
 }
 
+__global__ __launch_bounds__(256) void k_box_kat(int n, const double* recs, int32_t* out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double* q = recs + 12 * (size_t)i;
+    out[i] = box_hit(v3(q[0], q[1], q[2]), v3(q[3], q[4], q[5]), v3(q[6], q[7], q[8]),
+                     normalize(v3(q[9], q[10], q[11]))) ? 1 : 0;
+}
+
 __global__ void k_trace_ray(DevScene sc, V3 o, V3 d, V3 light, int32_t* out_i, double* out_d) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     RResult r;
@@ -611,6 +619,11 @@ hipError_t launch_unshard(int w, int h, int shard_count, const double* packed, c
     const TileMap m = make_map(w, h, shard_count, 0);
     const long long n = m.n_tiles * kTile * kTile;
     hipLaunchKernelGGL(k_unshard, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, m, packed, packed8, rgb, rgb8);
+    return hipGetLastError();
+}
+
+hipError_t launch_box_kat(int n, const double* recs, int32_t* out, hipStream_t stream) {
+    if (n > 0) hipLaunchKernelGGL(k_box_kat, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, n, recs, out);
     return hipGetLastError();
 }
 

@@ -105,12 +105,29 @@ GI_HD bool tri_hit(V3 p1, V3 p2, V3 p3, V3 n, V3 pos, const float* e1f, const fl
     return true;
 }
 
+// Exact-safe early rejection for tri_hit.  The reference's acceptance test (:232-237) needs the
+// three normalised sub-triangle normals at the computed point to agree within sqrt(1e-3)
+// (~0.03 rad); the point always lies on the ray's line.  Outside the triangle's plane region one
+// sub-normal flips (|d_i - d_j|^2 ~ 4); above/below it the side normals tilt apart unless the
+// height is < ~3% of the distance to the edges; far away they follow P x edge_k, which differ.
+// So every accepted point lies within 1.01x the bounding-sphere radius of the vertex centroid,
+// and a line that misses that sphere (with rounding slack) cannot produce a hit.
+GI_HD bool tri_may_hit(V3 p1, V3 p2, V3 p3, V3 o, V3 d) {
+    const V3 c = (p1 + p2 + p3) * (1.0 / 3.0);
+    const double r2 = smax(smax(sq3(p1 - c), sq3(p2 - c)), sq3(p3 - c));
+    const V3 oc = c - o;
+    const V3 x = cross(oc, d);
+    return dot(x, x) <= r2 * 1.0201 + 1e-12 * dot(oc, oc);
+}
+
 GI_HD bool tri_hit(const TriRec& t, V3 o, V3 d, V3& P, V3& N) {
+    if (!tri_may_hit(ld3(t.p1), ld3(t.p2), ld3(t.p3), o, d)) return false;
     return tri_hit(ld3(t.p1), ld3(t.p2), ld3(t.p3), ld3(t.n), ld3(t.pos), t.e1f, t.e2f, o, d, P, N);
 }
 
 // A triangle built on the fly from three corners (ExpBox faces, entities.h:319-324).
 GI_HD bool tri_hit_corners(V3 p1, V3 p2, V3 p3, V3 o, V3 d) {
+    if (!tri_may_hit(p1, p2, p3, o, d)) return false;
     const V3 e1 = p2 - p1, e2 = p3 - p1;
     const V3 n = normalize(cross(e1, e2));
     const V3 pos = 0.5 * (0.5 * (p1 + p2) + p3);

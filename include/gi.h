@@ -163,6 +163,10 @@ int gi_unshard_device(int w, int h, int shard_count, const double* d_packed, con
 int gi_trace_ray(gi_scene* scene, const double origin[3], const double dir[3], const double light[3],
                  gi_hit* hit, double rgb[3]);
 
+/* Known-answer hook: the device's ExpBox node test (entities.h:379-440 as octree.h:242-247 uses
+ * it) over n host records (min[3], max[3], origin[3], dir[3]); out[i] = 0/1. */
+int gi_kat_expbox(int n, const double* recs, int32_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -273,3 +273,9 @@ def test_unshard_matches_host_layout(torch_cuda):
         got = pk.cpu().numpy().reshape(-1, 3)
         assert U.bits_equal(got[pp >= 0], f[pp[pp >= 0]]).all()
         assert (got[pp < 0] == 0).all()
+
+
+def test_expbox_node_test_kat_on_device(torch_cuda):
+    z = np.load(os.path.join(GOLD, "boxes.npz"))
+    got = gi.kat_expbox(z["recs"])
+    assert (got == z["hit"]).all(), f"{(got != z['hit']).sum()} node tests differ from the reference"
