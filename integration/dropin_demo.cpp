@@ -1,0 +1,44 @@
+// dropin_demo.cpp — the reference application's render path with the drop-in headers.
+//
+// Builds the main.cpp scene (main.cpp:24-48) with the reference's own, unmodified Camera /
+// ImpSphere / ExpQuad / Image classes, then renders it with gi_dropin/raytracer.h (same class
+// name and API as the reference's RayTracer), copying the RayTracer by value as Gui/Viewer do
+// (gui.h:19,35).  Writes the RGB888 frame the Viewer would paint.
+//   dropin_demo <w> <h> <out.rgb>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+
+#include "raytracer.h"   // resolves to include/gi_dropin/raytracer.h (first on the include path)
+
+int main(int argc, char** argv) {
+    if (argc < 4) { std::fprintf(stderr, "usage: dropin_demo w h out.rgb\n"); return 2; }
+    const int w = std::atoi(argv[1]), h = std::atoi(argv[2]);
+    Camera camera({-10, 0, 0}, {1, 0, 0}, 0.1);
+    glm::dvec3 light{-10, 10, 10};
+    RayTracer raytracer(camera, light);
+    Octree scene({-20, -20, -20}, {20, 20, 20});
+    ImpSphere* s2 = new ImpSphere(glm::dvec3{3, 4, 4}, 2, {1, 0, 0});
+    ImpSphere* s3 = new ImpSphere(glm::dvec3{4, -4, 4}, 2, {0, 0, 1});
+    ExpQuad* q = new ExpQuad(glm::dvec3{0, 0, 0}, 2, 3, (90.0 * M_PI / 180.0), {1, 2, 3});
+    scene.push_back(q);
+    scene.push_back(s2);
+    scene.push_back(s3);
+    raytracer.setScene(&scene);
+    RayTracer viewer_copy = raytracer;
+    viewer_copy.start();
+    viewer_copy.run(w, h);
+    std::shared_ptr<Image> img = viewer_copy.getImage();
+    if (img->width() != w || img->height() != h) return 1;
+    FILE* f = std::fopen(argv[3], "wb");
+    if (!f) return 1;
+    for (int y = 0; y < h; ++y)
+        for (int x = 0; x < w; ++x) {
+            const glm::dvec3 p = img->getPixel(x, y);
+            const unsigned char px[3] = {(unsigned char)(p.x * 255. + 0.5), (unsigned char)(p.y * 255. + 0.5),
+                                         (unsigned char)(p.z * 255. + 0.5)};
+            std::fwrite(px, 1, 3, f);
+        }
+    std::fclose(f);
+    return 0;
+}

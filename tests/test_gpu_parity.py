@@ -279,3 +279,18 @@ def test_expbox_node_test_kat_on_device(torch_cuda):
     z = np.load(os.path.join(GOLD, "boxes.npz"))
     got = gi.kat_expbox(z["recs"])
     assert (got == z["hit"]).all(), f"{(got != z['hit']).sum()} node tests differ from the reference"
+
+
+def test_cpp_dropin_raytracer_matches_reference_run(torch_cuda, tmp_path):
+    """The reference app's own classes + include/gi_dropin/raytracer.h (built by integration/Makefile
+    where the reference tree exists) give RayTracer::run's frame of the main.cpp scene."""
+    import subprocess
+    exe = os.path.join(U.ROOT, "integration", "_build", "dropin_demo")
+    if not os.path.exists(exe):
+        pytest.skip("integration/_build/dropin_demo not built (needs the reference tree)")
+    out = tmp_path / "f.rgb"
+    env = dict(os.environ, QT_QPA_PLATFORM="offscreen")
+    subprocess.run([exe, "200", "200", str(out)], check=True, env=env, timeout=120)
+    got = np.frombuffer(out.read_bytes(), np.uint8).reshape(200, 200, 3)
+    z = np.load(os.path.join(GOLD, "main_200x200.npz"))
+    assert (got == z["run_q"]).all()
