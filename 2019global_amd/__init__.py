@@ -37,11 +37,11 @@ __all__ = [
 ]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libgi.so")
+LIB_PATH = os.environ.get("GI_LIB") or os.path.join(HERE, "libgi.so")   # GI_LIB: A/B builds
 
 MODE_R, MODE_X = 0, 1
 FLAG_STATS = 1
-STAT_RAYS, STAT_NODES, STAT_PRIMS, STAT_PIXELS = 0, 1, 2, 3
+STAT_RAYS, STAT_NODES, STAT_PRIMS, STAT_PIXELS, STAT_PBOX = 0, 1, 2, 3, 4
 STATS_N = 8
 TILE = 8
 ABI_VERSION = 1

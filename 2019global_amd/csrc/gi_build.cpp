@@ -442,8 +442,29 @@ bool build_host_scene(const gi_scene_desc& desc, HostScene& hs, std::string& err
         else ref[i] = ~(nleaf++);
     }
     hs.xleaves.assign((size_t)nleaf, XLeaf{0, 0});
+    hs.xhot.clear();
+    hs.xbox.clear();
     for (size_t i = 0; i < nx; ++i)
-        if (hs.xnodes[i].child_mask == 0) hs.xleaves[~ref[i]] = XLeaf{hs.xnodes[i].prim_off, hs.xnodes[i].prim_cnt};
+        if (hs.xnodes[i].child_mask == 0) {
+            const XNode& n = hs.xnodes[i];
+            hs.xleaves[~ref[i]] = XLeaf{(int32_t)hs.xhot.size(), n.prim_cnt};   // range in xhot
+            for (int k = 0; k < n.prim_cnt; ++k) {
+                const int32_t pi = hs.xprim_idx[n.prim_off + k];
+                const XPrim& p = hs.xprims[pi];
+                XHot h;
+                memcpy(h.a, p.a, sizeof h.a);
+                memcpy(h.b, p.b, sizeof h.b);
+                memcpy(h.c, p.c, sizeof h.c);
+                h.prim = pi;
+                h.kind = p.kind;
+                hs.xhot.push_back(h);
+                XBox bx;
+                for (int a = 0; a < 3; ++a) { bx.lo[a] = lo32(pb[pi].mn[a]); bx.hi[a] = hi32(pb[pi].mx[a]); }
+                bx.pad[0] = pi;
+                bx.pad[1] = p.kind;
+                hs.xbox.push_back(bx);
+            }
+        }
     const bool root_leaf = hs.xnodes[0].child_mask == 0;
     hs.xwnodes.assign(root_leaf ? 1 : (size_t)nwide, XWNode());
     auto empty_slot = [](XWNode& w, int c) {
@@ -452,11 +473,19 @@ bool build_host_scene(const gi_scene_desc& desc, HostScene& hs, std::string& err
     };
     for (XWNode& w : hs.xwnodes) {
         for (int c = 0; c < 8; ++c) empty_slot(w, c);
-        for (int c = 0; c < 8; ++c) w.pad[c] = 0;
+        w.parent = -1;
+        for (int c = 0; c < 8; ++c) w.cnt[c] = 0;
+        for (int c = 0; c < 3; ++c) w.pad[c] = 0;
     }
     auto fill_slot = [&](XWNode& w, int c, const XNode& n, int32_t r) {
         for (int k = 0; k < 3; ++k) { w.lo[k][c] = lo32(n.mn[k]); w.hi[k][c] = hi32(n.mx[k]); }
-        w.child[c] = r;
+        if (r >= 0) {
+            w.child[c] = r;
+        } else {   // leaf: offset of its records in xhot + count
+            const XLeaf& lf = hs.xleaves[~r];
+            w.child[c] = ~lf.off;
+            w.cnt[c] = (uint16_t)std::min(lf.cnt, 65535);
+        }
     };
     if (root_leaf) {
         fill_slot(hs.xwnodes[0], 0, hs.xnodes[0], ref[0]);
@@ -470,6 +499,7 @@ bool build_host_scene(const gi_scene_desc& desc, HostScene& hs, std::string& err
                 if ((n.child_mask >> c) & 1) {
                     const int ci = n.child_base + rank++;
                     fill_slot(w, c, hs.xnodes[ci], ref[ci]);
+                    if (ref[ci] >= 0) hs.xwnodes[ref[ci]].parent = ref[i];
                 }
         }
     }

@@ -149,9 +149,10 @@ int gi_scene_create(const gi_scene_desc* desc, gi_scene** out) {
     const HostScene& h = s->host;
     if ((e = upload(s, h.rnodes, &d.rnodes)) != hipSuccess || (e = upload(s, h.leaf_ents, &d.leaf_ents)) != hipSuccess ||
         (e = upload(s, h.ents, &d.ents)) != hipSuccess || (e = upload(s, h.tris, &d.tris)) != hipSuccess ||
-        (e = upload(s, h.xwnodes, &d.xwnodes)) != hipSuccess || (e = upload(s, h.xleaves, &d.xleaves)) != hipSuccess ||
-        (e = upload(s, h.xprim_idx, &d.xprim_idx)) != hipSuccess ||
-        (e = upload(s, h.xprims, &d.xprims)) != hipSuccess) {
+        (e = upload(s, h.xwnodes, &d.xwnodes)) != hipSuccess || (e = upload(s, h.xhot, &d.xhot)) != hipSuccess ||
+        (e = upload(s, h.xbox, &d.xbox)) != hipSuccess ||
+        (e = upload(s, h.xprims, &d.xprims)) != hipSuccess ||
+        (e = upload(s, std::vector<unsigned>(16, 0u), const_cast<const unsigned**>(&d.work))) != hipSuccess) {
         gi_scene_destroy(s);
         return hip_fail(e, "scene upload");
     }

@@ -18,6 +18,7 @@
 // contraction; f64 div/sqrt are correctly rounded on gfx950).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
 
@@ -197,9 +198,8 @@ struct TileMap {
 };
 
 // pixel of this lane; returns false when the lane has no pixel
-__device__ __forceinline__ bool lane_pixel(const TileMap& m, long long& out_idx, int& x, int& y) {
+__device__ __forceinline__ bool lane_pixel(const TileMap& m, long long lt, long long& out_idx, int& x, int& y) {
     const int lane = threadIdx.x & 63;
-    const long long lt = (long long)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     if (lt >= m.n_local) return false;
     const long long t = (long long)m.shard_index + lt * m.shard_count;
     if (t >= m.n_tiles) { out_idx = -1; return false; }
@@ -221,7 +221,8 @@ __global__ __launch_bounds__(256) void k_mode_r(DevScene sc, CamDev cam, V3 ligh
                                                  uint8_t* rgb8, unsigned long long* stats) {
     long long idx = -1;
     int x = 0, y = 0;
-    const bool ok = lane_pixel(m, idx, x, y);
+    const long long lt = (long long)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    const bool ok = lane_pixel(m, lt, idx, x, y);
     y += m.y0;
     uint32_t nnode = 0, nprim = 0;
     if (ok) {
@@ -243,22 +244,24 @@ __global__ __launch_bounds__(256) void k_mode_r(DevScene sc, CamDev cam, V3 ligh
         if (rgb) { rgb[3 * idx] = 0; rgb[3 * idx + 1] = 0; rgb[3 * idx + 2] = 0; }
         if (rgb8) { rgb8[3 * idx] = 0; rgb8[3 * idx + 1] = 0; rgb8[3 * idx + 2] = 0; }
     }
-    if (STATS) {
-        const long long lt = (long long)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-        if (lt < m.n_local) wave_add_stats(stats, ok ? 1 : 0, nnode, nprim, ok ? 1 : 0);
-    }
+    if (STATS && lt < m.n_local) wave_add_stats(stats, ok ? 1 : 0, nnode, nprim, ok ? 1 : 0);
 }
 
 // ---------------------------------------------------------------------------------------------
 // Mode X
 // ---------------------------------------------------------------------------------------------
-// worst case 7 pushes per level x XMAX_DEPTH (12) + 1; a line crosses at most 4 octants
-constexpr int kXStack = 96;
-
 struct F3 {
     float x, y, z;
 };
 __device__ __forceinline__ F3 f3(float x, float y, float z) { F3 r; r.x = x; r.y = y; r.z = z; return r; }
+__device__ __forceinline__ uint32_t lvl_get(uint64_t lo, uint64_t hi, int l) {
+    return (uint32_t)((l < 8 ? lo >> (8 * l) : hi >> (8 * (l - 8))) & 0xFF);
+}
+__device__ __forceinline__ void lvl_set(uint64_t& lo, uint64_t& hi, int l, uint32_t m) {
+    if (l < 8) lo = (lo & ~(0xFFull << (8 * l))) | ((uint64_t)m << (8 * l));
+    else hi = (hi & ~(0xFFull << (8 * (l - 8)))) | ((uint64_t)m << (8 * (l - 8)));
+}
+
 // smallest float >= v (conservative culling bound)
 __device__ __forceinline__ float up32(double v) {
     float f = (float)v;
@@ -266,7 +269,7 @@ __device__ __forceinline__ float up32(double v) {
     return f;
 }
 
-__device__ __forceinline__ double x_prim_t(const XPrim& p, V3 o, V3 d, double tmin) {
+__device__ __forceinline__ double x_prim_t(const XHot& p, V3 o, V3 d, double tmin) {
     if (p.kind == 0) {   // Möller–Trumbore, two-sided
         const V3 e1 = ld3(p.b), e2 = ld3(p.c);
         const V3 pv = cross(d, e2);
@@ -293,6 +296,32 @@ __device__ __forceinline__ double x_prim_t(const XPrim& p, V3 o, V3 d, double tm
     if (t > tmin) return t;
     t = -b + sq;
     return (t > tmin) ? t : INFINITY;
+}
+
+// fp32 slab test of child c of a wide node against [0, tmax]; boxes are outward-rounded + padded
+__device__ __forceinline__ bool child_hit(const XWNode* nd, int c, F3 of, F3 ivf, float tmax) {
+    const float tx0 = (nd->lo[0][c] - of.x) * ivf.x, tx1 = (nd->hi[0][c] - of.x) * ivf.x;
+    const float ty0 = (nd->lo[1][c] - of.y) * ivf.y, ty1 = (nd->hi[1][c] - of.y) * ivf.y;
+    const float tz0 = (nd->lo[2][c] - of.z) * ivf.z, tz1 = (nd->hi[2][c] - of.z) * ivf.z;
+    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+    const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
+    return tn <= tf;
+}
+__device__ __forceinline__ bool box32_hit(const XBox& b, F3 of, F3 ivf, float tmax) {
+    const float tx0 = (b.lo[0] - of.x) * ivf.x, tx1 = (b.hi[0] - of.x) * ivf.x;
+    const float ty0 = (b.lo[1] - of.y) * ivf.y, ty1 = (b.hi[1] - of.y) * ivf.y;
+    const float tz0 = (b.lo[2] - of.z) * ivf.z, tz1 = (b.hi[2] - of.z) * ivf.z;
+    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+    const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
+    return tn <= tf;
+}
+// mask of hit, existing children with bit k for child k ^ dmask (bit order = front-to-back)
+__device__ __forceinline__ uint32_t children_mask(const XWNode* nd, F3 of, F3 ivf, float tmax, int dmask) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+        if (nd->child[c] != XEMPTY && child_hit(nd, c, of, ivf, tmax)) m |= 1u << (c ^ dmask);
+    return m;
 }
 
 __device__ void x_texcoord(const DevScene& sc, const REnt& e, V3 ip, int32_t& x, int32_t& y) {
@@ -339,15 +368,22 @@ __device__ void x_texcoord(const DevScene& sc, const REnt& e, V3 ip, int32_t& x,
 // bit-identical whatever the schedule.
 enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_DONE = 2, PH_START = 3 };
 
-template <bool STATS>
-__global__ __launch_bounds__(256) void k_mode_x(DevScene sc, CamDev cam, V3 light, TileMap m, int spp, int depth,
-                                                 uint64_t seed, double* rgb, uint8_t* rgb8,
-                                                 unsigned long long* stats) {
+#ifndef GI_X_PRIM_PREFILTER
+#define GI_X_PRIM_PREFILTER 0   // fp32 AABB cull before each fp64 primitive test (measured slower: +1 dependent load)
+#endif
+#ifndef GI_X_MIN_WAVES
+#define GI_X_MIN_WAVES 1   // minimum waves per SIMD for k_mode_x (register budget knob)
+#endif
+
+__device__ __forceinline__ void mode_x_tile(const DevScene& sc, const CamDev& cam, V3 light, const TileMap& m, long long lt,
+                                            int spp, int depth, uint64_t seed, double* rgb, uint8_t* rgb8,
+                                            uint64_t& c_rays, uint64_t& c_nodes, uint64_t& c_prims, uint64_t& c_px,
+                                            uint64_t& c_box) {
     long long idx = -1;
     int x = 0, y = 0;
-    const bool ok = lane_pixel(m, idx, x, y);
+    const bool ok = lane_pixel(m, lt, idx, x, y);
     y += m.y0;
-    uint32_t nnode = 0, nprim = 0, nrays = 0;
+    uint32_t nnode = 0, nprim = 0, nrays = 0, nbox = 0;
     const uint64_t pix = (uint64_t)y * (uint64_t)m.w + (uint64_t)x;
     const uint64_t key = mx_key(seed, pix);
 
@@ -355,12 +391,12 @@ __global__ __launch_bounds__(256) void k_mode_x(DevScene sc, CamDev cam, V3 ligh
     int smp = 0, b = 0;
     // current ray
     V3 o = cam.pos, d = v3(1, 0, 0);
-    int dmask = 0, best = -1, sp = 0;
+    int dmask = 0, best = -1, node = 0, level = 0;
+    bool raying = false;
+    uint64_t mlo = 0, mhi = 0;
     double tbest = INFINITY, tmax = INFINITY;
     float tbest_f = INFINITY;
     F3 of = f3(0, 0, 0), ivf = f3(1, 1, 1);
-    int stk_ref[kXStack];
-    float stk_t[kXStack];
     // path
     V3 L = v3(0, 0, 0), T = v3(1, 1, 1);
     double s0 = 0, s1 = 0, s2 = 0;
@@ -369,47 +405,56 @@ __global__ __launch_bounds__(256) void k_mode_x(DevScene sc, CamDev cam, V3 ligh
     bool has_next = false;
 
     while (phase != PH_DONE) {
-        const bool trav = sp > 0;
+        const bool trav = raying;
         const unsigned long long m_live = __ballot(1);
         const unsigned long long m_trav = __ballot(trav);
         const int n_wait = __popcll(m_live & ~m_trav);
         const bool handle = !trav && (2 * n_wait >= __popcll(m_live) || m_trav == 0);
         if (trav) {
-            // ---- one traversal step --------------------------------------------------------
-            --sp;
-            const int ref = stk_ref[sp];
-            if (stk_t[sp] <= tbest_f) {   // pruned on pop when a closer hit arrived since the push
-                if (ref < 0) {            // leaf: fp64 primitive tests (these decide the result)
-                    const XLeaf lf = sc.xleaves[~ref];
-                    for (int k = 0; k < lf.cnt; ++k) {
-                        const int pi = sc.xprim_idx[lf.off + k];
-                        ++nprim;
-                        const double t = x_prim_t(sc.xprims[pi], o, d, MX_TMIN);
-                        if (phase == PH_SHADOW) {
-                            if (t < tmax) { best = pi; sp = 0; break; }   // any hit occludes
-                        } else if (t < tbest || (t == tbest && pi < best)) {
-                            tbest = t;
-                            best = pi;
-                            tbest_f = up32(t);
+            // ---- one traversal step (stackless: 8-bit "children left" mask per level) --------
+            uint32_t msk = lvl_get(mlo, mhi, level);
+            while (msk == 0 && level > 0) {   // climb to the nearest level with children left
+                node = sc.xwnodes[node].parent;
+                --level;
+                msk = lvl_get(mlo, mhi, level);
+            }
+            if (msk == 0) {
+                raying = false;               // ray finished
+            } else {
+                const int k = __builtin_ctz(msk);          // next child in front-to-back order
+                lvl_set(mlo, mhi, level, msk & (msk - 1));
+                const int c = k ^ dmask;
+                const XWNode* nd = sc.xwnodes + node;
+                const int ch = nd->child[c];
+                // a closer hit may have arrived since the mask was computed: re-cull this child
+                bool keep = true;
+                if (phase == PH_CLOSEST && best >= 0) keep = child_hit(nd, c, of, ivf, tbest_f);
+                if (keep) {
+                    if (ch < 0) {             // leaf: fp64 primitive tests (these decide the result)
+                        const XHot* hp = sc.xhot + ~ch;
+                        const XBox* bp = sc.xbox + ~ch;
+                        const int cnt = nd->cnt[c];
+                        for (int j = 0; j < cnt; ++j) {
+#if GI_X_PRIM_PREFILTER
+                            ++nbox;
+                            if (!box32_hit(bp[j], of, ivf, tbest_f)) continue;   // conservative fp32 cull
+#endif
+                            ++nprim;
+                            const double t = x_prim_t(hp[j], o, d, MX_TMIN);
+                            const int pi = hp[j].prim;
+                            if (phase == PH_SHADOW) {
+                                if (t < tmax) { best = pi; raying = false; break; }   // any hit occludes
+                            } else if (t < tbest || (t == tbest && pi < best)) {
+                                tbest = t;
+                                best = pi;
+                                tbest_f = up32(t);
+                            }
                         }
-                    }
-                } else {                  // interior: cull the 8 children in fp32, push hits
-                    ++nnode;
-                    const XWNode* nd = sc.xwnodes + ref;
-#pragma unroll
-                    for (int k = 7; k >= 0; --k) {   // far-to-near: octant dmask pops first
-                        const int c = k ^ dmask;
-                        const int ch = nd->child[c];
-                        const float tx0 = (nd->lo[0][c] - of.x) * ivf.x, tx1 = (nd->hi[0][c] - of.x) * ivf.x;
-                        const float ty0 = (nd->lo[1][c] - of.y) * ivf.y, ty1 = (nd->hi[1][c] - of.y) * ivf.y;
-                        const float tz0 = (nd->lo[2][c] - of.z) * ivf.z, tz1 = (nd->hi[2][c] - of.z) * ivf.z;
-                        const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
-                        const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tbest_f));
-                        if (ch != XEMPTY && tn <= tf) {
-                            stk_ref[sp] = ch;
-                            stk_t[sp] = tn;
-                            ++sp;
-                        }
+                    } else {                  // descend: cull the child's 8 children in fp32
+                        ++nnode;
+                        node = ch;
+                        ++level;
+                        lvl_set(mlo, mhi, level, children_mask(sc.xwnodes + ch, of, ivf, tbest_f, dmask));
                     }
                 }
             }
@@ -421,8 +466,8 @@ __global__ __launch_bounds__(256) void k_mode_x(DevScene sc, CamDev cam, V3 ligh
                 if (best < 0) {
                     end_path = true;
                 } else {
-                    const XPrim p = sc.xprims[best];
-                    const REnt e = sc.ents[p.ent];
+                    const XPrim& p = sc.xprims[best];   // by reference: only used fields are loaded
+                    const REnt& e = sc.ents[p.ent];
                     P = o + tbest * d;
                     V3 N = p.kind == 0 ? ld3(p.n) : normalize(P - ld3(p.a));
                     if (!(dot(d, N) < 0)) N = -N;
@@ -510,9 +555,11 @@ __global__ __launch_bounds__(256) void k_mode_x(DevScene sc, CamDev cam, V3 ligh
                 ivf = f3((float)inv.x, (float)inv.y, (float)inv.z);
                 dmask = (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
                 best = -1;
-                stk_ref[0] = 0;   // root wide node
-                stk_t[0] = 0.0f;
-                sp = 1;
+                node = 0;   // root wide node
+                level = 0;
+                mlo = mhi = 0;
+                lvl_set(mlo, mhi, 0, children_mask(sc.xwnodes, of, ivf, tbest_f, dmask));
+                raying = true;
             }
         }
     }
@@ -524,9 +571,32 @@ __global__ __launch_bounds__(256) void k_mode_x(DevScene sc, CamDev cam, V3 ligh
         if (rgb) { rgb[3 * idx] = 0; rgb[3 * idx + 1] = 0; rgb[3 * idx + 2] = 0; }
         if (rgb8) { rgb8[3 * idx] = 0; rgb8[3 * idx + 1] = 0; rgb8[3 * idx + 2] = 0; }
     }
+    c_rays += nrays;
+    c_nodes += nnode;
+    c_prims += nprim;
+    c_px += ok ? 1 : 0;
+    c_box += nbox;
+}
+
+// Persistent waves with dynamic tile scheduling: each wave pulls the next 8x8 tile from a
+// device counter (one returning atomic per tile, SURVEY §7 hard part 4: per-ray cost varies ~10x
+// between background and scene tiles), so no wave idles behind a workgroup sibling or the grid tail.
+template <bool STATS>
+__global__ __launch_bounds__(256, GI_X_MIN_WAVES) void k_mode_x(DevScene sc, CamDev cam, V3 light, TileMap m, int spp, int depth,
+                                                 uint64_t seed, double* rgb, uint8_t* rgb8,
+                                                 unsigned long long* stats, unsigned* tile_counter) {
+    uint64_t c_rays = 0, c_nodes = 0, c_prims = 0, c_px = 0, c_box = 0;
+    for (;;) {
+        unsigned v = 0;
+        if ((threadIdx.x & 63) == 0) v = atomicAdd(tile_counter, 1u);
+        const long long lt = (long long)__builtin_amdgcn_readfirstlane(v);
+        if (lt >= m.n_local) break;
+        mode_x_tile(sc, cam, light, m, lt, spp, depth, seed, rgb, rgb8, c_rays, c_nodes, c_prims, c_px, c_box);
+    }
     if (STATS) {
-        const long long lt = (long long)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-        if (lt < m.n_local) wave_add_stats(stats, nrays, nnode, nprim, ok ? 1 : 0);
+        wave_add_stats(stats, c_rays, c_nodes, c_prims, c_px);
+        for (int off = 32; off > 0; off >>= 1) c_box += __shfl_xor(c_box, off);
+        if ((threadIdx.x & 63) == 0) atomicAdd(stats + GI_STAT_PBOX, (unsigned long long)c_box);
     }
 }
 
@@ -606,10 +676,24 @@ hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w,
         if (stats) hipLaunchKernelGGL(k_mode_r<true>, grid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st);
         else hipLaunchKernelGGL(k_mode_r<false>, grid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st);
     } else {
+        // persistent grid: as many 4-wave blocks as can be resident, each wave pulls tiles
+        static int resident_blocks = 0;
+        if (resident_blocks == 0) {
+            int dev = 0, cus = 0, per_cu = 0;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k_mode_x<false>),
+                                                              64 * kWavesPerBlock, 0);
+            resident_blocks = std::max(1, cus) * std::max(1, per_cu);
+        }
+        const long long want = (m.n_local + kWavesPerBlock - 1) / kWavesPerBlock;
+        const dim3 pgrid((unsigned)std::min<long long>(want, resident_blocks));
+        hipError_t e = hipMemsetAsync(sc.work, 0, 16 * sizeof(unsigned), stream);
+        if (e != hipSuccess) return e;
         if (stats)
-            hipLaunchKernelGGL(k_mode_x<true>, grid, block, 0, stream, sc, cam, light, m, o.spp, o.depth, o.seed, rgb, rgb8, st);
+            hipLaunchKernelGGL(k_mode_x<true>, pgrid, block, 0, stream, sc, cam, light, m, o.spp, o.depth, o.seed, rgb, rgb8, st, sc.work);
         else
-            hipLaunchKernelGGL(k_mode_x<false>, grid, block, 0, stream, sc, cam, light, m, o.spp, o.depth, o.seed, rgb, rgb8, st);
+            hipLaunchKernelGGL(k_mode_x<false>, pgrid, block, 0, stream, sc, cam, light, m, o.spp, o.depth, o.seed, rgb, rgb8, st, sc.work);
     }
     return hipGetLastError();
 }

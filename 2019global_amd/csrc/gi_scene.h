@@ -5,7 +5,8 @@
 //             8 consecutive records in octant order 0..7 (octree.h:195-209).
 //   leaf_ents int32 entity indices, each leaf's list in push order.
 //   REnt[]    entity records (kind, material, sphere/quad parameters) + TriRec[] triangles.
-// Mode X uses its own tight octree over primitives (XNode[], xprim_idx[], XPrim[]).
+// Mode X uses its own tight octree over primitives (XWNode[] traversal nodes, XHot[] leaf records,
+// XPrim[] shading records).
 #pragma once
 #include <stdint.h>
 #include <vector>
@@ -62,12 +63,29 @@ constexpr int32_t XEMPTY = (int32_t)0x80000000;
 struct XWNode {            // 256 bytes, 2 cache lines
     float lo[3][8];        // child box minima, SoA over the 8 octants
     float hi[3][8];
-    int32_t child[8];      // >= 0: wide node; < 0 (not XEMPTY): ~leaf index; XEMPTY: no child
-    int32_t pad[8];
+    int32_t child[8];      // >= 0: wide node; < 0 (not XEMPTY): leaf = ~(offset into xhot[]); XEMPTY: none
+    int32_t parent;        // wide node of the parent cell, -1 at the root (stackless traversal)
+    uint16_t cnt[8];       // leaf children: number of xhot records
+    int32_t pad[3];
 };
 static_assert(sizeof(XWNode) == 256, "XWNode layout");
+// Leaf primitive records, duplicated per leaf reference and stored contiguously per leaf, so a
+// leaf costs one dependent load level: exactly what Moller-Trumbore / the sphere test read.
+struct XHot {              // 80 bytes
+    double a[3], b[3], c[3];   // triangle v0, e1, e2 | sphere centre, (r, 0, 0)
+    int32_t prim;          // global primitive index (tie-break, shading record)
+    int32_t kind;          // 0 triangle, 1 sphere
+};
+static_assert(sizeof(XHot) == 80, "XHot layout");
+// fp32 prefilter record parallel to xhot[]: the primitive's AABB rounded outward and padded, so a
+// ray that misses it cannot hit the primitive; the 80-B fp64 record is fetched only otherwise.
+struct XBox {              // 32 bytes
+    float lo[3], hi[3];
+    int32_t pad[2];
+};
+static_assert(sizeof(XBox) == 32, "XBox layout");
 struct XLeaf {
-    int32_t off, cnt;      // range in xprim_idx
+    int32_t off, cnt;      // host build only: range in xprim_idx
 };
 
 struct HostScene {
@@ -82,6 +100,8 @@ struct HostScene {
     std::vector<XWNode> xwnodes;
     std::vector<XLeaf> xleaves;
     std::vector<int32_t> xprim_idx;
+    std::vector<XHot> xhot;
+    std::vector<XBox> xbox;
     std::vector<XPrim> xprims;
     int32_t x_max_depth = 0;
 };
@@ -93,9 +113,10 @@ struct DevScene {
     const REnt* ents;
     const TriRec* tris;
     const XWNode* xwnodes;
-    const XLeaf* xleaves;
-    const int32_t* xprim_idx;
+    const XHot* xhot;
+    const XBox* xbox;
     const XPrim* xprims;
+    unsigned* work;        // 16 device counters (persistent-kernel tile queue), reset per launch
     int32_t n_rnodes, n_ents, n_xwnodes, n_xprims;
     int32_t x_max_depth, pad;
 };

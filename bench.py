@@ -39,8 +39,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-NODE_BYTES = {0: 64, 1: 64}    # RNode / XNode records
-PRIM_BYTES = {0: 144, 1: 112}  # Mode R: TriRec (sphere/quad records are <= 160 B; triangle scenes) / XPrim
+NODE_BYTES = {0: 64, 1: 256}   # RNode / XWNode (8 child boxes) records
+PRIM_BYTES = {0: 144, 1: 80}   # Mode R: TriRec (sphere/quad records are <= 160 B) / Mode X: XHot fp64 record
+PBOX_BYTES = 32                # Mode X: XBox fp32 prefilter record
 
 WORKLOADS = {
     # name: (scene, w, h, mode, spp, depth, description)
@@ -207,7 +208,7 @@ def main():
         value = rays_frame * args.steps / elapsed / 1e6
         # algorithmic bytes per launch of the dominant kernel (this rank's launch; N=1: the frame)
         alg = (st[gi.STAT_NODES] * NODE_BYTES[mode] + st[gi.STAT_PRIMS] * PRIM_BYTES[mode] +
-               st[gi.STAT_PIXELS] * 27) / world
+               st[gi.STAT_PBOX] * PBOX_BYTES + st[gi.STAT_PIXELS] * 27) / world
         achieved = alg / (kern_ms * 1e-3) / 1e9
         traffic = pmc_traffic(args.workload) if world == 1 else None
         out = {
@@ -231,7 +232,8 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "alg_bytes_per_launch": int(alg),
                          "kernel_ms": round(kern_ms, 3),
-                         "node_visits": st[gi.STAT_NODES], "prim_tests": st[gi.STAT_PRIMS]},
+                         "node_visits": st[gi.STAT_NODES], "prim_tests": st[gi.STAT_PRIMS],
+                         "prim_box_tests": st[gi.STAT_PBOX]},
         }
         if not args.no_cpu_baseline and world == 1:
             scn = sc.to_scn()

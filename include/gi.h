@@ -99,8 +99,9 @@ typedef struct gi_opts {
 /* stats[] slots */
 #define GI_STAT_RAYS 0        /* rays traced (primary + bounce + shadow) */
 #define GI_STAT_NODES 1       /* octree node records fetched & tested */
-#define GI_STAT_PRIMS 2       /* primitive records fetched & tested */
+#define GI_STAT_PRIMS 2       /* primitive records fetched & tested in fp64 */
 #define GI_STAT_PIXELS 3
+#define GI_STAT_PBOX 4        /* Mode X primitive prefilter boxes tested (32-B fp32 records) */
 #define GI_STATS_N 8
 
 #define GI_TILE 8             /* shard granularity: 8x8 pixel tiles, dealt round-robin to ranks */
