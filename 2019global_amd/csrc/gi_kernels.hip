@@ -371,6 +371,9 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_DONE = 2, PH_START = 3 };
 #ifndef GI_X_PRIM_PREFILTER
 #define GI_X_PRIM_PREFILTER 0   // fp32 AABB cull before each fp64 primitive test (measured slower: +1 dependent load)
 #endif
+#ifndef GI_X_HANDLE_QUARTERS
+#define GI_X_HANDLE_QUARTERS 2   // shade once >= this many quarters of the live lanes wait
+#endif
 #ifndef GI_X_MIN_WAVES
 #define GI_X_MIN_WAVES 1   // minimum waves per SIMD for k_mode_x (register budget knob)
 #endif
@@ -409,7 +412,7 @@ __device__ __forceinline__ void mode_x_tile(const DevScene& sc, const CamDev& ca
         const unsigned long long m_live = __ballot(1);
         const unsigned long long m_trav = __ballot(trav);
         const int n_wait = __popcll(m_live & ~m_trav);
-        const bool handle = !trav && (2 * n_wait >= __popcll(m_live) || m_trav == 0);
+        const bool handle = !trav && (4 * n_wait >= GI_X_HANDLE_QUARTERS * __popcll(m_live) || m_trav == 0);
         if (trav) {
             // ---- one traversal step (stackless: 8-bit "children left" mask per level) --------
             uint32_t msk = lvl_get(mlo, mhi, level);
