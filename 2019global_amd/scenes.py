@@ -35,6 +35,8 @@ EXP_QUAD = 3
 EXP_SPHERE = 4
 EXP_CUBE = 5
 EXP_CONE = 6
+EXP_RECTANGLE = 7
+EXP_BOX = 8
 
 _KW = {
     IMP_SPHERE: "impsphere",
@@ -43,10 +45,13 @@ _KW = {
     EXP_SPHERE: "expsphere",
     EXP_CUBE: "expcube",
     EXP_CONE: "expcone",
+    EXP_RECTANGLE: "exprectangle",
+    EXP_BOX: "expbox",
 }
 _KIND = {v: k for k, v in _KW.items()}
 # number of ctor arguments per kind (after the keyword)
-_NARGS = {IMP_SPHERE: 7, IMP_TRIANGLE: 9, EXP_QUAD: 9, EXP_SPHERE: 7, EXP_CUBE: 9, EXP_CONE: 11}
+_NARGS = {IMP_SPHERE: 7, IMP_TRIANGLE: 9, EXP_QUAD: 9, EXP_SPHERE: 7, EXP_CUBE: 9, EXP_CONE: 11, EXP_RECTANGLE: 9,
+          EXP_BOX: 6}
 
 
 @dataclass
@@ -97,6 +102,12 @@ class Scene:
 
     def exp_cone(self, pos: Vec3, direction: Vec3, height: float, radius: float, color: Vec3) -> Entity:
         return self._add(EXP_CONE, (*pos, *direction, height, radius, *color))
+
+    def exp_rectangle(self, p1: Vec3, p2: Vec3, p3: Vec3) -> Entity:
+        return self._add(EXP_RECTANGLE, (*p1, *p2, *p3))
+
+    def exp_box(self, mn: Vec3, mx: Vec3) -> Entity:
+        return self._add(EXP_BOX, (*mn, *mx))
 
     def _add(self, kind: int, args: Sequence[float]) -> Entity:
         e = Entity(kind, tuple(float(a) for a in args))
@@ -248,8 +259,42 @@ def soup_digest(n: int = 100_000, seed: int = 2019) -> str:
     return hashlib.sha256(soup_vertices(n, seed).astype("<f8").tobytes()).hexdigest()
 
 
+def zoo_scene() -> Scene:
+    """Every entity type of entities.h in one frame: the commented-out scene
+    objects of main.cpp:31-40 plus an ExpRectangle/ExpBox; not a BASELINE config."""
+    s = Scene(name="zoo")
+    s.exp_sphere((-2.0, 0.0, 0.0), 2, (0, 1, 0))                    # main.cpp:38
+    s.exp_cube((0.0, 0.0, 0.0), 2, 2, 2, (1, 0, 0))                 # main.cpp:39
+    s.exp_cone((0.0, 0.0, 2.0), (-1.0, 1.0, -3.0), 5, 3, (1, 1, 0))  # main.cpp:37
+    s.exp_quad((0.0, 0.0, 0.0), 2, 3, 90.0 * math.pi / 180.0, (1, 2, 3))
+    s.imp_sphere((3.0, 4.0, 4.0), 2, (1, 0, 0))
+    s.imp_triangle((0.0, 3.0, 2.0), (3.0, 3.0, -4.0), (3.0, -3.0, -4.0), (0, 1, 1))   # main.cpp:36
+    s.exp_rectangle((1.0, -6.0, -3.0), (1.0, -3.0, 0.0), (1.0, -6.0, 0.0))
+    s.exp_box((2.0, 4.0, -5.0), (4.0, 6.0, -3.0))
+    return s
+
+
+def only_scene(kind_name: str) -> Scene:
+    """One entity of the zoo alone, e.g. only_scene("expcone") (exercises its shading in frames)."""
+    z = zoo_scene()
+    s = Scene(name=f"only_{kind_name}")
+    s.entities = [e for e in z.entities if _KW[e.kind] == kind_name]
+    assert s.entities, kind_name
+    return s
+
+
+def named_scene(name: str) -> Scene:
+    """Scene factory used by tests, goldens and bench: main, sphere, cornell, zoo, soupN, only_<kind>."""
+    if name.startswith("soup"):
+        return soup_scene(int(name[4:]))
+    if name.startswith("only_"):
+        return only_scene(name[5:])
+    return CONFIG_SCENES[name]()
+
+
 CONFIG_SCENES = {
     "main": main_scene,
     "sphere": sphere_scene,
     "cornell": cornell_scene,
+    "zoo": zoo_scene,
 }

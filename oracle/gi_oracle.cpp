@@ -136,7 +136,8 @@ bool sphere_intersect(V3 pos, float radius, V3 o, V3 d, V3& P, V3& N) {
     return true;
 }
 
-enum Kind { IMP_SPHERE = 1, IMP_TRIANGLE = 2, EXP_QUAD = 3 };
+enum Kind { IMP_SPHERE = 1, IMP_TRIANGLE = 2, EXP_QUAD = 3, EXP_SPHERE = 4, EXP_CUBE = 5, EXP_CONE = 6,
+            EXP_RECTANGLE = 7, EXP_BOX = 8 };
 
 struct Ent {
     int kind = 0;
@@ -144,8 +145,10 @@ struct Ent {
     V3 pos{0, 0, 0};
     float radius = 0, width = 0, length_ = 0, alpha = 0;
     Tri tri;
-    std::vector<Tri> tris;   // ExpQuad triangles
-    V3 qv[4];                // ExpQuad vertices
+    std::vector<Tri> tris;   // group triangles (ExpQuad/Sphere/Cube/Cone; Rectangle t1,t2; Box 6x(t1,t2))
+    V3 qv[4];                // ExpQuad vertices; ExpCube vertices[0]; ExpRectangle p1, p3, p4
+    float height = 0;        // ExpCube / ExpCone
+    double cone_theta = 0;   // ExpCone: atan(radius/height) evaluated in float (entities.h:950)
     V3 bmin, bmax;           // boundingBox() as the reference reports it (A.5, A.13)
 };
 
@@ -200,12 +203,174 @@ Ent make_exp_quad(V3 pos, double w_arg, double l_arg, double a_arg, V3 color) { 
     return e;
 }
 
+// glm::mat3 (float) * dvec3: the vector is narrowed to vec3, product in fp32 (type_mat3x3.inl:429-435)
+struct M3f { float c[3][3]; };   // c[col][row]
+V3 m3_mul(const M3f& m, V3 v) {
+    const float x = (float)v.x, y = (float)v.y, z = (float)v.z;
+    return {(double)(m.c[0][0] * x + m.c[1][0] * y + m.c[2][0] * z), (double)(m.c[0][1] * x + m.c[1][1] * y + m.c[2][1] * z),
+            (double)(m.c[0][2] * x + m.c[1][2] * y + m.c[2][2] * z)};
+}
+
+Ent make_exp_sphere(V3 pos, double radius_arg, V3 color) {   // entities.h:461-506
+    Ent e;
+    e.kind = EXP_SPHERE;
+    e.mat.color = color;
+    e.radius = (float)radius_arg;
+    e.pos = pos;
+    const int sectornum = 10, stacknum = 10;
+    const float sectorStep = (float)(2 * REF_PI / sectornum);
+    const float stackStep = (float)(REF_PI / stacknum);
+    std::vector<V3> vert;
+    for (int i = 0; i <= stacknum; ++i) {
+        const float stackAngle = (float)(REF_PI / 2 - (double)(i * stackStep));
+        const float tmp = e.radius * cosf(stackAngle);
+        const float z = (float)((double)(e.radius * sinf(stackAngle)) - pos.z);   // vertices offset by -pos
+        for (int j = 0; j <= sectornum; ++j) {
+            const float sectorAngle = j * sectorStep;
+            const float x = (float)((double)(tmp * cosf(sectorAngle)) - pos.x);
+            const float y = (float)((double)(tmp * sinf(sectorAngle)) - pos.y);
+            vert.push_back({(double)x, (double)y, (double)z});
+        }
+    }
+    std::vector<Tri> all;
+    for (int i = 0; i < stacknum; ++i) {
+        int k1 = i * (sectornum + 1), k2 = k1 + sectornum + 1;
+        for (int j = 0; j < sectornum; ++j, ++k1, ++k2) {
+            if (i != 0) all.push_back(make_tri(vert[k1], vert[k2], vert[k1 + 1]));
+            if (i != stacknum - 1) all.push_back(make_tri(vert[k1 + 1], vert[k2], vert[k2 + 1]));
+        }
+    }
+    e.tris.assign(all.begin() + 1, all.end());   // intersect() starts at triangle 1 (entities.h:520)
+    const double r = e.radius;
+    e.bmin = {(double)(float)(0.0 - r), (double)(float)(0.0 - r), (double)(float)(0.0 - r)};
+    e.bmax = {(double)(float)(0.0 + r), (double)(float)(0.0 + r), (double)(float)(0.0 + r)};
+    return e;
+}
+
+Ent make_exp_cube(V3 pos, double w_arg, double l_arg, double h_arg, V3 color) {   // entities.h:652-727
+    Ent e;
+    e.kind = EXP_CUBE;
+    e.mat.color = color;
+    e.width = (float)w_arg; e.length_ = (float)l_arg; e.height = (float)h_arg;
+    e.pos = pos;
+    const float hw = e.width / 2, hl = e.length_ / 2, hh = e.height / 2;
+    const V3 v[8] = {{pos.x - hw, pos.y - hl, pos.z - hh}, {pos.x - hw, pos.y - hl, pos.z + hh},
+                     {pos.x + hw, pos.y - hl, pos.z - hh}, {pos.x + hw, pos.y - hl, pos.z + hh},
+                     {pos.x - hw, pos.y + hl, pos.z + hh}, {pos.x - hw, pos.y + hl, pos.z - hh},
+                     {pos.x + hw, pos.y + hl, pos.z - hh}, {pos.x + hw, pos.y + hl, pos.z + hh}};
+    const int T[12][3] = {{0, 1, 2}, {3, 1, 2}, {4, 5, 7}, {7, 5, 6}, {1, 0, 4}, {4, 0, 5},
+                          {3, 7, 2}, {7, 6, 2}, {1, 4, 3}, {3, 4, 7}, {0, 5, 2}, {2, 5, 6}};
+    for (auto& t : T) e.tris.push_back(make_tri(v[t[0]], v[t[1]], v[t[2]]));
+    e.qv[0] = v[0];
+    e.bmin = {(double)(float)(0.0 - hw), (double)(float)(0.0 - hl), (double)(float)(0.0 - hh)};
+    e.bmax = {(double)(float)(0.0 + hw), (double)(float)(0.0 + hl), (double)(float)(0.0 + hh)};
+    return e;
+}
+
+Ent make_exp_cone(V3 pos, V3 dir_arg, double h_arg, double r_arg, V3 color) {   // entities.h:823-899
+    Ent e;
+    e.kind = EXP_CONE;
+    e.mat.color = color;
+    e.height = (float)h_arg;
+    e.radius = (float)r_arg;
+    e.pos = pos;
+    const V3 dir = normalize(V3{-1, 0, -10});   // assigns the shadowing ctor parameter (:825)
+    M3f I = {{{1, 0, 0}, {0, 1, 0}, {0, 0, 1}}}, rx = I, ry = I;
+    const double x_sign = dir.y < 0 ? 1.0 : -1.0;
+    const V3 x_dir{0, dir.y, dir.z};
+    if (!(x_dir.x == 0 && x_dir.y == 0 && x_dir.z == 0)) {
+        const double a = x_sign * std::acos(dot(normalize(x_dir), V3{0, 0, -1}));
+        rx = {{{1, 0, 0}, {0, (float)std::cos(a), (float)(-std::sin(a))}, {0, (float)std::sin(a), (float)std::cos(a)}}};
+    }
+    const double y_sign = dir.x > 0 ? 1.0 : -1.0;
+    const V3 y_dir{dir.x, 0, -std::sqrt(dir.z * dir.z + dir.y * dir.y)};
+    if (!(y_dir.x == 0 && y_dir.y == 0 && y_dir.z == 0)) {
+        const double a = y_sign * std::acos(dot(normalize(y_dir), V3{0, 0, -1}));
+        ry = {{{(float)std::cos(a), 0, (float)std::sin(a)}, {0, 1, 0}, {(float)(-std::sin(a)), 0, (float)std::cos(a)}}};
+    }
+    std::vector<V3> vert{pos};
+    const double nsub = 50.0;
+    for (int i = 0; i <= nsub; ++i) {
+        const float alpha = (float)(i * 360.0 / nsub);
+        V3 loc{pos.x + (double)e.radius * std::cos((double)alpha * REF_PI / 180.0),
+               pos.y + (double)e.radius * std::sin((double)alpha * REF_PI / 180.0), pos.z - (double)e.height};
+        loc = loc - pos;
+        loc = m3_mul(rx, loc);
+        loc = m3_mul(ry, loc);
+        loc = loc + pos;
+        vert.push_back(loc);
+    }
+    const V3 bottom = pos + normalize(dir) * (double)e.height;
+    for (size_t i = 1; i < vert.size() - 1; ++i) {
+        e.tris.push_back(make_tri(pos, vert[i], vert[i + 1]));
+        e.tris.push_back(make_tri(bottom, vert[i], vert[i + 1]));
+    }
+    e.cone_theta = (double)std::atan(e.radius / e.height);   // float atan (:950)
+    (void)dir_arg;   // the member dir keeps the argument but nothing reads it
+    e.bmin = {(double)(float)(0.0 - (double)e.radius), (double)(float)(0.0 - (double)e.radius), (double)(float)(0.0 - (double)e.height)};
+    e.bmax = {(double)(float)(0.0 + (double)e.radius), (double)(float)(0.0 + (double)e.radius), (double)(float)0.0};
+    return e;
+}
+
+Ent make_exp_rectangle(V3 p1, V3 p2, V3 p3) {   // entities.h:310-340 (p4 = -p3, A.4)
+    Ent e;
+    e.kind = EXP_RECTANGLE;   // Entity(): red
+    const V3 p4 = -p3;
+    e.tris.push_back(make_tri(p1, p2, p3));
+    e.tris.push_back(make_tri(p1, p2, p4));
+    e.qv[0] = p1; e.qv[1] = p3; e.qv[2] = p4;
+    e.pos = 0.5 * (p1 + p2);
+    e.bmin = {smin(p1.x, p2.x), smin(p1.y, p2.y), smin(p1.z, p2.z)};
+    e.bmax = {smax(p1.x, p2.x), smax(p1.y, p2.y), smax(p1.z, p2.z)};
+    return e;
+}
+
+void box_faces(V3 mn, V3 mx, V3 F[6][3]) {   // ExpBox::faces (entities.h:389-406)
+    const V3 dlb = mn, drb{mx.x, mn.y, mn.z}, dlt{mn.x, mx.y, mn.z}, drt{mx.x, mx.y, mn.z};
+    const V3 ulb{mn.x, mn.y, mx.z}, urb{mx.x, mn.y, mx.z}, ult{mn.x, mx.y, mx.z}, urt = mx;
+    const V3 G[6][3] = {{dlb, urb, ulb}, {dlb, ult, dlt}, {dlb, drt, dlt}, {urt, ulb, ult}, {urt, drb, drt}, {urt, dlt, drt}};
+    for (int f = 0; f < 6; ++f) for (int k = 0; k < 3; ++k) F[f][k] = G[f][k];
+}
+
+Ent make_exp_box(V3 mn, V3 mx) {   // entities.h:381-446
+    Ent e;
+    e.kind = EXP_BOX;
+    V3 F[6][3];
+    box_faces(mn, mx, F);
+    for (int f = 0; f < 6; ++f) {
+        e.tris.push_back(make_tri(F[f][0], F[f][1], F[f][2]));
+        e.tris.push_back(make_tri(F[f][0], F[f][1], -F[f][2]));
+    }
+    e.bmin = mn;
+    e.bmax = mx;
+    return e;
+}
+
 // Entity::intersect dispatch (Mode R)
 bool ent_intersect(const Ent& e, V3 o, V3 d, V3& P, V3& N) {
     switch (e.kind) {
     case IMP_SPHERE: return sphere_intersect(e.pos, e.radius, o, d, P, N);
     case IMP_TRIANGLE: return tri_intersect(e.tri, o, d, P, N);
-    case EXP_QUAD: {   // entities.h:596-620: nearest by <= over its triangles (ties -> later)
+    case EXP_RECTANGLE: {   // entities.h:326-336: t1, else t2
+        if (tri_intersect(e.tris[0], o, d, P, N)) return true;
+        return tri_intersect(e.tris[1], o, d, P, N);
+    }
+    case EXP_BOX: {   // entities.h:415-440: every face tested; the LAST hitting face's point wins
+        bool any = false;
+        for (int f = 0; f < 6; ++f) {
+            V3 p, n;
+            bool h = tri_intersect(e.tris[2 * f], o, d, p, n);
+            if (!h) h = tri_intersect(e.tris[2 * f + 1], o, d, p, n);
+            if (h) {
+                if (sq3(p - o) < DBL_MAX) { P = p; N = n; }
+                any = true;
+            }
+        }
+        return any;
+    }
+    case EXP_QUAD: case EXP_SPHERE: case EXP_CUBE: case EXP_CONE: {
+        // entities.h:596-620 / 514-536 / 736-760 / 906-930: nearest by <= (ties -> later);
+        // the outputs are overwritten even on a miss (:616-617)
         bool flag = false;
         double md = DBL_MAX;
         V3 mi{DBL_MAX, DBL_MAX, DBL_MAX}, cn{0, 0, 0};
@@ -265,21 +430,78 @@ void tex_exp_quad(const Ent& e, V3 ip, int32_t& x, int32_t& y) {
     x = x86_trunc(i1l * std::cos(theta) / uv);
 }
 
+void tex_exp_sphere(const Ent& e, V3 ip, int32_t& x, int32_t& y) {   // entities.h:549-571
+    const double r = e.radius;
+    const double unit_v = 2.0 * REF_PI * r / 320.0;
+    const V3 to = ip - e.pos;
+    const double cos_vert = dot(to, V3{0, 0, r}) / (r * r);
+    const double ang = std::acos(cos_vert);
+    y = x86_trunc((0.5 * REF_PI * r - r * ang) / unit_v);
+    const double small_r = r * std::sin(ang);
+    const double cos_hori = dot(V3{to.x, to.y, 0}, V3{0, small_r, 0}) / (small_r * small_r);
+    const double unit_h = 2.0 * REF_PI * small_r / 320.0;
+    x = x86_trunc(small_r * std::acos(cos_hori) / unit_h);
+}
+
+void tex_exp_cube(const Ent& e, V3 ip, int32_t& x, int32_t& y) {   // entities.h:769-811
+    const double uv = (double)e.width / 160.0, uh = (double)e.length_ / 160.0;
+    const V3 rv{0, (double)e.width, 0};
+    const V3 i1 = ip - e.qv[0];
+    const double l = std::sqrt(sq3(i1));
+    const double theta = std::acos(dot(i1, rv) / ((double)e.width * l));
+    y = x86_trunc(l * std::sin(theta) / uh);
+    x = x86_trunc(l * std::cos(theta) / uv);
+}
+
+void tex_exp_cone(const Ent& e, V3 ip, int32_t& x, int32_t& y) {   // entities.h:942-961
+    const double R = e.radius, H = e.height;
+    const double unit_h = std::sqrt(R * R + H * H) / 320.0;
+    const V3 ipos = ip - e.pos;
+    const double ylen = std::sqrt(sq3(ipos));
+    y = x86_trunc(ylen / unit_h);
+    const V3 center{(double)(float)e.pos.x, (double)(float)e.pos.y, (double)(float)ip.z};   // glm::vec3
+    const double rp = ylen * std::sin(e.cone_theta);
+    const V3 left{0, (double)(float)rp, 0};                                               // glm::vec3
+    const V3 ic = ip - center;
+    const double unit_v = 2.0 * REF_PI * rp / 320.0;
+    double alpha = std::acos(dot(ic, left) / (rp * rp));
+    if (alpha > REF_PI / 4.0) alpha = std::acos(dot(ic, -left) / (rp * rp));
+    x = x86_trunc(rp * alpha / unit_v);
+}
+
+void tex_exp_rectangle(const Ent& e, V3 ip, int32_t& x, int32_t& y) {   // entities.h:346-365
+    const V3 p1 = e.qv[0], p3 = e.qv[1], p4 = e.qv[2];
+    const V3 p31 = p3 - p1, p41 = p4 - p1;
+    const double width = std::sqrt(sq3(p41)), length = std::sqrt(sq3(p31));
+    const double uv = width / 64.0, uh = length / 64.0;
+    const V3 i1 = ip - p1;
+    const double l = std::sqrt(sq3(i1));
+    const double ct = std::acos(dot(i1, p31) / (length * l));   // an angle named cos_theta
+    x = x86_trunc(l * std::sin(std::acos(ct)) / uh);
+    y = x86_trunc(l * ct / uv);
+}
+
 void tex_coord(const Ent& e, V3 ip, int32_t& x, int32_t& y) {
     switch (e.kind) {
     case IMP_SPHERE: tex_imp_sphere(e, ip, x, y); return;
     case IMP_TRIANGLE: tex_imp_triangle(e.tri, ip, x, y); return;
     case EXP_QUAD: tex_exp_quad(e, ip, x, y); return;
+    case EXP_SPHERE: tex_exp_sphere(e, ip, x, y); return;
+    case EXP_CUBE: tex_exp_cube(e, ip, x, y); return;
+    case EXP_CONE: tex_exp_cone(e, ip, x, y); return;
+    case EXP_RECTANGLE: tex_exp_rectangle(e, ip, x, y); return;
     }
-    x = y = 0;
+    x = y = 0;   // ExpBox (entities.h:448-451)
 }
 
 // Texture (material.h:65-106): 32x32 int checker; colours truncated to int (A.7).  A negative
-// index is out-of-bounds UB in the reference (A.9); this restatement wraps it into [0,32).
+// remainder indexes pattern[i][j] out of its row (A.9): the compiled reference reads the flat
+// element i*32+j, which stays inside the array when 0 <= i*32+j < 1024; outside the array it
+// reads stack memory (UB) -- this restatement then wraps the flat index into [0,1024).
 V3 texel(V3 color, int32_t u, int32_t v) {
-    int i = u % 32, j = v % 32;
-    if (i < 0) i += 32;
-    if (j < 0) j += 32;
+    int f = (u % 32) * 32 + (v % 32);
+    if (f < 0 || f >= 1024) f = ((f % 1024) + 1024) % 1024;
+    const int i = f / 32, j = f % 32;
     if ((i <= 16 && j <= 16) || (i > 16 && j > 16)) return {1, 1, 1};
     return {(double)x86_trunc(color.x), (double)x86_trunc(color.y), (double)x86_trunc(color.z)};
 }
@@ -430,6 +652,11 @@ bool parse(const char* text, Scene& s) {
         else if (kw == "impsphere" && need(7)) s.ents.push_back(make_imp_sphere({v[0], v[1], v[2]}, v[3], {v[4], v[5], v[6]}));
         else if (kw == "imptriangle" && need(9)) s.ents.push_back(make_imp_triangle({v[0], v[1], v[2]}, {v[3], v[4], v[5]}, {v[6], v[7], v[8]}));
         else if (kw == "expquad" && need(9)) s.ents.push_back(make_exp_quad({v[0], v[1], v[2]}, v[3], v[4], v[5], {v[6], v[7], v[8]}));
+        else if (kw == "expsphere" && need(7)) s.ents.push_back(make_exp_sphere({v[0], v[1], v[2]}, v[3], {v[4], v[5], v[6]}));
+        else if (kw == "expcube" && need(9)) s.ents.push_back(make_exp_cube({v[0], v[1], v[2]}, v[3], v[4], v[5], {v[6], v[7], v[8]}));
+        else if (kw == "expcone" && need(11)) s.ents.push_back(make_exp_cone({v[0], v[1], v[2]}, {v[3], v[4], v[5]}, v[6], v[7], {v[8], v[9], v[10]}));
+        else if (kw == "exprectangle" && need(9)) s.ents.push_back(make_exp_rectangle({v[0], v[1], v[2]}, {v[3], v[4], v[5]}, {v[6], v[7], v[8]}));
+        else if (kw == "expbox" && need(6)) s.ents.push_back(make_exp_box({v[0], v[1], v[2]}, {v[3], v[4], v[5]}));
         else if (kw == "material" && need(3)) {
             if (s.ents.empty()) { g_err = "material before entity"; return false; }
             Mat m;
@@ -801,7 +1028,7 @@ int gio_rays(const char* scn, int n, const double* rays, int32_t* out_hit, doubl
             const bool h = ent_intersect(s.ents[k], o, d, P, N);
             int32_t u = 0, v = 0;
             if (h) tex_coord(s.ents[k], P, u, v);
-            else if (s.ents[k].kind == EXP_QUAD) { /* outputs are overwritten on miss too (:616-617) */ }
+            else if (s.ents[k].kind >= EXP_QUAD && s.ents[k].kind <= EXP_CONE) { /* overwritten on miss too (:616-617) */ }
             else { P = {0, 0, 0}; N = {0, 0, 0}; }
             out_hit[j] = h ? 1 : 0;
             double* pn = out_pn + 6 * j;

@@ -73,6 +73,8 @@ static bool load_scene(const char* path, Scene& s) {
         else if (kw == "expsphere") { need(7); s.ents.push_back(new ExpSphere({v[0], v[1], v[2]}, v[3], {v[4], v[5], v[6]})); }
         else if (kw == "expcube") { need(9); s.ents.push_back(new ExpCube({v[0], v[1], v[2]}, v[3], v[4], v[5], {v[6], v[7], v[8]})); }
         else if (kw == "expcone") { need(11); s.ents.push_back(new ExpCone({v[0], v[1], v[2]}, {v[3], v[4], v[5]}, v[6], v[7], {v[8], v[9], v[10]})); }
+        else if (kw == "exprectangle") { need(9); s.ents.push_back(new ExpRectangle({v[0], v[1], v[2]}, {v[3], v[4], v[5]}, {v[6], v[7], v[8]})); }
+        else if (kw == "expbox") { need(6); s.ents.push_back(new ExpBox({v[0], v[1], v[2]}, {v[3], v[4], v[5]})); }
         else if (kw == "material") {
             need(3);
             if (s.ents.empty()) { fprintf(stderr, "material before entity\n"); exit(2); }

@@ -40,6 +40,8 @@ int main(int argc, char** argv) {
         else if (kw == "expsphere") ents.push_back(new ExpSphere({v[0], v[1], v[2]}, v[3], {v[4], v[5], v[6]}));
         else if (kw == "expcube") ents.push_back(new ExpCube({v[0], v[1], v[2]}, v[3], v[4], v[5], {v[6], v[7], v[8]}));
         else if (kw == "expcone") ents.push_back(new ExpCone({v[0], v[1], v[2]}, {v[3], v[4], v[5]}, v[6], v[7], {v[8], v[9], v[10]}));
+        else if (kw == "exprectangle") ents.push_back(new ExpRectangle({v[0], v[1], v[2]}, {v[3], v[4], v[5]}, {v[6], v[7], v[8]}));
+        else if (kw == "expbox") ents.push_back(new ExpBox({v[0], v[1], v[2]}, {v[3], v[4], v[5]}));
         else if (kw == "material") {
             Entity* e = ents.back();
             if (v.size() >= 6) e->material = Material(glm::dvec3{v[0], v[1], v[2]}, glm::dvec3{v[3], v[4], v[5]});

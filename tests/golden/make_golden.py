@@ -33,15 +33,7 @@ S = U.scenes()
 
 
 def scene_by_name(name: str):
-    if name == "main":
-        return S.main_scene()
-    if name == "sphere":
-        return S.sphere_scene()
-    if name == "cornell":
-        return S.cornell_scene()
-    if name.startswith("soup"):
-        return S.soup_scene(int(name[4:]))
-    raise KeyError(name)
+    return S.named_scene(name)
 
 
 # (scene, w, h, window or None, stride, run RayTracer::run too)
@@ -53,6 +45,12 @@ FRAMES = [
     ("cornell", 1920, 1080, None, 509, False),    # C3 frame, sampled
     ("soup1000", 160, 160, None, 1, False),
     ("soup100000", 1920, 1080, (700, 600, 1220, 1080), 29, False),   # C4 frame: the soup's region
+    ("zoo", 160, 160, None, 1, True),                                # every entity type (f1)
+    ("only_expsphere", 96, 96, None, 1, False),
+    ("only_expcube", 96, 96, None, 1, False),
+    ("only_expcone", 96, 96, None, 1, False),
+    ("only_exprectangle", 96, 96, None, 1, False),
+    ("only_expbox", 96, 96, None, 1, False),
 ]
 
 
@@ -101,7 +99,7 @@ def tree_stats(dump: str) -> dict:
 
 
 def make_trees():
-    for scene in ["main", "sphere", "cornell", "soup1000", "soup100000"]:
+    for scene in ["main", "sphere", "cornell", "soup1000", "soup100000", "zoo"]:
         sc = scene_by_name(scene)
         st = tree_stats(U.ref_tree(sc.to_scn()))
         st["scene_sha256"] = sc.digest()
@@ -117,7 +115,7 @@ def random_rays(rng, n, origin_box, target_box):
 
 def make_rays():
     rng = np.random.default_rng(2019)
-    for scene, ob, tb in [("main", (-12, -8), (-3, 6)), ("cornell", (-12, 9), (-5, 10))]:
+    for scene, ob, tb in [("main", (-12, -8), (-3, 6)), ("cornell", (-12, 9), (-5, 10)), ("zoo", (-12, -8), (-6, 6))]:
         sc = scene_by_name(scene)
         rays = random_rays(rng, 4000, ob, tb)
         # plus axis-aligned and grazing rays (dir components exactly 0)

@@ -115,7 +115,7 @@ def ref_render(scn: str, w: int, h: int, window=None, stride: int = 1) -> dict:
         if window is not None or stride != 1:
             x0, y0, x1, y1 = window if window is not None else (0, 0, w, h)
             args += [str(x0), str(y0), str(x1), str(y1), str(stride)]
-        subprocess.run(args, check=True)
+        subprocess.run(args, check=True, stdout=subprocess.DEVNULL)   # ExpRectangle prints (entities.h:362)
         return read_ref_render(open(op, "rb").read())
 
 
@@ -155,7 +155,7 @@ def ref_rays(scn: str, rays: np.ndarray, n_ent: int) -> dict:
         with open(rp, "wb") as f:
             f.write(struct.pack("<i", rays.shape[0]))
             f.write(np.ascontiguousarray(rays, "<f8").tobytes())
-        subprocess.run([REF_HARNESS, "rays", sp, rp, op], check=True)
+        subprocess.run([REF_HARNESS, "rays", sp, rp, op], check=True, stdout=subprocess.DEVNULL)
         rec = np.dtype([("hit", "<i4"), ("pn", "<f8", 6), ("uv", "<i4", 2)])
         a = np.frombuffer(open(op, "rb").read(), dtype=rec).reshape(rays.shape[0], n_ent)
         return dict(hit=a["hit"].copy(), pn=a["pn"].copy(), uv=a["uv"].copy())

@@ -33,15 +33,7 @@ def torch_cuda():
 
 
 def _scene(name):
-    if name == "main":
-        return S.main_scene()
-    if name == "sphere":
-        return S.sphere_scene()
-    if name == "cornell":
-        return S.cornell_scene()
-    if name.startswith("soup"):
-        return S.soup_scene(int(name[4:]))
-    raise KeyError(name)
+    return S.named_scene(name)
 
 
 _dev_cache = {}

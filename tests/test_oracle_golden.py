@@ -17,15 +17,7 @@ GOLD = U.GOLDEN
 
 
 def _scene(name):
-    if name == "main":
-        return S.main_scene()
-    if name == "sphere":
-        return S.sphere_scene()
-    if name == "cornell":
-        return S.cornell_scene()
-    if name.startswith("soup"):
-        return S.soup_scene(int(name[4:]))
-    raise KeyError(name)
+    return S.named_scene(name)
 
 
 FRAMES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLD, "*.npz"))
@@ -46,6 +38,15 @@ def render_pixels(scn, w, h, xs, ys, **kw):
     return {k: v[idx] for k, v in o.items()}
 
 
+def texel_ub_mask(hit, uv):
+    """Pixels whose texture lookup reads outside the reference's 32x32 array (negative flat index
+    (u%32)*32 + v%32, C remainder semantics; texture.h / entities.h).  The reference reads stack memory
+    there (undefined behaviour), so those pixels carry no parity claim; the oracle and the device both
+    wrap the flat index into the array instead.  See DESIGN.md, texture UB."""
+    f = np.fmod(uv[:, 0], 32) * 32 + np.fmod(uv[:, 1], 32)
+    return (hit >= 0) & ((f < 0) | (f >= 1024))
+
+
 def test_frames_present():
     assert len(FRAMES) >= 6, FRAMES
 
@@ -58,15 +59,18 @@ def test_mode_r_bit_exact_vs_reference_golden(name):
     if meta["scene"] == "soup100000" and len(z["x"]) > 9000:
         pytest.skip("large")
     o = render_pixels(sc.to_scn(), meta["w"], meta["h"], z["x"], z["y"])
-    assert U.bits_equal(o["rgb"], z["rgb"]).all(), "fp64 radiance differs from the reference"
+    ok = ~texel_ub_mask(z["hit"], z["uv"])
+    assert ok.mean() > 0.9
+    assert U.bits_equal(o["rgb"], z["rgb"])[ok].all(), "fp64 radiance differs from the reference"
     assert (o["hit"] == z["hit"]).all()
     assert (o["uv"] == z["uv"]).all()
     assert (o["ncand"] == z["ncand"]).all()
     assert (o["nnode"] == z["nnode"]).all()
-    assert (o["q"] == z["q"]).all()
+    assert (o["q"] == z["q"])[ok].all()
     if "run_q" in z.files:   # RayTracer::run's own QImage (Qt) agrees with the restated quantisation
         q = z["q"].reshape(meta["h"], meta["w"], 3)
-        assert (z["run_q"] == q).all()
+        okq = ok.reshape(meta["h"], meta["w"])
+        assert (z["run_q"] == q)[okq].all()
 
 
 def test_main_scene_checksum_anchor():
@@ -77,7 +81,7 @@ def test_main_scene_checksum_anchor():
     assert int((q.sum(1) > 0).sum()) == 53182
 
 
-@pytest.mark.parametrize("scene", ["main", "sphere", "cornell", "soup1000"])
+@pytest.mark.parametrize("scene", ["main", "sphere", "cornell", "soup1000", "zoo"])
 def test_octree_structure_vs_reference(scene):
     import hashlib
     st = json.load(open(os.path.join(GOLD, f"tree_{scene}.json")))
@@ -91,7 +95,7 @@ def test_cornell_tree_stats():
     assert (st["n_nodes"], st["n_leaves"], st["max_depth"], st["n_reachable"]) == (81, 71, 4, 22)
 
 
-@pytest.mark.parametrize("scene", ["main", "cornell"])
+@pytest.mark.parametrize("scene", ["main", "cornell", "zoo"])
 def test_entity_intersect_kat(scene):
     z = np.load(os.path.join(GOLD, f"rays_{scene}.npz"))
     sc = _scene(scene)
@@ -117,6 +121,13 @@ def test_main_cpp_kat_values():
     assert np.array_equal(o["pn"][0, 0, 3:], kat["entity_test.normal"])
 
 
+def test_zoo_kat_covers_every_entity_kind():
+    z = np.load(os.path.join(GOLD, "rays_zoo.npz"))
+    kinds = [e.kind for e in S.zoo_scene().entities]
+    assert sorted(set(kinds)) == list(range(1, 9))
+    assert (z["hit"].sum(0) > 0).all(), "every zoo entity is hit by some KAT ray"
+
+
 def test_soup_generator_digest():
     d = json.load(open(os.path.join(GOLD, "soup_digest.json")))
     assert S.soup_digest(1000, 2019) == d["soup1000_vertices_sha256"]
@@ -134,9 +145,13 @@ def test_live_reference_random_scene():
         v = c + rng.uniform(-2, 2, (3, 3))
         s.imp_triangle(tuple(v[0]), tuple(v[1]), tuple(v[2]), tuple(rng.integers(0, 2, 3)))
     s.exp_quad((1.0, 0.5, -0.5), 3, 2, 0.7, (1, 1, 0))
+    s.exp_sphere(tuple(rng.uniform(-2, 4, 3)), 1.5, (1, 0, 1))
+    s.exp_cube(tuple(rng.uniform(-2, 4, 3)), 1.0, 2.0, 1.5, (0, 1, 1))
+    s.exp_cone(tuple(rng.uniform(-2, 4, 3)), (1.0, -0.5, 0.3), 3, 1.2, (1, 1, 0))
     scn = s.to_scn()
     r = U.ref_render(scn, 96, 96)
     o = U.oracle_render(scn, 96, 96)
-    assert U.bits_equal(r["rgb"], o["rgb"]).all()
+    ok = ~texel_ub_mask(r["hit"], r["uv"])
+    assert U.bits_equal(r["rgb"], o["rgb"])[ok].all()
     assert (r["hit"] == o["hit"]).all() and (r["nnode"] == o["nnode"]).all()
     assert U.ref_tree(scn) == U.oracle_tree(scn)
