@@ -32,6 +32,7 @@ from . import scenes as _scenes
 
 __all__ = [
     "GIError", "lib", "Camera", "Material", "Octree", "ImpSphere", "ImpTriangle", "ExpQuad",
+    "ExpSphere", "ExpCube", "ExpCone", "ExpRectangle", "ExpBox",
     "RayTracer", "DeviceScene", "MODE_R", "MODE_X", "STAT_RAYS", "STAT_NODES", "STAT_PRIMS",
     "STAT_PIXELS", "TILE",
 ]
@@ -202,6 +203,47 @@ class ExpQuad(_Entity):
 
     def __init__(self, pos, width, length, alpha, color):
         super().__init__((*pos, width, length, alpha, *color), None)
+
+
+class ExpSphere(_Entity):
+    """ExpSphere(pos, float radius, color) (entities.h:461): 10x10 stack/sector triangle mesh."""
+    kind = _scenes.EXP_SPHERE
+
+    def __init__(self, pos, radius, color):
+        super().__init__((*pos, radius, *color), None)
+
+
+class ExpCube(_Entity):
+    """ExpCube(pos, float width, float length, float height, color) (entities.h:652)."""
+    kind = _scenes.EXP_CUBE
+
+    def __init__(self, pos, width, length, height, color):
+        super().__init__((*pos, width, length, height, *color), None)
+
+
+class ExpCone(_Entity):
+    """ExpCone(pos, dir, float height, float radius, color) (entities.h:823).  As in the reference,
+    dir is kept but the mesh always points along (-1, 0, -10) (:825)."""
+    kind = _scenes.EXP_CONE
+
+    def __init__(self, pos, dir, height, radius, color):
+        super().__init__((*pos, *dir, height, radius, *color), None)
+
+
+class ExpRectangle(_Entity):
+    """ExpRectangle(p1, p2, p3) (entities.h:310); requires (p1-p3).(p2-p3) == 0 (:312)."""
+    kind = _scenes.EXP_RECTANGLE
+
+    def __init__(self, p1, p2, p3):
+        super().__init__((*p1, *p2, *p3), None)
+
+
+class ExpBox(_Entity):
+    """ExpBox(min, max) (entities.h:381); getTextureCoord is (0, 0)."""
+    kind = _scenes.EXP_BOX
+
+    def __init__(self, mn, mx):
+        super().__init__((*mn, *mx), None)
 
 
 class Octree:

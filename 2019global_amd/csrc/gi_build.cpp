@@ -4,6 +4,12 @@
 //   ImpSphere   entities.h:45-47, bbox :98-99 (member-init while pos == {0,0,0})
 //   ImpTriangle entities.h:138-148, bbox :251-275 (+0.01 on max.z, +1e-5 on flat axes, A.13)
 //   ExpQuad     entities.h:581-590 (float trig on the float alpha), bbox :623-624 (A.5)
+//   ExpSphere   entities.h:461-506 (fp32 stack/sector trig, vertices offset by -pos; intersect()
+//               skips triangle 0, :520), bbox origin-centred (A.5)
+//   ExpCube     entities.h:652-727 (12 triangles, texture frame vertices[0])
+//   ExpCone     entities.h:823-899 (fixed axis (-1,0,-10), fp32 glm::mat3 rotations, 50 sectors)
+//   ExpRectangle entities.h:310-340 (t1 = (p1,p2,p3), t2 = (p1,p2,-p3): p4 = -p3, A.4)
+//   ExpBox      entities.h:381-446 (6 faces x (t1, t2 with the third corner negated))
 // then pushed into the reference octree with Octree::push_back semantics (octree.h:121-230,
 // bbox.h:25-39), including the silent drop (A.14) and entities kept only at the split node (A.6).
 #include <algorithm>
@@ -86,6 +92,158 @@ bool build_entity(const gi_entity_desc& d, BEnt& e, std::string& err) {
         st3(e.rec.qv1, q[1]);
         e.bmin = v3((float)(0.0 - hw), (float)(0.0 - hl), (float)0.0);
         e.bmax = v3((float)(0.0 + hw), (float)(0.0 + hl), (float)(0.0 + (0.0 + hw) * sa));
+        break;
+    }
+    case GI_EXP_SPHERE: {
+        e.rec = blank_rec(K_EXP_SPHERE);
+        set_color(e.rec, a + 4);
+        const V3 pos = v3(a[0], a[1], a[2]);
+        st3(e.rec.pos, pos);
+        const float rad = (float)a[3];
+        e.rec.radius = rad;
+        const int nsec = 10, nstk = 10;
+        const float sec_step = (float)(2 * REF_PI / nsec), stk_step = (float)(REF_PI / nstk);
+        std::vector<V3> vert;
+        for (int i = 0; i <= nstk; ++i) {
+            const float stk = (float)(REF_PI / 2 - (double)(i * stk_step));
+            const float xy = rad * cosf(stk);
+            const float z = (float)((double)(rad * sinf(stk)) - pos.z);
+            for (int j = 0; j <= nsec; ++j) {
+                const float sec = j * sec_step;
+                vert.push_back(v3((float)((double)(xy * cosf(sec)) - pos.x), (float)((double)(xy * sinf(sec)) - pos.y), z));
+            }
+        }
+        bool first = true;   // intersect() starts at triangle 1 (entities.h:520)
+        for (int i = 0; i < nstk; ++i) {
+            int k1 = i * (nsec + 1), k2 = k1 + nsec + 1;
+            for (int j = 0; j < nsec; ++j, ++k1, ++k2) {
+                TriRec t;
+                if (i != 0) {
+                    make_tri(vert[k1], vert[k2], vert[k1 + 1], t);
+                    if (!first) e.tris.push_back(t);
+                    first = false;
+                }
+                if (i != nstk - 1) {
+                    make_tri(vert[k1 + 1], vert[k2], vert[k2 + 1], t);
+                    if (!first) e.tris.push_back(t);
+                    first = false;
+                }
+            }
+        }
+        const double r = rad;
+        e.bmin = v3((float)(0.0 - r), (float)(0.0 - r), (float)(0.0 - r));
+        e.bmax = v3((float)(0.0 + r), (float)(0.0 + r), (float)(0.0 + r));
+        break;
+    }
+    case GI_EXP_CUBE: {
+        e.rec = blank_rec(K_EXP_CUBE);
+        set_color(e.rec, a + 6);
+        const V3 pos = v3(a[0], a[1], a[2]);
+        st3(e.rec.pos, pos);
+        const float w = (float)a[3], l = (float)a[4], h = (float)a[5];
+        e.rec.width = w; e.rec.length = l; e.rec.height = h;
+        const float hw = w / 2, hl = l / 2, hh = h / 2;
+        const V3 c[8] = {v3(pos.x - hw, pos.y - hl, pos.z - hh), v3(pos.x - hw, pos.y - hl, pos.z + hh),
+                         v3(pos.x + hw, pos.y - hl, pos.z - hh), v3(pos.x + hw, pos.y - hl, pos.z + hh),
+                         v3(pos.x - hw, pos.y + hl, pos.z + hh), v3(pos.x - hw, pos.y + hl, pos.z - hh),
+                         v3(pos.x + hw, pos.y + hl, pos.z - hh), v3(pos.x + hw, pos.y + hl, pos.z + hh)};
+        static const int F[12][3] = {{0, 1, 2}, {3, 1, 2}, {4, 5, 7}, {7, 5, 6}, {1, 0, 4}, {4, 0, 5},
+                                     {3, 7, 2}, {7, 6, 2}, {1, 4, 3}, {3, 4, 7}, {0, 5, 2}, {2, 5, 6}};
+        for (const auto& f : F) {
+            TriRec t;
+            make_tri(c[f[0]], c[f[1]], c[f[2]], t);
+            e.tris.push_back(t);
+        }
+        st3(e.rec.qv0, c[0]);
+        e.bmin = v3((float)(0.0 - hw), (float)(0.0 - hl), (float)(0.0 - hh));
+        e.bmax = v3((float)(0.0 + hw), (float)(0.0 + hl), (float)(0.0 + hh));
+        break;
+    }
+    case GI_EXP_CONE: {
+        e.rec = blank_rec(K_EXP_CONE);
+        set_color(e.rec, a + 8);
+        const V3 pos = v3(a[0], a[1], a[2]);
+        st3(e.rec.pos, pos);
+        const float h = (float)a[6], rad = (float)a[7];
+        e.rec.height = h; e.rec.radius = rad;
+        const V3 axis = normalize(v3(-1, 0, -10));   // entities.h:825 overrides the argument
+        // glm::mat3 (fp32, column-major m[col][row]) rotations about x then y, applied to a vec3
+        float rx[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}}, ry[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+        const V3 xd = v3(0, axis.y, axis.z);
+        if (!(xd.x == 0 && xd.y == 0 && xd.z == 0)) {
+            const double ang = (axis.y < 0 ? 1.0 : -1.0) * std::acos(dot(normalize(xd), v3(0, 0, -1)));
+            rx[1][1] = (float)std::cos(ang); rx[1][2] = (float)(-std::sin(ang));
+            rx[2][1] = (float)std::sin(ang); rx[2][2] = (float)std::cos(ang);
+        }
+        const V3 yd = v3(axis.x, 0, -std::sqrt(axis.z * axis.z + axis.y * axis.y));
+        if (!(yd.x == 0 && yd.y == 0 && yd.z == 0)) {
+            const double ang = (axis.x > 0 ? 1.0 : -1.0) * std::acos(dot(normalize(yd), v3(0, 0, -1)));
+            ry[0][0] = (float)std::cos(ang); ry[0][2] = (float)std::sin(ang);
+            ry[2][0] = (float)(-std::sin(ang)); ry[2][2] = (float)std::cos(ang);
+        }
+        auto rot = [](const float m[3][3], V3 v) {
+            const float x = (float)v.x, y = (float)v.y, z = (float)v.z;
+            return v3(m[0][0] * x + m[1][0] * y + m[2][0] * z, m[0][1] * x + m[1][1] * y + m[2][1] * z,
+                      m[0][2] * x + m[1][2] * y + m[2][2] * z);
+        };
+        std::vector<V3> rim;
+        const double nsub = 50.0;
+        for (int i = 0; i <= nsub; ++i) {
+            const float deg = (float)(i * 360.0 / nsub);
+            V3 p = v3(pos.x + (double)rad * std::cos((double)deg * REF_PI / 180.0),
+                      pos.y + (double)rad * std::sin((double)deg * REF_PI / 180.0), pos.z - (double)h);
+            p = rot(ry, rot(rx, p - pos)) + pos;
+            rim.push_back(p);
+        }
+        const V3 base = pos + normalize(axis) * (double)h;
+        for (size_t i = 0; i + 1 < rim.size(); ++i) {
+            TriRec t;
+            make_tri(pos, rim[i], rim[i + 1], t);
+            e.tris.push_back(t);
+            make_tri(base, rim[i], rim[i + 1], t);
+            e.tris.push_back(t);
+        }
+        const double theta = (double)std::atan(rad / h);   // float atan (entities.h:950)
+        e.rec.sin_theta = std::sin(theta);
+        e.bmin = v3((float)(0.0 - (double)rad), (float)(0.0 - (double)rad), (float)(0.0 - (double)h));
+        e.bmax = v3((float)(0.0 + (double)rad), (float)(0.0 + (double)rad), (float)0.0);
+        break;
+    }
+    case GI_EXP_RECTANGLE: {
+        e.rec = blank_rec(K_EXP_RECTANGLE);
+        const V3 p1 = v3(a[0], a[1], a[2]), p2 = v3(a[3], a[4], a[5]), p3 = v3(a[6], a[7], a[8]);
+        if (dot(p1 - p3, p2 - p3) != 0.0) {   // the reference asserts a right angle at p3 (entities.h:312)
+            err = "ExpRectangle: (p1-p3).(p2-p3) != 0";
+            return false;
+        }
+        const V3 p4 = -p3;
+        TriRec t;
+        make_tri(p1, p2, p3, t);
+        e.tris.push_back(t);
+        make_tri(p1, p2, p4, t);
+        e.tris.push_back(t);
+        st3(e.rec.qv0, p1); st3(e.rec.qv1, p3); st3(e.rec.qv2, p4);
+        st3(e.rec.pos, 0.5 * (p1 + p2));
+        e.bmin = v3(smin(p1.x, p2.x), smin(p1.y, p2.y), smin(p1.z, p2.z));
+        e.bmax = v3(smax(p1.x, p2.x), smax(p1.y, p2.y), smax(p1.z, p2.z));
+        break;
+    }
+    case GI_EXP_BOX: {
+        e.rec = blank_rec(K_EXP_BOX);
+        const V3 mn = v3(a[0], a[1], a[2]), mx = v3(a[3], a[4], a[5]);
+        const V3 dlb = mn, drb = v3(mx.x, mn.y, mn.z), dlt = v3(mn.x, mx.y, mn.z), drt = v3(mx.x, mx.y, mn.z);
+        const V3 ulb = v3(mn.x, mn.y, mx.z), urb = v3(mx.x, mn.y, mx.z), ult = v3(mn.x, mx.y, mx.z), urt = mx;
+        const V3 face[6][3] = {{dlb, urb, ulb}, {dlb, ult, dlt}, {dlb, drt, dlt},
+                               {urt, ulb, ult}, {urt, drb, drt}, {urt, dlt, drt}};   // ExpBox::faces (:389-406)
+        for (const auto& f : face) {
+            TriRec t;
+            make_tri(f[0], f[1], f[2], t);
+            e.tris.push_back(t);
+            make_tri(f[0], f[1], -f[2], t);
+            e.tris.push_back(t);
+        }
+        e.bmin = mn;
+        e.bmax = mx;
         break;
     }
     default:

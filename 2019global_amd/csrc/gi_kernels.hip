@@ -49,7 +49,31 @@ __device__ bool ent_hit(const DevScene& sc, const REnt& e, V3 o, V3 d, V3& P, V3
         ++nprim;
         return tri_hit(sc.tris[e.tri_first], o, d, P, N);
     }
-    // ExpQuad::intersect (entities.h:596-620): nearest by <= over its triangles, ties -> later
+    if (e.kind == K_EXP_RECTANGLE) {   // entities.h:326-336: t1, else t2
+        nprim += 1;
+        if (tri_hit(sc.tris[e.tri_first], o, d, P, N)) return true;
+        nprim += 1;
+        return tri_hit(sc.tris[e.tri_first + 1], o, d, P, N);
+    }
+    if (e.kind == K_EXP_BOX) {   // entities.h:415-440: every face; the LAST hitting face's point wins
+        bool any = false;
+        for (int f = 0; f < 6; ++f) {
+            V3 p, n;
+            ++nprim;
+            bool h = tri_hit(sc.tris[e.tri_first + 2 * f], o, d, p, n);
+            if (!h) {
+                ++nprim;
+                h = tri_hit(sc.tris[e.tri_first + 2 * f + 1], o, d, p, n);
+            }
+            if (h) {
+                if (sq3(p - o) < DBL_MAX) { P = p; N = n; }
+                any = true;
+            }
+        }
+        return any;
+    }
+    // ExpQuad / ExpSphere / ExpCube / ExpCone ::intersect (entities.h:596-620, 514-536, 736-760,
+    // 906-930): nearest by <= over the triangles (ties -> later); outputs overwritten on a miss
     bool flag = false;
     double md = DBL_MAX;
     V3 mi = v3(DBL_MAX, DBL_MAX, DBL_MAX), cn = v3(0, 0, 0);
@@ -93,7 +117,7 @@ __device__ void tex_coord(const DevScene& sc, const REnt& e, V3 ip, int32_t& x, 
         const double uv = vl / 160.0, uh = hl / 160.0;
         y = x86_trunc(i1l / uh);
         x = x86_trunc(ixl / uv);
-    } else {
+    } else if (e.kind == K_EXP_QUAD) {
         const double uv = (double)e.width / 160.0, uh = (double)e.length / 160.0;
         const V3 rv = ld3(e.qv0) - ld3(e.qv1);
         const V3 i1 = ip - ld3(e.qv1);
@@ -101,6 +125,48 @@ __device__ void tex_coord(const DevScene& sc, const REnt& e, V3 ip, int32_t& x, 
         const double theta = acos(dot(i1, rv) / ((double)e.width * i1l));
         y = x86_trunc(i1l * sin(theta) / uh);
         x = x86_trunc(i1l * cos(theta) / uv);
+    } else if (e.kind == K_EXP_SPHERE) {   // entities.h:549-571 (latitude measured from the equator)
+        const double r = e.radius;
+        const double unit_v = 2.0 * REF_PI * r / 320.0;
+        const V3 to = ip - ld3(e.pos);
+        const double ang = acos(dot(to, v3(0, 0, r)) / (r * r));
+        y = x86_trunc((0.5 * REF_PI * r - r * ang) / unit_v);
+        const double small_r = r * sin(ang);
+        const double cos_hori = dot(v3(to.x, to.y, 0), v3(0, small_r, 0)) / (small_r * small_r);
+        const double unit_h = 2.0 * REF_PI * small_r / 320.0;
+        x = x86_trunc(small_r * acos(cos_hori) / unit_h);
+    } else if (e.kind == K_EXP_CUBE) {     // entities.h:769-811
+        const double uv = (double)e.width / 160.0, uh = (double)e.length / 160.0;
+        const V3 i1 = ip - ld3(e.qv0);
+        const double l = gsqrt(sq3(i1));
+        const double theta = acos(dot(i1, v3(0, (double)e.width, 0)) / ((double)e.width * l));
+        y = x86_trunc(l * sin(theta) / uh);
+        x = x86_trunc(l * cos(theta) / uv);
+    } else if (e.kind == K_EXP_CONE) {     // entities.h:942-961
+        const double R = e.radius, H = e.height;
+        const double unit_h = gsqrt(R * R + H * H) / 320.0;
+        const V3 pos = ld3(e.pos);
+        const double ylen = gsqrt(sq3(ip - pos));
+        y = x86_trunc(ylen / unit_h);
+        const V3 center = v3((float)pos.x, (float)pos.y, (float)ip.z);   // glm::vec3
+        const double rp = ylen * e.sin_theta;
+        const V3 left = v3(0, (float)rp, 0);                              // glm::vec3
+        const V3 ic = ip - center;
+        const double unit_v = 2.0 * REF_PI * rp / 320.0;
+        double alpha = acos(dot(ic, left) / (rp * rp));
+        if (alpha > REF_PI / 4.0) alpha = acos(dot(ic, -left) / (rp * rp));
+        x = x86_trunc(rp * alpha / unit_v);
+    } else if (e.kind == K_EXP_RECTANGLE) {   // entities.h:346-365 (acos of an angle, as written)
+        const V3 p1 = ld3(e.qv0), p31 = ld3(e.qv1) - p1, p41 = ld3(e.qv2) - p1;
+        const double width = gsqrt(sq3(p41)), length = gsqrt(sq3(p31));
+        const V3 i1 = ip - p1;
+        const double l = gsqrt(sq3(i1));
+        const double ct = acos(dot(i1, p31) / (length * l));
+        x = x86_trunc(l * sin(acos(ct)) / (length / 64.0));
+        y = x86_trunc(l * ct / (width / 64.0));
+    } else {   // ExpBox: (0, 0) (entities.h:448-451)
+        x = 0;
+        y = 0;
     }
 }
 
@@ -346,13 +412,55 @@ __device__ void x_texcoord(const DevScene& sc, const REnt& e, V3 ip, int32_t& x,
         const double hl = gsqrt(sq3(0.5 * ((-p32) + (-p31))));
         y = x86_trunc(i1l / (hl / 160.0));
         x = x86_trunc(ixl / (vl / 160.0));
-    } else {
+    } else if (e.kind == K_EXP_QUAD) {
         const double uv = (double)e.width / 160.0, uh = (double)e.length / 160.0;
         const V3 rv = ld3(e.qv0) - ld3(e.qv1), i1 = ip - ld3(e.qv1);
         const double i1l = gsqrt(sq3(i1));
         const double c = dot(i1, rv) / ((double)e.width * i1l);
         y = x86_trunc(i1l * mx_sin_acos(c) / uh);
         x = x86_trunc(i1l * mx_cos_acos(c) / uv);
+    } else if (e.kind == K_EXP_SPHERE) {
+        const double r = e.radius;
+        const double unit_v = 2.0 * REF_PI * r / 320.0;
+        const V3 to = ip - ld3(e.pos);
+        const double cv = dot(to, v3(0, 0, r)) / (r * r);
+        y = x86_trunc((0.5 * REF_PI * r - r * mx_acos(cv)) / unit_v);
+        const double small_r = r * mx_sin_acos(cv);
+        const double ch = dot(v3(to.x, to.y, 0), v3(0, small_r, 0)) / (small_r * small_r);
+        const double unit_h = 2.0 * REF_PI * small_r / 320.0;
+        x = x86_trunc(small_r * mx_acos(ch) / unit_h);
+    } else if (e.kind == K_EXP_CUBE) {
+        const double uv = (double)e.width / 160.0, uh = (double)e.length / 160.0;
+        const V3 i1 = ip - ld3(e.qv0);
+        const double l = gsqrt(sq3(i1));
+        const double c = dot(i1, v3(0, (double)e.width, 0)) / ((double)e.width * l);
+        y = x86_trunc(l * mx_sin_acos(c) / uh);
+        x = x86_trunc(l * mx_cos_acos(c) / uv);
+    } else if (e.kind == K_EXP_CONE) {
+        const double R = e.radius, H = e.height;
+        const double unit_h = gsqrt(R * R + H * H) / 320.0;
+        const V3 pos = ld3(e.pos);
+        const double ylen = gsqrt(sq3(ip - pos));
+        y = x86_trunc(ylen / unit_h);
+        const V3 center = v3((float)pos.x, (float)pos.y, (float)ip.z);
+        const double rp = ylen * e.sin_theta;
+        const V3 left = v3(0, (float)rp, 0);
+        const V3 ic = ip - center;
+        const double unit_v = 2.0 * REF_PI * rp / 320.0;
+        double alpha = mx_acos(dot(ic, left) / (rp * rp));
+        if (alpha > REF_PI / 4.0) alpha = mx_acos(dot(ic, -left) / (rp * rp));
+        x = x86_trunc(rp * alpha / unit_v);
+    } else if (e.kind == K_EXP_RECTANGLE) {
+        const V3 p1 = ld3(e.qv0), p31 = ld3(e.qv1) - p1, p41 = ld3(e.qv2) - p1;
+        const double width = gsqrt(sq3(p41)), length = gsqrt(sq3(p31));
+        const V3 i1 = ip - p1;
+        const double l = gsqrt(sq3(i1));
+        const double ct = mx_acos(dot(i1, p31) / (length * l));
+        x = x86_trunc(l * mx_sin_acos(ct) / (length / 64.0));
+        y = x86_trunc(l * ct / (width / 64.0));
+    } else {
+        x = 0;
+        y = 0;
     }
 }
 

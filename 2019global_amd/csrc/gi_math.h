@@ -234,9 +234,12 @@ GI_HD double mx_powi(double x, int p) {
 // Texture (material.h:65-106): 32x32 int checker, colour truncated to int (A.7); a negative
 // index (out-of-bounds UB in the reference, A.9) wraps into [0,32).
 GI_HD V3 texel(V3 color, int32_t u, int32_t v) {
-    int i = u % 32, j = v % 32;
-    if (i < 0) i += 32;
-    if (j < 0) j += 32;
+    // pattern[u % 32][v % 32] with C remainders: the compiled reference reads the FLAT element
+    // (u%32)*32 + v%32 of the 32x32 array; inside [0,1024) that is exact, outside it reads stack
+    // memory (UB, no parity claim) and this path wraps the flat index into the array (oracle: same).
+    int f = (u % 32) * 32 + (v % 32);
+    if (f < 0 || f >= 1024) f = ((f % 1024) + 1024) % 1024;
+    const int i = f >> 5, j = f & 31;
     if ((i <= 16 && j <= 16) || (i > 16 && j > 16)) return v3(1, 1, 1);
     return v3((double)x86_trunc(color.x), (double)x86_trunc(color.y), (double)x86_trunc(color.z));
 }

@@ -15,7 +15,8 @@
 
 namespace gi {
 
-enum EntKind : int32_t { K_IMP_SPHERE = 1, K_IMP_TRIANGLE = 2, K_EXP_QUAD = 3 };
+enum EntKind : int32_t { K_IMP_SPHERE = 1, K_IMP_TRIANGLE = 2, K_EXP_QUAD = 3, K_EXP_SPHERE = 4, K_EXP_CUBE = 5,
+                         K_EXP_CONE = 6, K_EXP_RECTANGLE = 7, K_EXP_BOX = 8 };
 
 struct RNode {             // 64 bytes
     double mn[3], mx[3];
@@ -26,15 +27,19 @@ struct RNode {             // 64 bytes
 };
 static_assert(sizeof(RNode) == 64, "RNode layout");
 
-struct REnt {              // 160 bytes
+struct REnt {              // 208 bytes
     int32_t kind, tri_first, tri_count, pad0;
-    double pos[3];         // ImpSphere centre / ExpQuad pos
+    double pos[3];         // ImpSphere / ExpSphere / ExpCone centre, ExpQuad / ExpCube pos
     float radius, width, length, alpha;
-    double qv0[3], qv1[3]; // ExpQuad vertices[0], [1] (texture frame, entities.h:634-635)
+    double qv0[3], qv1[3], qv2[3];   // texture frames: ExpQuad vertices[0], [1] (entities.h:634-635);
+                                     // ExpCube vertices[0] (:772); ExpRectangle p1, p3, p4 (:346-350)
     double color[3], shader[3];
     double spec_pow;
+    float height, pad1;    // ExpCube / ExpCone height
+    double sin_theta;      // ExpCone: sin(cone_theta), cone_theta = float atan(radius/height) (:950-953)
+    double pad2;
 };
-static_assert(sizeof(REnt) == 160, "REnt layout");
+static_assert(sizeof(REnt) == 208, "REnt layout");
 
 // Mode X primitive: triangle (v0, e1, e2, n) or sphere (c, r)
 struct XPrim {             // 112 bytes

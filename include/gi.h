@@ -47,9 +47,12 @@ typedef enum gi_entity_kind {
     GI_IMP_SPHERE = 1,   /* ImpSphere(pos, float radius, color)              entities.h:45  args: px py pz r cr cg cb            */
     GI_IMP_TRIANGLE = 2, /* ImpTriangle(p1, p2, p3) (material: red)          entities.h:138 args: p1 p2 p3 (9)                   */
     GI_EXP_QUAD = 3,     /* ExpQuad(pos, float w, float l, float alpha, col) entities.h:581 args: px py pz w l alpha cr cg cb    */
-    GI_EXP_SPHERE = 4,   /* reserved */
-    GI_EXP_CUBE = 5,     /* reserved */
-    GI_EXP_CONE = 6      /* reserved */
+    GI_EXP_SPHERE = 4,   /* ExpSphere(pos, float radius, color)              entities.h:461 args: px py pz r cr cg cb            */
+    GI_EXP_CUBE = 5,     /* ExpCube(pos, float w, float l, float h, color)   entities.h:652 args: px py pz w l h cr cg cb        */
+    GI_EXP_CONE = 6,     /* ExpCone(pos, dir, float h, float r, color)       entities.h:823 args: px py pz dx dy dz h r cr cg cb */
+                         /*   (dir is stored but unused: the reference cone always points along (-1,0,-10), :825)           */
+    GI_EXP_RECTANGLE = 7,/* ExpRectangle(p1, p2, p3) (material: red)         entities.h:310 args: p1 p2 p3 (9)                   */
+    GI_EXP_BOX = 8       /* ExpBox(min, max) (material: red)                 entities.h:381 args: min max (6)                    */
 } gi_entity_kind;
 
 typedef struct gi_entity_desc {

@@ -110,6 +110,29 @@ class RayTracer {
             const double a[9] = {q->pos.x, q->pos.y, q->pos.z, (double)q->width, (double)q->length, (double)q->alpha,
                                  q->material.color.x, q->material.color.y, q->material.color.z};
             std::copy(a, a + 9, d.args);
+        } else if (auto* es = dynamic_cast<const ExpSphere*>(e)) {
+            d.kind = GI_EXP_SPHERE;
+            const double a[7] = {es->pos.x, es->pos.y, es->pos.z, (double)es->radius,
+                                 es->material.color.x, es->material.color.y, es->material.color.z};
+            std::copy(a, a + 7, d.args);
+        } else if (auto* c = dynamic_cast<const ExpCube*>(e)) {
+            d.kind = GI_EXP_CUBE;
+            const double a[9] = {c->pos.x, c->pos.y, c->pos.z, (double)c->width, (double)c->length, (double)c->height,
+                                 c->material.color.x, c->material.color.y, c->material.color.z};
+            std::copy(a, a + 9, d.args);
+        } else if (auto* k = dynamic_cast<const ExpCone*>(e)) {
+            d.kind = GI_EXP_CONE;   // the member dir holds the constructor argument (entities.h:823)
+            const double a[11] = {k->pos.x, k->pos.y, k->pos.z, k->dir.x, k->dir.y, k->dir.z, (double)k->height,
+                                  (double)k->radius, k->material.color.x, k->material.color.y, k->material.color.z};
+            std::copy(a, a + 11, d.args);
+        } else if (auto* r = dynamic_cast<const ExpRectangle*>(e)) {
+            d.kind = GI_EXP_RECTANGLE;
+            const double a[9] = {r->p1.x, r->p1.y, r->p1.z, r->p2.x, r->p2.y, r->p2.z, r->p3.x, r->p3.y, r->p3.z};
+            std::copy(a, a + 9, d.args);
+        } else if (auto* b = dynamic_cast<const ExpBox*>(e)) {
+            d.kind = GI_EXP_BOX;
+            const double a[6] = {b->min.x, b->min.y, b->min.z, b->max.x, b->max.y, b->max.z};
+            std::copy(a, a + 6, d.args);
         } else {
             return false;
         }
@@ -122,7 +145,7 @@ class RayTracer {
         for (const Entity* e : _scene->entities()) {
             gi_entity_desc d;
             if (!describe(e, d)) {
-                std::fprintf(stderr, "gi: entity type not supported by the GPU path yet\n");
+                std::fprintf(stderr, "gi: unknown entity type (not one of entities.h's eight)\n");
                 return false;
             }
             ents.push_back(d);

@@ -4,10 +4,13 @@
 // ImpSphere / ExpQuad / Image classes, then renders it with gi_dropin/raytracer.h (same class
 // name and API as the reference's RayTracer), copying the RayTracer by value as Gui/Viewer do
 // (gui.h:19,35).  Writes the RGB888 frame the Viewer would paint.
-//   dropin_demo <w> <h> <out.rgb>
+// With "zoo" it builds the every-entity scene of scenes.zoo_scene() instead (entities.h's eight
+// entity classes, constructed by the reference's own constructors).
+//   dropin_demo <w> <h> <out.rgb> [zoo]
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 
 #include "raytracer.h"   // resolves to include/gi_dropin/raytracer.h (first on the include path)
 
@@ -18,12 +21,26 @@ int main(int argc, char** argv) {
     glm::dvec3 light{-10, 10, 10};
     RayTracer raytracer(camera, light);
     Octree scene({-20, -20, -20}, {20, 20, 20});
-    ImpSphere* s2 = new ImpSphere(glm::dvec3{3, 4, 4}, 2, {1, 0, 0});
-    ImpSphere* s3 = new ImpSphere(glm::dvec3{4, -4, 4}, 2, {0, 0, 1});
-    ExpQuad* q = new ExpQuad(glm::dvec3{0, 0, 0}, 2, 3, (90.0 * M_PI / 180.0), {1, 2, 3});
-    scene.push_back(q);
-    scene.push_back(s2);
-    scene.push_back(s3);
+    if (argc > 4 && std::string(argv[4]) == "zoo") {
+        scene.push_back(new ExpSphere(glm::dvec3{-2, 0, 0}, 2, {0, 1, 0}));
+        scene.push_back(new ExpCube(glm::dvec3{0, 0, 0}, 2, 2, 2, {1, 0, 0}));
+        scene.push_back(new ExpCone(glm::dvec3{0, 0, 2}, glm::dvec3{-1, 1, -3}, 5, 3, {1, 1, 0}));
+        scene.push_back(new ExpQuad(glm::dvec3{0, 0, 0}, 2, 3, (90.0 * M_PI / 180.0), {1, 2, 3}));
+        scene.push_back(new ImpSphere(glm::dvec3{3, 4, 4}, 2, {1, 0, 0}));
+        ImpTriangle* t = new ImpTriangle(glm::dvec3{0, 3, 2}, glm::dvec3{3, 3, -4}, glm::dvec3{3, -3, -4});
+        t->material = Material(glm::dvec3{0, 1, 1}, glm::dvec3{0.1, 0.7, 1.0});
+        t->material.specular_power = 5;
+        scene.push_back(t);
+        scene.push_back(new ExpRectangle(glm::dvec3{1, -6, -3}, glm::dvec3{1, -3, 0}, glm::dvec3{1, -6, 0}));
+        scene.push_back(new ExpBox(glm::dvec3{2, 4, -5}, glm::dvec3{4, 6, -3}));
+    } else {
+        ImpSphere* s2 = new ImpSphere(glm::dvec3{3, 4, 4}, 2, {1, 0, 0});
+        ImpSphere* s3 = new ImpSphere(glm::dvec3{4, -4, 4}, 2, {0, 0, 1});
+        ExpQuad* q = new ExpQuad(glm::dvec3{0, 0, 0}, 2, 3, (90.0 * M_PI / 180.0), {1, 2, 3});
+        scene.push_back(q);
+        scene.push_back(s2);
+        scene.push_back(s3);
+    }
     raytracer.setScene(&scene);
     RayTracer viewer_copy = raytracer;
     viewer_copy.start();

@@ -865,7 +865,45 @@ void mx_texcoord(const Ent& e, V3 ip, int32_t& x, int32_t& y) {
         const double c = dot(i1, rv) / ((double)e.width * i1l);
         y = x86_trunc(i1l * mx_sin_acos(c) / uh);
         x = x86_trunc(i1l * mx_cos_acos(c) / uv);
-    } else x = y = 0;
+    } else if (e.kind == EXP_SPHERE) {   // tex_exp_sphere with the Mode X acos
+        const double r = e.radius;
+        const double unit_v = 2.0 * REF_PI * r / 320.0;
+        const V3 to = ip - e.pos;
+        const double cv = dot(to, V3{0, 0, r}) / (r * r);
+        y = x86_trunc((0.5 * REF_PI * r - r * mx_acos(cv)) / unit_v);
+        const double small_r = r * mx_sin_acos(cv);
+        const double ch = dot(V3{to.x, to.y, 0}, V3{0, small_r, 0}) / (small_r * small_r);
+        const double unit_h = 2.0 * REF_PI * small_r / 320.0;
+        x = x86_trunc(small_r * mx_acos(ch) / unit_h);
+    } else if (e.kind == EXP_CUBE) {
+        const double uv = (double)e.width / 160.0, uh = (double)e.length_ / 160.0;
+        const V3 i1 = ip - e.qv[0];
+        const double l = std::sqrt(sq3(i1));
+        const double c = dot(i1, V3{0, (double)e.width, 0}) / ((double)e.width * l);
+        y = x86_trunc(l * mx_sin_acos(c) / uh);
+        x = x86_trunc(l * mx_cos_acos(c) / uv);
+    } else if (e.kind == EXP_CONE) {   // sin(cone_theta) is a build-time constant (host libm)
+        const double R = e.radius, H = e.height;
+        const double unit_h = std::sqrt(R * R + H * H) / 320.0;
+        const double ylen = std::sqrt(sq3(ip - e.pos));
+        y = x86_trunc(ylen / unit_h);
+        const V3 center{(double)(float)e.pos.x, (double)(float)e.pos.y, (double)(float)ip.z};
+        const double rp = ylen * std::sin(e.cone_theta);
+        const V3 left{0, (double)(float)rp, 0};
+        const V3 ic = ip - center;
+        const double unit_v = 2.0 * REF_PI * rp / 320.0;
+        double alpha = mx_acos(dot(ic, left) / (rp * rp));
+        if (alpha > REF_PI / 4.0) alpha = mx_acos(dot(ic, -left) / (rp * rp));
+        x = x86_trunc(rp * alpha / unit_v);
+    } else if (e.kind == EXP_RECTANGLE) {
+        const V3 p1 = e.qv[0], p31 = e.qv[1] - p1, p41 = e.qv[2] - p1;
+        const double width = std::sqrt(sq3(p41)), length = std::sqrt(sq3(p31));
+        const V3 i1 = ip - p1;
+        const double l = std::sqrt(sq3(i1));
+        const double ct = mx_acos(dot(i1, p31) / (length * l));
+        x = x86_trunc(l * mx_sin_acos(ct) / (length / 64.0));
+        y = x86_trunc(l * ct / (width / 64.0));
+    } else x = y = 0;   // ExpBox
 }
 
 void pixel_mode_x(const Scene& s, const std::vector<Prim>& prims, const Cam& c, int w, int x, int y,
