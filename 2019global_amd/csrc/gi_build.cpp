@@ -14,6 +14,7 @@
 // bbox.h:25-39), including the silent drop (A.14) and entities kept only at the split node (A.6).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -384,6 +385,7 @@ struct XBuild {
     std::vector<int32_t>* idx;
     double pad;
     int max_depth = 0;
+    int leaf_max = XLEAF_MAX;
 
     static bool overlap(const Box& a, const Box& b) {
         for (int k = 0; k < 3; ++k)
@@ -414,7 +416,7 @@ struct XBuild {
         n0.child_base = -1; n0.child_mask = 0; n0.prim_off = 0; n0.prim_cnt = 0;
         std::vector<int32_t> kids[8];
         Box cb[8];
-        bool split = (int)prims.size() > XLEAF_MAX && depth < XMAX_DEPTH;
+        bool split = (int)prims.size() > leaf_max && depth < XMAX_DEPTH;
         if (split) {
             double mid[3];
             for (int k = 0; k < 3; ++k) mid[k] = 0.5 * (cell.mn[k] + cell.mx[k]);
@@ -551,6 +553,16 @@ bool build_host_scene(const gi_scene_desc& desc, HostScene& hs, std::string& err
     }
     hs.xnodes.clear();
     hs.xprim_idx.clear();
+    const char* accel = std::getenv("GI_XACCEL");   // tuning knob: "octree" = the earlier SAT octree
+    if (!(accel && std::string(accel) == "octree")) {
+        std::vector<double> bounds(6 * pb.size());
+        for (size_t i = 0; i < pb.size(); ++i)
+            for (int k = 0; k < 3; ++k) { bounds[6 * i + k] = pb[i].mn[k]; bounds[6 * i + 3 + k] = pb[i].mx[k]; }
+        int leaf_max = 4;
+        if (const char* lm = std::getenv("GI_XLEAF_MAX")) leaf_max = std::max(1, std::atoi(lm));
+        build_xbvh(hs.xprims, bounds, leaf_max, hs);
+        return true;
+    }
     hs.xnodes.resize(1);
     Box rootb;
     for (int k = 0; k < 3; ++k) { rootb.mn[k] = INFINITY; rootb.mx[k] = -INFINITY; }
@@ -567,6 +579,7 @@ bool build_host_scene(const gi_scene_desc& desc, HostScene& hs, std::string& err
     xb.out = &hs.xnodes;
     xb.idx = &hs.xprim_idx;
     xb.pad = 1e-9 * ext;
+    if (const char* lm = std::getenv("GI_XLEAF_MAX")) xb.leaf_max = std::max(1, std::atoi(lm));   // tuning knob
     std::vector<int32_t> all(pb.size());
     for (size_t i = 0; i < pb.size(); ++i) all[i] = (int32_t)i;
     if (pb.empty()) {

@@ -1,0 +1,316 @@
+// gi_bvh.cpp — Mode X acceleration structure: an 8-wide bounding volume hierarchy (host build).
+//
+// Mode X's result is defined by its primitive tests alone (closest t > 1e-7, ties to the lower
+// primitive index), so the acceleration structure is free.  The measured cost of one wide-node
+// visit is ~4 fp64 triangle tests (dependent loads dominate), so the build minimises node visits:
+//   1. binary BVH, binned SAH (32 bins per axis), leaves of <= leaf_max primitives;
+//   2. collapse to 8-wide: a wide node takes its binary node's children and repeatedly opens the
+//      interior child of largest surface area until it has 8 children (Wald et al. 2008);
+//   3. child slots ordered so that visiting slot k ^ octant(ray) for k = 0..7 is approximately
+//      front to back for every ray octant (greedy form of the slot assignment of Ylitie, Karras &
+//      Laine 2017): child i goes to the slot s whose octant direction best matches the offset of
+//      its centroid from the parent's;
+//   4. each primitive appears in exactly one leaf; a leaf's records (XHot) are contiguous.
+// The fp32 child boxes are rounded outward and padded, so culling is conservative and the fp64
+// primitive tests alone decide hits (bit-exact with the oracle's brute force).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <functional>
+#include <vector>
+
+#include "gi_scene.h"
+
+namespace gi {
+
+namespace {
+
+struct BBox {
+    double mn[3], mx[3];
+    void reset() {
+        for (int k = 0; k < 3; ++k) { mn[k] = INFINITY; mx[k] = -INFINITY; }
+    }
+    void grow(const BBox& b) {
+        for (int k = 0; k < 3; ++k) { mn[k] = std::min(mn[k], b.mn[k]); mx[k] = std::max(mx[k], b.mx[k]); }
+    }
+    double area() const {
+        const double dx = mx[0] - mn[0], dy = mx[1] - mn[1], dz = mx[2] - mn[2];
+        if (!(dx >= 0 && dy >= 0 && dz >= 0)) return 0.0;
+        return 2.0 * (dx * dy + dy * dz + dz * dx);
+    }
+    double centre(int k) const { return 0.5 * (mn[k] + mx[k]); }
+};
+
+struct BNode {
+    BBox box;
+    int left = -1, right = -1;   // interior: children; leaf: left < 0
+    int first = 0, count = 0;    // leaf: range in the primitive order array
+};
+
+struct Builder {
+    const std::vector<BBox>* pb;
+    std::vector<int32_t> order;
+    std::vector<double> cen;   // 3 per primitive
+    std::vector<BNode> nodes;
+    int leaf_max = 4;
+    static constexpr int kBins = 32;
+    static constexpr double kTraverse = 1.0;   // SAH cost of a node visit relative to one primitive test
+
+    int build(int first, int count, int depth) {
+        const int ni = (int)nodes.size();
+        nodes.emplace_back();
+        BBox box, cb;
+        box.reset();
+        cb.reset();
+        for (int i = first; i < first + count; ++i) {
+            const int32_t p = order[i];
+            box.grow((*pb)[p]);
+            for (int k = 0; k < 3; ++k) { cb.mn[k] = std::min(cb.mn[k], cen[3 * p + k]); cb.mx[k] = std::max(cb.mx[k], cen[3 * p + k]); }
+        }
+        nodes[ni].box = box;
+        nodes[ni].first = first;
+        nodes[ni].count = count;
+        if (count <= 1 || depth > 60) return ni;
+        // binned SAH over the centroid bounds
+        int best_axis = -1, best_split = -1;
+        double best_cost = INFINITY;
+        for (int k = 0; k < 3; ++k) {
+            const double lo = cb.mn[k], ext = cb.mx[k] - cb.mn[k];
+            if (!(ext > 0)) continue;
+            BBox bb[kBins];
+            int bn[kBins] = {0};
+            for (auto& b : bb) b.reset();
+            const double sc = kBins / ext;
+            for (int i = first; i < first + count; ++i) {
+                const int32_t p = order[i];
+                int bi = (int)((cen[3 * p + k] - lo) * sc);
+                bi = std::min(std::max(bi, 0), kBins - 1);
+                ++bn[bi];
+                bb[bi].grow((*pb)[p]);
+            }
+            double ra[kBins];
+            int rn[kBins];
+            BBox acc;
+            acc.reset();
+            int n = 0;
+            for (int i = kBins - 1; i > 0; --i) {
+                acc.grow(bb[i]);
+                n += bn[i];
+                ra[i] = acc.area();
+                rn[i] = n;
+            }
+            acc.reset();
+            n = 0;
+            for (int i = 0; i < kBins - 1; ++i) {
+                acc.grow(bb[i]);
+                n += bn[i];
+                if (n == 0 || rn[i + 1] == 0) continue;
+                const double c = acc.area() * n + ra[i + 1] * rn[i + 1];
+                if (c < best_cost) { best_cost = c; best_axis = k; best_split = i; }
+            }
+        }
+        const double parea = box.area();
+        const double split_cost = parea > 0 ? kTraverse + best_cost / parea : INFINITY;
+        if (count <= leaf_max && !(split_cost < (double)count)) return ni;   // SAH prefers a leaf
+        int mid;
+        if (best_axis < 0) {   // all centroids equal: object median
+            mid = first + count / 2;
+        } else {
+            const double lo = cb.mn[best_axis], sc = kBins / (cb.mx[best_axis] - cb.mn[best_axis]);
+            auto it = std::partition(order.begin() + first, order.begin() + first + count, [&](int32_t p) {
+                int bi = (int)((cen[3 * p + best_axis] - lo) * sc);
+                bi = std::min(std::max(bi, 0), kBins - 1);
+                return bi <= best_split;
+            });
+            mid = (int)(it - order.begin());
+            if (mid == first || mid == first + count) mid = first + count / 2;
+        }
+        const int l = build(first, mid - first, depth + 1);
+        const int r = build(mid, first + count - mid, depth + 1);
+        nodes[ni].left = l;
+        nodes[ni].right = r;
+        return ni;
+    }
+};
+
+}  // namespace
+
+// Builds hs.xwnodes / xhot / xbox from the Mode X primitives and their fp64 bounds.
+void build_xbvh(const std::vector<XPrim>& prims, const std::vector<double>& bounds, int leaf_max, HostScene& hs) {
+    const size_t np = prims.size();
+    std::vector<BBox> pb(np);
+    BBox scene;
+    scene.reset();
+    for (size_t i = 0; i < np; ++i) {
+        for (int k = 0; k < 3; ++k) { pb[i].mn[k] = bounds[6 * i + k]; pb[i].mx[k] = bounds[6 * i + 3 + k]; }
+        scene.grow(pb[i]);
+    }
+    double ext = 1.0;
+    for (int k = 0; k < 3; ++k)
+        if (np) ext = std::max(ext, std::max(std::fabs(scene.mn[k]), std::fabs(scene.mx[k])));
+    const double pad32 = 1e-5 * ext;
+    auto lo32 = [&](double v) {
+        float f = (float)(v - pad32);
+        if ((double)f > v - pad32) f = std::nextafter(f, -INFINITY);
+        return f;
+    };
+    auto hi32 = [&](double v) {
+        float f = (float)(v + pad32);
+        if ((double)f < v + pad32) f = std::nextafter(f, INFINITY);
+        return f;
+    };
+
+    hs.xwnodes.clear();
+    hs.xhot.clear();
+    hs.xbox.clear();
+    XWNode blank;
+    for (int c = 0; c < 8; ++c) {
+        for (int k = 0; k < 3; ++k) { blank.lo[k][c] = INFINITY; blank.hi[k][c] = -INFINITY; }
+        blank.child[c] = XEMPTY;
+        blank.cnt[c] = 0;
+    }
+    blank.parent = -1;
+    blank.pad[0] = blank.pad[1] = blank.pad[2] = 0;
+    hs.xwnodes.push_back(blank);   // root
+    hs.x_max_depth = 0;
+    if (np == 0) return;
+
+    Builder b;
+    b.pb = &pb;
+    b.leaf_max = std::max(1, leaf_max);
+    b.order.resize(np);
+    b.cen.resize(3 * np);
+    for (size_t i = 0; i < np; ++i) {
+        b.order[i] = (int32_t)i;
+        for (int k = 0; k < 3; ++k) b.cen[3 * i + k] = pb[i].centre(k);
+    }
+    b.nodes.reserve(2 * np);
+    const int root = b.build(0, (int)np, 0);
+
+    auto emit_leaf = [&](int first, int count) {   // -> ~offset into xhot
+        const int32_t off = (int32_t)hs.xhot.size();
+        std::vector<int32_t> ids(b.order.begin() + first, b.order.begin() + first + count);
+        std::sort(ids.begin(), ids.end());   // ascending primitive index inside a leaf
+        for (int32_t pi : ids) {
+            const XPrim& p = prims[pi];
+            XHot h;
+            memcpy(h.a, p.a, sizeof h.a);
+            memcpy(h.b, p.b, sizeof h.b);
+            memcpy(h.c, p.c, sizeof h.c);
+            h.prim = pi;
+            h.kind = p.kind;
+            hs.xhot.push_back(h);
+            XBox bx;
+            for (int a = 0; a < 3; ++a) { bx.lo[a] = lo32(pb[pi].mn[a]); bx.hi[a] = hi32(pb[pi].mx[a]); }
+            bx.pad[0] = pi;
+            bx.pad[1] = p.kind;
+            hs.xbox.push_back(bx);
+        }
+        return off;
+    };
+    // collect all primitives under a binary subtree into one leaf range (depth cap fallback)
+    std::function<void(int, std::vector<int32_t>&)> gather = [&](int n, std::vector<int32_t>& out) {
+        const BNode& bn = b.nodes[n];
+        if (bn.left < 0) {
+            out.insert(out.end(), b.order.begin() + bn.first, b.order.begin() + bn.first + bn.count);
+            return;
+        }
+        gather(bn.left, out);
+        gather(bn.right, out);
+    };
+
+    // fill wide node `wi` (depth `wd`) from binary node `bn`'s subtree
+    std::function<void(int, int, int)> fill = [&](int wi, int bn, int wd) {
+        hs.x_max_depth = std::max(hs.x_max_depth, wd);
+        std::vector<int> kids;
+        if (b.nodes[bn].left < 0) {
+            kids.push_back(bn);   // root that is a single leaf
+        } else {
+            kids.push_back(b.nodes[bn].left);
+            kids.push_back(b.nodes[bn].right);
+            while (kids.size() < 8) {
+                int pick = -1;
+                double best = -1;
+                for (int i = 0; i < (int)kids.size(); ++i) {
+                    const BNode& k = b.nodes[kids[i]];
+                    if (k.left >= 0 && k.box.area() > best) { best = k.box.area(); pick = i; }
+                }
+                if (pick < 0) break;
+                const int n = kids[pick];
+                kids[pick] = b.nodes[n].left;
+                kids.push_back(b.nodes[n].right);
+            }
+        }
+        // slot assignment: child centroid offset vs octant direction of each slot (greedy)
+        const BBox& pbox = b.nodes[bn].box;
+        const int nk = (int)kids.size();
+        double cost[8][8];
+        for (int i = 0; i < nk; ++i)
+            for (int s = 0; s < 8; ++s) {
+                double c = 0;
+                for (int k = 0; k < 3; ++k) {
+                    const double off = b.nodes[kids[i]].box.centre(k) - pbox.centre(k);
+                    c -= ((s >> k) & 1 ? 1.0 : -1.0) * off;
+                }
+                cost[i][s] = c;
+            }
+        int slot_of[8];
+        bool used_kid[8] = {false}, used_slot[8] = {false};
+        for (int it = 0; it < nk; ++it) {
+            int bi = -1, bs = -1;
+            double bc = INFINITY;
+            for (int i = 0; i < nk; ++i) {
+                if (used_kid[i]) continue;
+                for (int s = 0; s < 8; ++s)
+                    if (!used_slot[s] && cost[i][s] < bc) { bc = cost[i][s]; bi = i; bs = s; }
+            }
+            used_kid[bi] = used_slot[bs] = true;
+            slot_of[bi] = bs;
+        }
+        for (int i = 0; i < nk; ++i) {
+            const int s = slot_of[i];
+            const BNode& k = b.nodes[kids[i]];
+            {
+                XWNode& w = hs.xwnodes[wi];
+                for (int a = 0; a < 3; ++a) { w.lo[a][s] = lo32(k.box.mn[a]); w.hi[a][s] = hi32(k.box.mx[a]); }
+            }
+            if (k.left < 0) {
+                const int32_t off = emit_leaf(k.first, k.count);
+                XWNode& w = hs.xwnodes[wi];
+                w.child[s] = ~off;
+                w.cnt[s] = (uint16_t)std::min(k.count, 65535);
+            } else if (wd + 1 > 15) {   // traversal keeps 16 levels of child masks: flatten below
+                std::vector<int32_t> ids;
+                gather(kids[i], ids);
+                const int32_t off = (int32_t)hs.xhot.size();
+                for (int32_t pi : ids) {   // emit_leaf on an explicit id list
+                    const XPrim& p = prims[pi];
+                    XHot h;
+                    memcpy(h.a, p.a, sizeof h.a);
+                    memcpy(h.b, p.b, sizeof h.b);
+                    memcpy(h.c, p.c, sizeof h.c);
+                    h.prim = pi;
+                    h.kind = p.kind;
+                    hs.xhot.push_back(h);
+                    XBox bx;
+                    for (int a = 0; a < 3; ++a) { bx.lo[a] = lo32(pb[pi].mn[a]); bx.hi[a] = hi32(pb[pi].mx[a]); }
+                    bx.pad[0] = pi;
+                    bx.pad[1] = p.kind;
+                    hs.xbox.push_back(bx);
+                }
+                XWNode& w = hs.xwnodes[wi];
+                w.child[s] = ~off;
+                w.cnt[s] = (uint16_t)std::min<size_t>(ids.size(), 65535);
+            } else {
+                const int ci = (int)hs.xwnodes.size();
+                hs.xwnodes.push_back(blank);
+                hs.xwnodes[ci].parent = wi;
+                hs.xwnodes[wi].child[s] = ci;
+                fill(ci, kids[i], wd + 1);
+            }
+        }
+    };
+    fill(0, root, 0);
+}
+
+}  // namespace gi

@@ -179,7 +179,7 @@ int gi_scene_get_info(const gi_scene* s, gi_scene_info* info) {
     info->max_depth = s->host.max_depth;
     info->n_reachable = s->host.n_reachable;
     info->n_dropped = s->host.n_dropped;
-    info->x_nodes = (int32_t)s->host.xnodes.size();
+    info->x_nodes = (int32_t)(s->host.xnodes.empty() ? s->host.xwnodes.size() : s->host.xnodes.size());
     info->x_prims = (int32_t)s->host.xprims.size();
     info->device_bytes = s->bytes;
     return GI_OK;

@@ -277,6 +277,19 @@ __device__ __forceinline__ bool lane_pixel(const TileMap& m, long long lt, long 
     return x < m.w && y < m.h;
 }
 
+// pixel of slot j (0..63) of local tile lt (row-major 8x8 inside the tile); false: no pixel there
+__device__ __forceinline__ bool slot_pixel(const TileMap& m, long long lt, int j, long long& out_idx, int& x, int& y) {
+    out_idx = -1;
+    const long long t = (long long)m.shard_index + lt * m.shard_count;
+    if (t >= m.n_tiles) return false;
+    const int ty = (int)(t / m.tiles_x), tx = (int)(t % m.tiles_x);
+    x = tx * kTile + (j & 7);
+    y = ty * kTile + (j >> 3);
+    if (m.shard_count == 1) out_idx = (long long)y * m.w + x;
+    else out_idx = lt * (kTile * kTile) + j;
+    return x < m.w && y < m.h;
+}
+
 __device__ __forceinline__ V3 primary_dir(const CamDev& c, double fx, double fy) {
     // raytracer.h:41: top_left - left*x*res.x - up*y*res.y
     return (c.top_left - (c.left * fx) * c.rx) - (c.up * fy) * c.ry;
@@ -464,17 +477,18 @@ __device__ void x_texcoord(const DevScene& sc, const REnt& e, V3 ip, int32_t& x,
     }
 }
 
-// Mode X path state machine.  A lane owns one pixel and walks its spp samples in order; every
-// loop iteration a lane either makes ONE traversal step of its current ray (pop a node: cull,
+// Mode X path state machine.  A lane owns one pixel at a time and walks its spp samples in order;
+// every loop iteration a lane either makes ONE traversal step of its current ray (pop a node: cull,
 // push children, or test a leaf's primitives) or, once its ray has finished, runs the shading
 // handler that consumes the hit and spawns the lane's next ray (shadow ray, next bounce, or the
-// next sample's primary ray).  Lanes never wait for each other at sample/bounce boundaries
-// (the nested-loop form reconverged at every loop exit: ~16% VALU lane utilisation measured).
-// The handler runs once at least half of the live lanes have a finished ray, or when none is
-// still traversing, so it executes with a well-filled EXEC mask.  The per-path operation
-// sequence is exactly the oracle's (pixel_mode_x in oracle/gi_oracle.cpp), so results are
-// bit-identical whatever the schedule.
-enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_DONE = 2, PH_START = 3 };
+// next sample's primary ray).  When a lane's pixel is complete it writes it and takes the next
+// pixel from the device-wide slot counter (wave ballot + one atomic per refill), so lanes never
+// wait for each other at sample, bounce or pixel boundaries (a fixed 8x8 tile per wave left ~1/4
+// of the lanes idle behind the tile's slowest pixel).  The handler runs once at least half of the
+// live lanes have a finished ray, or when none is still traversing, so it executes with a
+// well-filled EXEC mask.  The per-path operation sequence is exactly the oracle's (pixel_mode_x in
+// oracle/gi_oracle.cpp), so results are bit-identical whatever the schedule.
+enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD = 4 };
 
 #ifndef GI_X_PRIM_PREFILTER
 #define GI_X_PRIM_PREFILTER 0   // fp32 AABB cull before each fp64 primitive test (measured slower: +1 dependent load)
@@ -486,19 +500,21 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_DONE = 2, PH_START = 3 };
 #define GI_X_MIN_WAVES 1   // minimum waves per SIMD for k_mode_x (register budget knob)
 #endif
 
-__device__ __forceinline__ void mode_x_tile(const DevScene& sc, const CamDev& cam, V3 light, const TileMap& m, long long lt,
-                                            int spp, int depth, uint64_t seed, double* rgb, uint8_t* rgb8,
-                                            uint64_t& c_rays, uint64_t& c_nodes, uint64_t& c_prims, uint64_t& c_px,
-                                            uint64_t& c_box) {
+struct XCounters {
+    uint64_t rays = 0, nodes = 0, prims = 0, px = 0, box = 0;
+};
+
+__device__ __forceinline__ void mode_x_wave(const DevScene& sc, const CamDev& cam, V3 light, const TileMap& m, int spp,
+                                            int depth, uint64_t seed, double* rgb, uint8_t* rgb8, unsigned* slot_counter,
+                                            XCounters& cnt) {
+    const int lane = threadIdx.x & 63;
+    const unsigned n_slots = (unsigned)(m.n_local * (kTile * kTile));
+    uint32_t nnode = 0, nprim = 0, nrays = 0, nbox = 0, npx = 0;
     long long idx = -1;
     int x = 0, y = 0;
-    const bool ok = lane_pixel(m, lt, idx, x, y);
-    y += m.y0;
-    uint32_t nnode = 0, nprim = 0, nrays = 0, nbox = 0;
-    const uint64_t pix = (uint64_t)y * (uint64_t)m.w + (uint64_t)x;
-    const uint64_t key = mx_key(seed, pix);
+    uint64_t key = 0;
 
-    int phase = ok ? PH_START : PH_DONE;
+    int phase = PH_NEED;
     int smp = 0, b = 0;
     // current ray
     V3 o = cam.pos, d = v3(1, 0, 0);
@@ -515,12 +531,14 @@ __device__ __forceinline__ void mode_x_tile(const DevScene& sc, const CamDev& ca
     V3 P = v3(0, 0, 0), nextd = v3(0, 0, 0), lit = v3(0, 0, 0), dark = v3(0, 0, 0), Tn = v3(0, 0, 0);
     bool has_next = false;
 
-    while (phase != PH_DONE) {
+    for (;;) {
+        const unsigned long long m_live = __ballot(phase != PH_DEAD);
+        if (m_live == 0) break;
         const bool trav = raying;
-        const unsigned long long m_live = __ballot(1);
         const unsigned long long m_trav = __ballot(trav);
         const int n_wait = __popcll(m_live & ~m_trav);
-        const bool handle = !trav && (4 * n_wait >= GI_X_HANDLE_QUARTERS * __popcll(m_live) || m_trav == 0);
+        const bool handle = phase != PH_DEAD && !trav &&
+                            (4 * n_wait >= GI_X_HANDLE_QUARTERS * __popcll(m_live) || m_trav == 0);
         if (trav) {
             // ---- one traversal step (stackless: 8-bit "children left" mask per level) --------
             uint32_t msk = lvl_get(mlo, mhi, level);
@@ -544,8 +562,8 @@ __device__ __forceinline__ void mode_x_tile(const DevScene& sc, const CamDev& ca
                     if (ch < 0) {             // leaf: fp64 primitive tests (these decide the result)
                         const XHot* hp = sc.xhot + ~ch;
                         const XBox* bp = sc.xbox + ~ch;
-                        const int cnt = nd->cnt[c];
-                        for (int j = 0; j < cnt; ++j) {
+                        const int cntl = nd->cnt[c];
+                        for (int j = 0; j < cntl; ++j) {
 #if GI_X_PRIM_PREFILTER
                             ++nbox;
                             if (!box32_hit(bp[j], of, ivf, tbest_f)) continue;   // conservative fp32 cull
@@ -561,6 +579,7 @@ __device__ __forceinline__ void mode_x_tile(const DevScene& sc, const CamDev& ca
                                 tbest_f = up32(t);
                             }
                         }
+                        (void)bp;
                     } else {                  // descend: cull the child's 8 children in fp32
                         ++nnode;
                         node = ch;
@@ -645,7 +664,39 @@ __device__ __forceinline__ void mode_x_tile(const DevScene& sc, const CamDev& ca
             if (end_path) {
                 s0 = s0 + L.x; s1 = s1 + L.y; s2 = s2 + L.z;
                 ++smp;
-                phase = smp < spp ? PH_START : PH_DONE;
+                if (smp < spp) {
+                    phase = PH_START;
+                } else {              // pixel complete
+                    const double c0 = smin(s0 / (double)spp, 1.0), c1 = smin(s1 / (double)spp, 1.0),
+                                 c2 = smin(s2 / (double)spp, 1.0);
+                    if (rgb) { rgb[3 * idx] = c0; rgb[3 * idx + 1] = c1; rgb[3 * idx + 2] = c2; }
+                    if (rgb8) quantize(c0, c1, c2, rgb8 + 3 * idx);
+                    ++npx;
+                    phase = PH_NEED;
+                }
+            }
+            // ---- lanes without a pixel take the next slots (one atomic per wave) ---------------
+            const unsigned long long m_need = __ballot(phase == PH_NEED);
+            if (m_need) {
+                const int leader = __ffsll((long long)m_need) - 1;
+                unsigned base = 0;
+                if (lane == leader) base = atomicAdd(slot_counter, (unsigned)__popcll(m_need));
+                base = __shfl(base, leader);
+                if (phase == PH_NEED) {
+                    const unsigned sl = base + (unsigned)__popcll(m_need & ((1ull << lane) - 1));
+                    if (sl >= n_slots) {
+                        phase = PH_DEAD;
+                    } else if (slot_pixel(m, (long long)(sl >> 6), (int)(sl & 63), idx, x, y)) {
+                        y += m.y0;
+                        key = mx_key(seed, (uint64_t)y * (uint64_t)m.w + (uint64_t)x);
+                        smp = 0;
+                        s0 = s1 = s2 = 0;
+                        phase = PH_START;
+                    } else if (idx >= 0 && m.shard_count > 1) {   // padding slot of a packed tile
+                        if (rgb) { rgb[3 * idx] = 0; rgb[3 * idx + 1] = 0; rgb[3 * idx + 2] = 0; }
+                        if (rgb8) { rgb8[3 * idx] = 0; rgb8[3 * idx + 1] = 0; rgb8[3 * idx + 2] = 0; }
+                    }
+                }
             }
             if (phase == PH_START) {
                 double jx = 0.0, jy = 0.0;
@@ -660,7 +711,7 @@ __device__ __forceinline__ void mode_x_tile(const DevScene& sc, const CamDev& ca
                 tbest = INFINITY;
                 tbest_f = INFINITY;
             }
-            if (phase != PH_DONE) {   // start traversing the new ray
+            if (phase == PH_CLOSEST || phase == PH_SHADOW) {   // start traversing the new ray
                 const V3 inv = v3(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
                 of = f3((float)o.x, (float)o.y, (float)o.z);
                 ivf = f3((float)inv.x, (float)inv.y, (float)inv.z);
@@ -674,40 +725,27 @@ __device__ __forceinline__ void mode_x_tile(const DevScene& sc, const CamDev& ca
             }
         }
     }
-    if (ok) {
-        const double c0 = smin(s0 / (double)spp, 1.0), c1 = smin(s1 / (double)spp, 1.0), c2 = smin(s2 / (double)spp, 1.0);
-        if (rgb) { rgb[3 * idx] = c0; rgb[3 * idx + 1] = c1; rgb[3 * idx + 2] = c2; }
-        if (rgb8) quantize(c0, c1, c2, rgb8 + 3 * idx);
-    } else if (idx >= 0 && m.shard_count > 1) {
-        if (rgb) { rgb[3 * idx] = 0; rgb[3 * idx + 1] = 0; rgb[3 * idx + 2] = 0; }
-        if (rgb8) { rgb8[3 * idx] = 0; rgb8[3 * idx + 1] = 0; rgb8[3 * idx + 2] = 0; }
-    }
-    c_rays += nrays;
-    c_nodes += nnode;
-    c_prims += nprim;
-    c_px += ok ? 1 : 0;
-    c_box += nbox;
+    cnt.rays += nrays;
+    cnt.nodes += nnode;
+    cnt.prims += nprim;
+    cnt.px += npx;
+    cnt.box += nbox;
 }
 
-// Persistent waves with dynamic tile scheduling: each wave pulls the next 8x8 tile from a
-// device counter (one returning atomic per tile, SURVEY §7 hard part 4: per-ray cost varies ~10x
-// between background and scene tiles), so no wave idles behind a workgroup sibling or the grid tail.
+// Persistent waves: the grid is sized to the resident capacity; every lane pulls pixel slots
+// from one device counter (SURVEY §7 hard part 4: per-ray cost varies ~10x between background
+// and scene pixels), so no lane idles behind a sibling, a workgroup or the grid tail.
 template <bool STATS>
 __global__ __launch_bounds__(256, GI_X_MIN_WAVES) void k_mode_x(DevScene sc, CamDev cam, V3 light, TileMap m, int spp, int depth,
                                                  uint64_t seed, double* rgb, uint8_t* rgb8,
-                                                 unsigned long long* stats, unsigned* tile_counter) {
-    uint64_t c_rays = 0, c_nodes = 0, c_prims = 0, c_px = 0, c_box = 0;
-    for (;;) {
-        unsigned v = 0;
-        if ((threadIdx.x & 63) == 0) v = atomicAdd(tile_counter, 1u);
-        const long long lt = (long long)__builtin_amdgcn_readfirstlane(v);
-        if (lt >= m.n_local) break;
-        mode_x_tile(sc, cam, light, m, lt, spp, depth, seed, rgb, rgb8, c_rays, c_nodes, c_prims, c_px, c_box);
-    }
+                                                 unsigned long long* stats, unsigned* slot_counter) {
+    XCounters c;
+    mode_x_wave(sc, cam, light, m, spp, depth, seed, rgb, rgb8, slot_counter, c);
     if (STATS) {
-        wave_add_stats(stats, c_rays, c_nodes, c_prims, c_px);
-        for (int off = 32; off > 0; off >>= 1) c_box += __shfl_xor(c_box, off);
-        if ((threadIdx.x & 63) == 0) atomicAdd(stats + GI_STAT_PBOX, (unsigned long long)c_box);
+        wave_add_stats(stats, c.rays, c.nodes, c.prims, c.px);
+        uint64_t cb = c.box;
+        for (int off = 32; off > 0; off >>= 1) cb += __shfl_xor(cb, off);
+        if ((threadIdx.x & 63) == 0) atomicAdd(stats + GI_STAT_PBOX, (unsigned long long)cb);
     }
 }
 

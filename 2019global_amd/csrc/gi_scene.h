@@ -111,6 +111,9 @@ struct HostScene {
     int32_t x_max_depth = 0;
 };
 
+// Mode X 8-wide BVH over the primitives (gi_bvh.cpp); bounds: 6 doubles (min xyz, max xyz) each.
+void build_xbvh(const std::vector<XPrim>& prims, const std::vector<double>& bounds, int leaf_max, HostScene& hs);
+
 // Device view passed to kernels by value.
 struct DevScene {
     const RNode* rnodes;

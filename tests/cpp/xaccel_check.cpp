@@ -1,0 +1,282 @@
+// xaccel_check.cpp — CPU check of the Mode X acceleration structure built by libgi's host code
+// (gi_build.cpp + gi_bvh.cpp, compiled here by g++ from the same sources).
+//
+//  * structure: every primitive in exactly one leaf (BVH) / at least one leaf (octree), every
+//    fp32 child box contains its subtree's fp64 primitive bounds, parent pointers consistent,
+//    depth within the 16 mask levels of the traversal;
+//  * traversal: the kernel's stackless front-to-back walk (k_mode_x, restated here step for step:
+//    per-level 8-bit child masks, slot k ^ octant order, re-cull against the current best t)
+//    returns the same closest hit (t, primitive) as a brute-force loop over all primitives, for
+//    closest and any-hit (shadow) queries, on random soups and on the Cornell box.
+//   xaccel_check <n_rays>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "gi.h"
+#include "gi_scene.h"
+
+namespace gi {
+bool build_host_scene(const gi_scene_desc& desc, HostScene& hs, std::string& err);
+}
+using namespace gi;
+
+static uint64_t g_rng = 0x2019;
+static double urand() {
+    g_rng += 0x9E3779B97F4A7C15ULL;
+    uint64_t z = g_rng;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    z ^= z >> 31;
+    return (double)(z >> 11) * 0x1.0p-53;
+}
+
+static double prim_t(const XHot& p, V3 o, V3 d, double tmin) {   // the kernel's x_prim_t
+    if (p.kind == 0) {
+        const V3 e1 = ld3(p.b), e2 = ld3(p.c);
+        const V3 pv = cross(d, e2);
+        const double det = dot(e1, pv);
+        if (det == 0.0) return INFINITY;
+        const double inv = 1.0 / det;
+        const V3 tv = o - ld3(p.a);
+        const double u = dot(tv, pv) * inv;
+        if (u < 0.0 || u > 1.0) return INFINITY;
+        const V3 qv = cross(tv, e1);
+        const double v = dot(d, qv) * inv;
+        if (v < 0.0 || u + v > 1.0) return INFINITY;
+        const double t = dot(e2, qv) * inv;
+        return (t > tmin) ? t : INFINITY;
+    }
+    const V3 oc = o - ld3(p.a);
+    const double b = dot(oc, d);
+    const double r = p.b[0];
+    const double c2 = dot(oc, oc) - r * r;
+    const double disc = b * b - c2;
+    if (disc < 0.0) return INFINITY;
+    const double sq = std::sqrt(disc);
+    double t = -b - sq;
+    if (t > tmin) return t;
+    t = -b + sq;
+    return (t > tmin) ? t : INFINITY;
+}
+
+static XHot hot_of(const XPrim& p, int i) {
+    XHot h;
+    for (int k = 0; k < 3; ++k) { h.a[k] = p.a[k]; h.b[k] = p.b[k]; h.c[k] = p.c[k]; }
+    h.prim = i;
+    h.kind = p.kind;
+    return h;
+}
+
+static float up32(double v) {
+    float f = (float)v;
+    if ((double)f < v) f = std::nextafter(f, INFINITY);
+    return f;
+}
+struct F3 { float x, y, z; };
+static bool child_hit(const XWNode* nd, int c, F3 of, F3 ivf, float tmax) {
+    const float tx0 = (nd->lo[0][c] - of.x) * ivf.x, tx1 = (nd->hi[0][c] - of.x) * ivf.x;
+    const float ty0 = (nd->lo[1][c] - of.y) * ivf.y, ty1 = (nd->hi[1][c] - of.y) * ivf.y;
+    const float tz0 = (nd->lo[2][c] - of.z) * ivf.z, tz1 = (nd->hi[2][c] - of.z) * ivf.z;
+    const float tn = std::fmax(std::fmax(std::fmin(tx0, tx1), std::fmin(ty0, ty1)), std::fmax(std::fmin(tz0, tz1), 0.0f));
+    const float tf = std::fmin(std::fmin(std::fmax(tx0, tx1), std::fmax(ty0, ty1)), std::fmin(std::fmax(tz0, tz1), tmax));
+    return tn <= tf;
+}
+static uint32_t children_mask(const XWNode* nd, F3 of, F3 ivf, float tmax, int dmask) {
+    uint32_t m = 0;
+    for (int c = 0; c < 8; ++c)
+        if (nd->child[c] != XEMPTY && child_hit(nd, c, of, ivf, tmax)) m |= 1u << (c ^ dmask);
+    return m;
+}
+static uint32_t lvl_get(uint64_t lo, uint64_t hi, int l) { return (uint32_t)((l < 8 ? lo >> (8 * l) : hi >> (8 * (l - 8))) & 0xFF); }
+static void lvl_set(uint64_t& lo, uint64_t& hi, int l, uint32_t m) {
+    if (l < 8) lo = (lo & ~(0xFFull << (8 * l))) | ((uint64_t)m << (8 * l));
+    else hi = (hi & ~(0xFFull << (8 * (l - 8)))) | ((uint64_t)m << (8 * (l - 8)));
+}
+
+// k_mode_x's traversal of one ray; shadow: any hit with t < tmax
+static long g_prim_tests = 0;
+static int traverse(const HostScene& s, V3 o, V3 d, bool shadow, double tmax, double& tbest, long& visits) {
+    const V3 inv = v3(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+    const F3 of = {(float)o.x, (float)o.y, (float)o.z}, ivf = {(float)inv.x, (float)inv.y, (float)inv.z};
+    const int dmask = (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
+    tbest = shadow ? tmax : INFINITY;
+    float tbest_f = shadow ? up32(tmax) : INFINITY;
+    int best = -1, node = 0, level = 0;
+    uint64_t mlo = 0, mhi = 0;
+    lvl_set(mlo, mhi, 0, children_mask(&s.xwnodes[0], of, ivf, tbest_f, dmask));
+    for (;;) {
+        uint32_t msk = lvl_get(mlo, mhi, level);
+        while (msk == 0 && level > 0) {
+            node = s.xwnodes[node].parent;
+            --level;
+            msk = lvl_get(mlo, mhi, level);
+        }
+        if (msk == 0) break;
+        const int k = __builtin_ctz(msk);
+        lvl_set(mlo, mhi, level, msk & (msk - 1));
+        const int c = k ^ dmask;
+        const XWNode* nd = &s.xwnodes[node];
+        const int ch = nd->child[c];
+        if (!shadow && best >= 0 && !child_hit(nd, c, of, ivf, tbest_f)) continue;
+        if (ch < 0) {
+            for (int j = 0; j < nd->cnt[c]; ++j) {
+                const XHot& h = s.xhot[~ch + j];
+                const double t = prim_t(h, o, d, 1e-7);
+                ++g_prim_tests;
+                if (shadow) {
+                    if (t < tmax) return h.prim;
+                } else if (t < tbest || (t == tbest && h.prim < best)) {
+                    tbest = t;
+                    best = h.prim;
+                    tbest_f = up32(t);
+                }
+            }
+        } else {
+            ++visits;
+            node = ch;
+            ++level;
+            if (level > 15) { std::printf("depth overflow\n"); std::exit(3); }
+            lvl_set(mlo, mhi, level, children_mask(&s.xwnodes[ch], of, ivf, tbest_f, dmask));
+        }
+    }
+    return best;
+}
+
+static int brute(const HostScene& s, V3 o, V3 d, bool shadow, double tmax, double& tbest) {
+    tbest = INFINITY;
+    int best = -1;
+    for (size_t i = 0; i < s.xprims.size(); ++i) {
+        const double t = prim_t(hot_of(s.xprims[i], (int)i), o, d, 1e-7);
+        if (shadow) {
+            if (t < tmax) return (int)i;
+        } else if (t < tbest) {
+            tbest = t;
+            best = (int)i;
+        }
+    }
+    return best;
+}
+
+static int check_structure(const HostScene& s, bool exact_once) {
+    std::vector<int> seen(s.xprims.size(), 0);
+    for (size_t w = 0; w < s.xwnodes.size(); ++w) {
+        const XWNode& n = s.xwnodes[w];
+        for (int c = 0; c < 8; ++c) {
+            if (n.child[c] == XEMPTY) continue;
+            if (n.child[c] >= 0) {
+                if (s.xwnodes[n.child[c]].parent != (int)w) { std::printf("parent mismatch\n"); return 1; }
+                continue;
+            }
+            for (int j = 0; j < n.cnt[c]; ++j) {
+                const XHot& h = s.xhot[~n.child[c] + j];
+                ++seen[h.prim];
+                const XPrim& p = s.xprims[h.prim];
+                double mn[3], mx[3];
+                for (int k = 0; k < 3; ++k) {
+                    if (p.kind == 1) { mn[k] = p.a[k] - p.b[0]; mx[k] = p.a[k] + p.b[0]; }
+                    else {
+                        const double v0 = p.a[k], v1 = p.a[k] + p.b[k], v2 = p.a[k] + p.c[k];
+                        mn[k] = std::fmin(std::fmin(v0, v1), v2);
+                        mx[k] = std::fmax(std::fmax(v0, v1), v2);
+                    }
+                    // the BVH pads with 1e-5*extent, far above the rounding of p.a + p.b (the octree
+                    // clips a primitive's box to each cell it overlaps, so only the BVH contains it)
+                    if (exact_once && ((double)n.lo[k][c] > mn[k] || (double)n.hi[k][c] < mx[k])) {
+                        std::printf("box does not contain prim\n");
+                        return 1;
+                    }
+                }
+            }
+        }
+    }
+    for (size_t i = 0; i < seen.size(); ++i)
+        if (seen[i] == 0 || (exact_once && seen[i] != 1)) { std::printf("prim %zu seen %d times\n", i, seen[i]); return 1; }
+    return 0;
+}
+
+static gi_entity_desc tri(double* v) {
+    gi_entity_desc e{};
+    e.kind = GI_IMP_TRIANGLE;
+    for (int k = 0; k < 9; ++k) e.args[k] = v[k];
+    return e;
+}
+
+// optional: a .scn file (impsphere / imptriangle lines only), e.g. the Cornell box
+static bool read_scn(const char* path, std::vector<gi_entity_desc>& ents) {
+    std::ifstream f(path);
+    std::string line;
+    while (std::getline(f, line)) {
+        std::istringstream is(line);
+        std::string kw;
+        is >> kw;
+        std::vector<double> v;
+        double x;
+        while (is >> x) v.push_back(x);
+        gi_entity_desc e{};
+        if (kw == "imptriangle") e.kind = GI_IMP_TRIANGLE;
+        else if (kw == "impsphere") e.kind = GI_IMP_SPHERE;
+        else continue;
+        for (size_t k = 0; k < v.size() && k < 11; ++k) e.args[k] = v[k];
+        ents.push_back(e);
+    }
+    return !ents.empty();
+}
+
+int main(int argc, char** argv) {
+    const int nrays = argc > 1 ? std::atoi(argv[1]) : 20000;
+    long mism = 0, total = 0, visits = 0;
+    const int first_scene = argc > 2 ? 4 : 0, last_scene = argc > 2 ? 5 : 4;
+    for (int scene = first_scene; scene < last_scene; ++scene) {
+        std::vector<gi_entity_desc> ents;
+        if (scene == 4 && !read_scn(argv[2], ents)) return 2;
+        const int ntri = scene == 0 ? 40 : scene == 1 ? 3000 : scene == 2 ? 20000 : scene == 3 ? 300 : 0;
+        for (int i = 0; i < ntri; ++i) {
+            double c[3] = {urand() * 10, urand() * 10 - 5, urand() * 10 - 5}, v[9];
+            const double sz = scene == 3 ? 6.0 : 0.6;   // scene 3: large overlapping triangles
+            for (int k = 0; k < 9; ++k) v[k] = c[k % 3] + sz * (2 * urand() - 1);
+            ents.push_back(tri(v));
+        }
+        for (int i = 0; i < (scene < 4 ? 6 : 0); ++i) {   // spheres
+            gi_entity_desc e{};
+            e.kind = GI_IMP_SPHERE;
+            e.args[0] = urand() * 10; e.args[1] = urand() * 10 - 5; e.args[2] = urand() * 10 - 5; e.args[3] = 0.3 + urand();
+            ents.push_back(e);
+        }
+        gi_scene_desc sd{};
+        for (int k = 0; k < 3; ++k) { sd.octree_min[k] = -20; sd.octree_max[k] = 20; }
+        sd.n_entities = (int32_t)ents.size();
+        sd.entities = ents.data();
+        HostScene hs;
+        std::string err;
+        if (!build_host_scene(sd, hs, err)) { std::printf("build failed: %s\n", err.c_str()); return 2; }
+        const bool bvh = hs.xnodes.empty();
+        if (check_structure(hs, bvh)) return 1;
+        const long visits0 = visits, prims0 = g_prim_tests;
+        for (int r = 0; r < nrays; ++r) {
+            V3 o, tgt;
+            if (r % 2 == 0) o = v3(-10, 0, 0);
+            else o = v3(urand() * 12 - 1, urand() * 12 - 6, urand() * 12 - 6);
+            tgt = v3(urand() * 12 - 1, urand() * 12 - 6, urand() * 12 - 6);
+            if (r % 7 == 0) tgt.y = o.y;   // axis-parallel components
+            const V3 d = normalize(tgt - o);
+            const bool shadow = (r % 3) == 0;
+            const double tmax = shadow ? 3.0 + 10 * urand() : INFINITY;
+            double t1, t2;
+            const int a = traverse(hs, o, d, shadow, tmax, t1, visits);
+            const int b = brute(hs, o, d, shadow, tmax, t2);
+            ++total;
+            if (shadow ? ((a >= 0) != (b >= 0)) : (a != b || !(t1 == t2 || (std::isinf(t1) && std::isinf(t2))))) ++mism;
+        }
+        std::printf("scene %d: %zu prims, %zu wide nodes, %zu leaf records, depth %d; per ray: %.2f node visits, %.2f prim tests\n",
+                    scene, hs.xprims.size(), hs.xwnodes.size(), hs.xhot.size(), hs.x_max_depth,
+                    (double)(visits - visits0) / nrays, (double)(g_prim_tests - prims0) / nrays);
+    }
+    std::printf("rays %ld mismatches %ld wide-node visits %ld\n", total, mism, visits);
+    return mism == 0 ? 0 : 1;
+}
