@@ -43,9 +43,11 @@ LIB_PATH = os.environ.get("GI_LIB") or os.path.join(HERE, "libgi.so")   # GI_LIB
 MODE_R, MODE_X = 0, 1
 FLAG_STATS = 1
 STAT_RAYS, STAT_NODES, STAT_PRIMS, STAT_PIXELS, STAT_PBOX = 0, 1, 2, 3, 4
-STATS_N = 8
+STAT_X_ITERS, STAT_X_TRAV, STAT_X_HANDLE, STAT_X_HLANES, STAT_X_HCLOSE, STAT_X_HSHADOW = 5, 6, 7, 8, 9, 10
+STAT_X_CYC_TRAV, STAT_X_CYC_HIT, STAT_X_CYC_NEXT, STAT_X_CYC_ALL = 11, 12, 13, 14
+STATS_N = 16
 TILE = 8
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 
 class GIError(RuntimeError):

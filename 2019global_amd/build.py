@@ -40,9 +40,15 @@ def _stale(out, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(verbose: bool = False, force: bool = False) -> str:
+def build(verbose: bool = False, force: bool = False, variant: str = "", hip_defines=()) -> str:
+    """Builds libgi.so; a named variant (tuning experiments: extra -D flags for the kernels) goes to
+    2019global_amd/_variants/libgi_<variant>.so and is selected at run time with GI_LIB=<path>."""
     hipcc = shutil.which("hipcc") or os.path.join(ROCM, "bin", "hipcc")
     objdir = os.path.join(HERE, "_obj")
+    out = OUT
+    if variant:
+        out = os.path.join(HERE, "_variants", f"libgi_{variant}.so")
+        os.makedirs(os.path.dirname(out), exist_ok=True)
     os.makedirs(objdir, exist_ok=True)
     hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "gi.h")]
     objs = []
@@ -52,16 +58,24 @@ def build(verbose: bool = False, force: bool = False) -> str:
             _run(["g++", "-O2", *COMMON, "-D__HIP_PLATFORM_AMD__", f"-I{ROCM}/include", "-c", src, "-o", obj], verbose)
         objs.append(obj)
     for s in DEV_SRCS:
-        src, obj = os.path.join(CSRC, s), os.path.join(objdir, s + ".o")
+        src = os.path.join(CSRC, s)
+        obj = os.path.join(objdir, s + (f".{variant}" if variant else "") + ".o")
         if force or _stale(obj, [src] + hdrs):
-            _run([hipcc, f"--offload-arch={ARCH}", "-O3", *COMMON, "-munsafe-fp-atomics", "-c", src, "-o", obj], verbose)
+            _run([hipcc, f"--offload-arch={ARCH}", "-O3", *COMMON, *[f"-D{d}" for d in hip_defines],
+                  "-munsafe-fp-atomics", "-c", src, "-o", obj], verbose)
         objs.append(obj)
-    if force or _stale(OUT, objs):
-        _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-o", OUT, *objs, f"-L{ROCM}/lib", "-lamdhip64"], verbose)
-        for leftover in glob.glob(OUT + ".0.*"):   # hipcc's unbundling temporaries
+    if force or _stale(out, objs):
+        _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-o", out, *objs, f"-L{ROCM}/lib", "-lamdhip64"], verbose)
+        for leftover in glob.glob(out + ".0.*"):   # hipcc's unbundling temporaries
             os.remove(leftover)
-    return OUT
+    return out
 
 
 if __name__ == "__main__":
-    build(verbose=True, force="--force" in sys.argv)
+    # python build.py [--force] [--variant NAME DEFINE ...]
+    args = sys.argv[1:]
+    var, defs = "", []
+    if "--variant" in args:
+        i = args.index("--variant")
+        var, defs = args[i + 1], [a for a in args[i + 2:] if not a.startswith("--")]
+    build(verbose=True, force="--force" in args, variant=var, hip_defines=defs)

@@ -63,6 +63,14 @@ bool build_entity(const gi_entity_desc& d, BEnt& e, std::string& err) {
         make_tri(p1, p2, p3, t);
         e.tris.push_back(t);
         e.rec.pos[0] = t.pos[0]; e.rec.pos[1] = t.pos[1]; e.rec.pos[2] = t.pos[2];
+        {   // getTextureCoord's per-triangle constants (entities.h:277-303), same fp64 ops as per hit
+            const V3 p21 = p2 - p1, p31 = p3 - p1, p32 = p3 - p2;
+            st3(e.rec.qv0, p1);
+            st3(e.rec.qv1, p21);
+            e.rec.qv2[0] = gsqrt(sq3(p21));                            // |p2 - p1|
+            e.rec.qv2[1] = gsqrt(sq3(0.5 * (p21 + p31))) / 160.0;      // unit_v
+            e.rec.qv2[2] = gsqrt(sq3(0.5 * ((-p32) + (-p31)))) / 160.0;   // unit_h
+        }
         e.bmin = v3(smin(smin(p1.x, p2.x), p3.x), smin(smin(p1.y, p2.y), p3.y), smin(smin(p1.z, p2.z), p3.z));
         e.bmax = v3(smax(smax(p1.x, p2.x), p3.x), smax(smax(p1.y, p2.y), p3.y), smax(smax(p1.z, p2.z), p3.z) + 0.01);
         if (e.bmax.x == e.bmin.x) e.bmax.x += 1e-5;

@@ -161,6 +161,16 @@ int gi_scene_create(const gi_scene_desc* desc, gi_scene** out) {
     d.n_xwnodes = (int32_t)h.xwnodes.size();
     d.n_xprims = (int32_t)h.xprims.size();
     d.x_max_depth = h.x_max_depth;
+    d.x_handle8 = h.x_handle8;
+    d.x_flags = h.x_flags;
+    for (int k = 0; k < 3; ++k) { d.root_lo[k] = INFINITY; d.root_hi[k] = -INFINITY; }
+    if (!h.xwnodes.empty())
+        for (int c = 0; c < 8; ++c)
+            if (h.xwnodes[0].child[c] != XEMPTY)
+                for (int k = 0; k < 3; ++k) {
+                    d.root_lo[k] = std::min(d.root_lo[k], h.xwnodes[0].lo[k][c]);
+                    d.root_hi[k] = std::max(d.root_hi[k], h.xwnodes[0].hi[k][c]);
+                }
     *out = s;
     return GI_OK;
 }

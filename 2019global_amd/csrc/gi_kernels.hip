@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 
 #include "gi.h"
 #include "gi_scene.h"
@@ -104,19 +105,13 @@ __device__ void tex_coord(const DevScene& sc, const REnt& e, V3 ip, int32_t& x, 
         const double cos_hori = dot(v3(to.x, to.y, 0), v3(0, small_r, 0)) / (small_r * small_r);
         const double unit_h = 2.0 * REF_PI * small_r / 320.0;
         x = x86_trunc(small_r * acos(cos_hori) / unit_h);
-    } else if (e.kind == K_IMP_TRIANGLE) {
-        const TriRec& t = sc.tris[e.tri_first];
-        const V3 p1 = ld3(t.p1), p2 = ld3(t.p2), p3 = ld3(t.p3);
-        const V3 p21 = p2 - p1, p31 = p3 - p1, p32 = p3 - p2, i1 = ip - p1;
-        const double p21l = gsqrt(sq3(p21));
+    } else if (e.kind == K_IMP_TRIANGLE) {   // per-triangle constants precomputed by the builder
+        const V3 p1 = ld3(e.qv0), p21 = ld3(e.qv1), i1 = ip - p1;
         const double i1l = gsqrt(sq3(i1));
-        const double theta = acos(dot(p21, i1) / (p21l * i1l));
+        const double theta = acos(dot(p21, i1) / (e.qv2[0] * i1l));
         const double ixl = i1l * sin(theta);
-        const double vl = gsqrt(sq3(0.5 * (p21 + p31)));
-        const double hl = gsqrt(sq3(0.5 * ((-p32) + (-p31))));
-        const double uv = vl / 160.0, uh = hl / 160.0;
-        y = x86_trunc(i1l / uh);
-        x = x86_trunc(ixl / uv);
+        y = x86_trunc(i1l / e.qv2[2]);
+        x = x86_trunc(ixl / e.qv2[1]);
     } else if (e.kind == K_EXP_QUAD) {
         const double uv = (double)e.width / 160.0, uh = (double)e.length / 160.0;
         const V3 rv = ld3(e.qv0) - ld3(e.qv1);
@@ -349,19 +344,19 @@ __device__ __forceinline__ float up32(double v) {
 }
 
 __device__ __forceinline__ double x_prim_t(const XHot& p, V3 o, V3 d, double tmin) {
-    if (p.kind == 0) {   // Möller–Trumbore, two-sided
+    if (p.kind == 0) {   // Möller–Trumbore, two-sided, barycentric tests on the numerators (no 1/det)
         const V3 e1 = ld3(p.b), e2 = ld3(p.c);
         const V3 pv = cross(d, e2);
         const double det = dot(e1, pv);
         if (det == 0.0) return INFINITY;
-        const double inv = 1.0 / det;
         const V3 tv = o - ld3(p.a);
-        const double u = dot(tv, pv) * inv;
-        if (u < 0.0 || u > 1.0) return INFINITY;
+        const double un = dot(tv, pv);
+        if (det > 0.0 ? (un < 0.0 || un > det) : (un > 0.0 || un < det)) return INFINITY;
         const V3 qv = cross(tv, e1);
-        const double v = dot(d, qv) * inv;
-        if (v < 0.0 || u + v > 1.0) return INFINITY;
-        const double t = dot(e2, qv) * inv;
+        const double vn = dot(d, qv);
+        const double uvn = un + vn;
+        if (det > 0.0 ? (vn < 0.0 || uvn > det) : (vn > 0.0 || uvn < det)) return INFINITY;
+        const double t = dot(e2, qv) / det;
         return (t > tmin) ? t : INFINITY;
     }
     const V3 oc = o - ld3(p.a);
@@ -403,6 +398,15 @@ __device__ __forceinline__ uint32_t children_mask(const XWNode* nd, F3 of, F3 iv
     return m;
 }
 
+__device__ __forceinline__ bool root_hit(const DevScene& sc, F3 of, F3 ivf) {
+    const float tx0 = (sc.root_lo[0] - of.x) * ivf.x, tx1 = (sc.root_hi[0] - of.x) * ivf.x;
+    const float ty0 = (sc.root_lo[1] - of.y) * ivf.y, ty1 = (sc.root_hi[1] - of.y) * ivf.y;
+    const float tz0 = (sc.root_lo[2] - of.z) * ivf.z, tz1 = (sc.root_hi[2] - of.z) * ivf.z;
+    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+    const float tf = fminf(fmaxf(tx0, tx1), fminf(fmaxf(ty0, ty1), fmaxf(tz0, tz1)));
+    return tn <= tf;
+}
+
 __device__ void x_texcoord(const DevScene& sc, const REnt& e, V3 ip, int32_t& x, int32_t& y) {
     if (e.kind == K_IMP_SPHERE) {
         const double r = e.radius;
@@ -415,16 +419,12 @@ __device__ void x_texcoord(const DevScene& sc, const REnt& e, V3 ip, int32_t& x,
         const double unit_h = 2.0 * REF_PI * small_r / 320.0;
         x = x86_trunc(small_r * mx_acos(ch) / unit_h);
     } else if (e.kind == K_IMP_TRIANGLE) {
-        const TriRec& t = sc.tris[e.tri_first];
-        const V3 p1 = ld3(t.p1), p2 = ld3(t.p2), p3 = ld3(t.p3);
-        const V3 p21 = p2 - p1, p31 = p3 - p1, p32 = p3 - p2, i1 = ip - p1;
-        const double p21l = gsqrt(sq3(p21)), i1l = gsqrt(sq3(i1));
-        const double c = dot(p21, i1) / (p21l * i1l);
+        const V3 p1 = ld3(e.qv0), p21 = ld3(e.qv1), i1 = ip - p1;
+        const double i1l = gsqrt(sq3(i1));
+        const double c = dot(p21, i1) / (e.qv2[0] * i1l);
         const double ixl = i1l * mx_sin_acos(c);
-        const double vl = gsqrt(sq3(0.5 * (p21 + p31)));
-        const double hl = gsqrt(sq3(0.5 * ((-p32) + (-p31))));
-        y = x86_trunc(i1l / (hl / 160.0));
-        x = x86_trunc(ixl / (vl / 160.0));
+        y = x86_trunc(i1l / e.qv2[2]);
+        x = x86_trunc(ixl / e.qv2[1]);
     } else if (e.kind == K_EXP_QUAD) {
         const double uv = (double)e.width / 160.0, uh = (double)e.length / 160.0;
         const V3 rv = ld3(e.qv0) - ld3(e.qv1), i1 = ip - ld3(e.qv1);
@@ -488,13 +488,13 @@ __device__ void x_texcoord(const DevScene& sc, const REnt& e, V3 ip, int32_t& x,
 // live lanes have a finished ray, or when none is still traversing, so it executes with a
 // well-filled EXEC mask.  The per-path operation sequence is exactly the oracle's (pixel_mode_x in
 // oracle/gi_oracle.cpp), so results are bit-identical whatever the schedule.
-enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD = 4 };
+enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD = 4, PH_DONEPX = 5 };
 
 #ifndef GI_X_PRIM_PREFILTER
 #define GI_X_PRIM_PREFILTER 0   // fp32 AABB cull before each fp64 primitive test (measured slower: +1 dependent load)
 #endif
-#ifndef GI_X_HANDLE_QUARTERS
-#define GI_X_HANDLE_QUARTERS 2   // shade once >= this many quarters of the live lanes wait
+#ifndef GI_X_START_BURST
+#define GI_X_START_BURST 16   // primary rays a lane may resolve by the root test per handler run
 #endif
 #ifndef GI_X_MIN_WAVES
 #define GI_X_MIN_WAVES 1   // minimum waves per SIMD for k_mode_x (register budget knob)
@@ -502,13 +502,17 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 
 struct XCounters {
     uint64_t rays = 0, nodes = 0, prims = 0, px = 0, box = 0;
+    uint64_t iters = 0, trav = 0, handle = 0, hlanes = 0, hclose = 0, hshadow = 0;   // wave-level (lane 0)
+    uint64_t cyc_trav = 0, cyc_hit = 0, cyc_next = 0, cyc_all = 0;                    // wave clock cycles
 };
 
+template <bool STATS>
 __device__ __forceinline__ void mode_x_wave(const DevScene& sc, const CamDev& cam, V3 light, const TileMap& m, int spp,
                                             int depth, uint64_t seed, double* rgb, uint8_t* rgb8, unsigned* slot_counter,
-                                            XCounters& cnt) {
+                                            int handle8, int xflags, XCounters& cnt) {
     const int lane = threadIdx.x & 63;
     const unsigned n_slots = (unsigned)(m.n_local * (kTile * kTile));
+    const bool inline_shadow = (xflags & 1) != 0;
     uint32_t nnode = 0, nprim = 0, nrays = 0, nbox = 0, npx = 0;
     long long idx = -1;
     int x = 0, y = 0;
@@ -524,13 +528,15 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, const CamDev& ca
     double tbest = INFINITY, tmax = INFINITY;
     float tbest_f = INFINITY;
     F3 of = f3(0, 0, 0), ivf = f3(1, 1, 1);
-    // path
-    V3 L = v3(0, 0, 0), T = v3(1, 1, 1);
+    // path: Lv = L while the closest ray is traced; across the shadow ray Lv / Lo hold the two
+    // candidate sums L + T*lit (light visible) and L + T*dark (occluded), and T already holds the
+    // next bounce's throughput (the oracle's operations, split around the shadow query)
+    V3 Lv = v3(0, 0, 0), Lo = v3(0, 0, 0), T = v3(1, 1, 1);
     double s0 = 0, s1 = 0, s2 = 0;
-    // carried across the shadow ray
-    V3 P = v3(0, 0, 0), nextd = v3(0, 0, 0), lit = v3(0, 0, 0), dark = v3(0, 0, 0), Tn = v3(0, 0, 0);
+    V3 nextd = v3(0, 0, 0);   // carried across the shadow ray (its origin = the shadow ray's)
     bool has_next = false;
 
+    const uint64_t t_begin = STATS ? clock64() : 0;
     for (;;) {
         const unsigned long long m_live = __ballot(phase != PH_DEAD);
         if (m_live == 0) break;
@@ -538,57 +544,106 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, const CamDev& ca
         const unsigned long long m_trav = __ballot(trav);
         const int n_wait = __popcll(m_live & ~m_trav);
         const bool handle = phase != PH_DEAD && !trav &&
-                            (4 * n_wait >= GI_X_HANDLE_QUARTERS * __popcll(m_live) || m_trav == 0);
-        if (trav) {
-            // ---- one traversal step (stackless: 8-bit "children left" mask per level) --------
-            uint32_t msk = lvl_get(mlo, mhi, level);
-            while (msk == 0 && level > 0) {   // climb to the nearest level with children left
-                node = sc.xwnodes[node].parent;
-                --level;
-                msk = lvl_get(mlo, mhi, level);
+                            (8 * n_wait >= handle8 * __popcll(m_live) || m_trav == 0);
+        if (STATS) {   // ballots over the whole wave, accumulated by lane 0
+            const unsigned long long m_h = __ballot(handle);
+            const unsigned long long m_hc = __ballot(handle && phase == PH_CLOSEST);
+            const unsigned long long m_hs = __ballot(handle && phase == PH_SHADOW);
+            if (lane == 0) {
+                ++cnt.iters;
+                cnt.trav += __popcll(m_trav);
+                if (m_h) {
+                    ++cnt.handle;
+                    cnt.hlanes += __popcll(m_h);
+                    cnt.hclose += __popcll(m_hc);
+                    cnt.hshadow += __popcll(m_hs);
+                }
             }
-            if (msk == 0) {
-                raying = false;               // ray finished
-            } else {
-                const int k = __builtin_ctz(msk);          // next child in front-to-back order
-                lvl_set(mlo, mhi, level, msk & (msk - 1));
-                const int c = k ^ dmask;
-                const XWNode* nd = sc.xwnodes + node;
-                const int ch = nd->child[c];
-                // a closer hit may have arrived since the mask was computed: re-cull this child
-                bool keep = true;
-                if (phase == PH_CLOSEST && best >= 0) keep = child_hit(nd, c, of, ivf, tbest_f);
-                if (keep) {
-                    if (ch < 0) {             // leaf: fp64 primitive tests (these decide the result)
-                        const XHot* hp = sc.xhot + ~ch;
-                        const XBox* bp = sc.xbox + ~ch;
-                        const int cntl = nd->cnt[c];
-                        for (int j = 0; j < cntl; ++j) {
+        }
+        const uint64_t t0 = STATS ? clock64() : 0;
+        if (trav) {
+            // ---- one traversal step (stackless: 8-bit "children left" mask per level).  Invariant:
+            // the current level has a child left; the step pops it, then climbs past exhausted
+            // levels, so a ray ends in the step that exhausts the root level (no empty iteration).
+            const uint32_t msk = lvl_get(mlo, mhi, level);
+            const int k = __builtin_ctz(msk);          // next child in front-to-back order
+            lvl_set(mlo, mhi, level, msk & (msk - 1));
+            const int c = k ^ dmask;
+            const XWNode* nd = sc.xwnodes + node;
+            const int ch = nd->child[c];
+            // a closer hit may have arrived since the mask was computed: re-cull this child
+            bool keep = true;
+            if (phase == PH_CLOSEST && best >= 0) keep = child_hit(nd, c, of, ivf, tbest_f);
+            if (keep) {
+                if (ch < 0) {             // leaf: fp64 primitive tests (these decide the result)
+                    const XHot* hp = sc.xhot + ~ch;
+                    const XBox* bp = sc.xbox + ~ch;
+                    const int cntl = nd->cnt[c];
+                    for (int j = 0; j < cntl; ++j) {
 #if GI_X_PRIM_PREFILTER
-                            ++nbox;
-                            if (!box32_hit(bp[j], of, ivf, tbest_f)) continue;   // conservative fp32 cull
+                        ++nbox;
+                        if (!box32_hit(bp[j], of, ivf, tbest_f)) continue;   // conservative fp32 cull
 #endif
-                            ++nprim;
-                            const double t = x_prim_t(hp[j], o, d, MX_TMIN);
-                            const int pi = hp[j].prim;
-                            if (phase == PH_SHADOW) {
-                                if (t < tmax) { best = pi; raying = false; break; }   // any hit occludes
-                            } else if (t < tbest || (t == tbest && pi < best)) {
-                                tbest = t;
-                                best = pi;
-                                tbest_f = up32(t);
-                            }
+                        ++nprim;
+                        const double t = x_prim_t(hp[j], o, d, MX_TMIN);
+                        const int pi = hp[j].prim;
+                        if (phase == PH_SHADOW) {
+                            if (t < tmax) { best = pi; raying = false; break; }   // any hit occludes
+                        } else if (t < tbest || (t == tbest && pi < best)) {
+                            tbest = t;
+                            best = pi;
+                            tbest_f = up32(t);
                         }
-                        (void)bp;
-                    } else {                  // descend: cull the child's 8 children in fp32
-                        ++nnode;
+                    }
+                    (void)bp;
+                } else {                  // descend if any of the child's 8 children is hit (fp32)
+                    ++nnode;
+                    const uint32_t cm = children_mask(sc.xwnodes + ch, of, ivf, tbest_f, dmask);
+                    if (cm) {
                         node = ch;
                         ++level;
-                        lvl_set(mlo, mhi, level, children_mask(sc.xwnodes + ch, of, ivf, tbest_f, dmask));
+                        lvl_set(mlo, mhi, level, cm);
                     }
                 }
             }
-        } else if (handle) {
+            if (raying) {                 // climb to the nearest level with children left
+                uint32_t rest = lvl_get(mlo, mhi, level);
+                while (rest == 0 && level > 0) {
+                    node = sc.xwnodes[node].parent;
+                    --level;
+                    rest = lvl_get(mlo, mhi, level);
+                }
+                if (rest == 0) raying = false;   // ray finished
+            }
+            // a finished shadow ray whose path continues: resolve it and start the next bounce
+            // right here (the bounce direction was drawn when the hit was shaded), so the lane
+            // keeps traversing instead of waiting for the shading handler (short-traversal scenes;
+            // for long ones the extra divergent root test costs more than it saves)
+            if (inline_shadow && !raying && phase == PH_SHADOW && has_next) {
+                ++nrays;
+                if (best >= 0) Lv = Lo;   // occluded: ambient term only
+                d = nextd;                // o is still the hit point
+                ++b;
+                phase = PH_CLOSEST;
+                tmax = INFINITY;
+                tbest = INFINITY;
+                tbest_f = INFINITY;
+                of = f3((float)o.x, (float)o.y, (float)o.z);
+                ivf = f3(__builtin_amdgcn_rcpf((float)d.x), __builtin_amdgcn_rcpf((float)d.y),
+                         __builtin_amdgcn_rcpf((float)d.z));
+                dmask = (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
+                const uint32_t rm = children_mask(sc.xwnodes, of, ivf, tbest_f, dmask);
+                best = -1;
+                node = 0;
+                level = 0;
+                mlo = mhi = 0;
+                lvl_set(mlo, mhi, 0, rm);
+                raying = rm != 0;
+            }
+        }
+        const uint64_t t1 = STATS ? clock64() : 0;
+        uint64_t t2 = t1;
+        if (handle) {
             // ---- the lane's ray is finished: consume it, spawn the next one --------------------
             bool end_path = false;
             if (phase == PH_CLOSEST) {
@@ -598,7 +653,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, const CamDev& ca
                 } else {
                     const XPrim& p = sc.xprims[best];   // by reference: only used fields are loaded
                     const REnt& e = sc.ents[p.ent];
-                    P = o + tbest * d;
+                    const V3 P = o + tbest * d;
                     V3 N = p.kind == 0 ? ld3(p.n) : normalize(P - ld3(p.a));
                     if (!(dot(d, N) < 0)) N = -N;
                     int32_t tu, tv;
@@ -613,11 +668,12 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, const CamDev& ca
                     const double spw = mx_powi(smax(0.0, dot(N, bis)), (int)e.spec_pow);
                     const V3 ls = v3(spw, spw, spw) * e.shader[2];
                     const V3 lo = (la + ldf) + ls;
-                    lit = v3(smin(lo.x, 1.0), smin(lo.y, 1.0), smin(lo.z, 1.0));
-                    dark = v3(smin(la.x, 1.0), smin(la.y, 1.0), smin(la.z, 1.0));
+                    Lo = Lv + vmul(T, v3(smin(la.x, 1.0), smin(la.y, 1.0), smin(la.z, 1.0)));
+                    Lv = Lv + vmul(T, v3(smin(lo.x, 1.0), smin(lo.y, 1.0), smin(lo.z, 1.0)));
                     has_next = false;
                     if (b != depth - 1) {
-                        Tn = vmul(T, tc * 0.5);
+                        const V3 Tn = vmul(T, tc * 0.5);
+                        T = Tn;
                         if (!(Tn.x == 0.0 && Tn.y == 0.0 && Tn.z == 0.0)) {
                             double sx = 0, sy = 0, r2 = 0;
                             for (int k = 0; k < 16; ++k) {
@@ -646,14 +702,11 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, const CamDev& ca
                 }
             } else if (phase == PH_SHADOW) {
                 ++nrays;
-                const V3 loc = best < 0 ? lit : dark;
-                L = L + vmul(T, loc);
+                if (best >= 0) Lv = Lo;   // occluded: ambient term only
                 if (!has_next) {
                     end_path = true;
                 } else {
-                    T = Tn;
-                    o = P;
-                    d = nextd;
+                    d = nextd;   // o is still the hit point
                     ++b;
                     phase = PH_CLOSEST;
                     tmax = INFINITY;
@@ -662,11 +715,19 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, const CamDev& ca
                 }
             }
             if (end_path) {
-                s0 = s0 + L.x; s1 = s1 + L.y; s2 = s2 + L.z;
+                s0 = s0 + Lv.x; s1 = s1 + Lv.y; s2 = s2 + Lv.z;
                 ++smp;
-                if (smp < spp) {
-                    phase = PH_START;
-                } else {              // pixel complete
+                phase = smp < spp ? PH_START : PH_DONEPX;
+            }
+            if (STATS) t2 = clock64();
+            // ---- the lane's next ray.  A primary ray that misses every child box of the root
+            // cannot hit anything: its sample adds exactly +0 to the pixel sums (the oracle traces
+            // it and adds L = 0), so it is resolved here and the lane moves on to its next sample,
+            // next pixel (fetched from the slot counter, one atomic per wave) -- up to
+            // GI_X_START_BURST primary rays per lane per handler run.
+            int burst = 0;
+            for (;;) {
+                if (phase == PH_DONEPX) {   // pixel complete
                     const double c0 = smin(s0 / (double)spp, 1.0), c1 = smin(s1 / (double)spp, 1.0),
                                  c2 = smin(s2 / (double)spp, 1.0);
                     if (rgb) { rgb[3 * idx] = c0; rgb[3 * idx + 1] = c1; rgb[3 * idx + 2] = c2; }
@@ -674,57 +735,81 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, const CamDev& ca
                     ++npx;
                     phase = PH_NEED;
                 }
-            }
-            // ---- lanes without a pixel take the next slots (one atomic per wave) ---------------
-            const unsigned long long m_need = __ballot(phase == PH_NEED);
-            if (m_need) {
-                const int leader = __ffsll((long long)m_need) - 1;
-                unsigned base = 0;
-                if (lane == leader) base = atomicAdd(slot_counter, (unsigned)__popcll(m_need));
-                base = __shfl(base, leader);
-                if (phase == PH_NEED) {
-                    const unsigned sl = base + (unsigned)__popcll(m_need & ((1ull << lane) - 1));
-                    if (sl >= n_slots) {
-                        phase = PH_DEAD;
-                    } else if (slot_pixel(m, (long long)(sl >> 6), (int)(sl & 63), idx, x, y)) {
-                        y += m.y0;
-                        key = mx_key(seed, (uint64_t)y * (uint64_t)m.w + (uint64_t)x);
-                        smp = 0;
-                        s0 = s1 = s2 = 0;
-                        phase = PH_START;
-                    } else if (idx >= 0 && m.shard_count > 1) {   // padding slot of a packed tile
-                        if (rgb) { rgb[3 * idx] = 0; rgb[3 * idx + 1] = 0; rgb[3 * idx + 2] = 0; }
-                        if (rgb8) { rgb8[3 * idx] = 0; rgb8[3 * idx + 1] = 0; rgb8[3 * idx + 2] = 0; }
+                const unsigned long long m_need = __ballot(phase == PH_NEED);
+                if (m_need) {
+                    const int leader = __ffsll((long long)m_need) - 1;
+                    unsigned base = 0;
+                    if (lane == leader) base = atomicAdd(slot_counter, (unsigned)__popcll(m_need));
+                    base = __shfl(base, leader);
+                    if (phase == PH_NEED) {
+                        const unsigned sl = base + (unsigned)__popcll(m_need & ((1ull << lane) - 1));
+                        if (sl >= n_slots) {
+                            phase = PH_DEAD;
+                        } else if (slot_pixel(m, (long long)(sl >> 6), (int)(sl & 63), idx, x, y)) {
+                            y += m.y0;
+                            key = mx_key(seed, (uint64_t)y * (uint64_t)m.w + (uint64_t)x);
+                            smp = 0;
+                            s0 = s1 = s2 = 0;
+                            phase = PH_START;
+                        } else if (idx >= 0 && m.shard_count > 1) {   // padding slot of a packed tile
+                            if (rgb) { rgb[3 * idx] = 0; rgb[3 * idx + 1] = 0; rgb[3 * idx + 2] = 0; }
+                            if (rgb8) { rgb8[3 * idx] = 0; rgb8[3 * idx + 1] = 0; rgb8[3 * idx + 2] = 0; }
+                        }
                     }
                 }
-            }
-            if (phase == PH_START) {
-                double jx = 0.0, jy = 0.0;
-                if (spp > 1) { jx = mx_u01k(key, smp, 0xFFFF, 0); jy = mx_u01k(key, smp, 0xFFFF, 1); }
-                o = cam.pos;
-                d = normalize(primary_dir(cam, (double)x + jx, (double)y + jy));
-                L = v3(0, 0, 0);
-                T = v3(1, 1, 1);
-                b = 0;
-                phase = PH_CLOSEST;
-                tmax = INFINITY;
-                tbest = INFINITY;
-                tbest_f = INFINITY;
-            }
-            if (phase == PH_CLOSEST || phase == PH_SHADOW) {   // start traversing the new ray
-                const V3 inv = v3(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+                if (phase == PH_NEED) continue;   // got a padding slot: take another
+                if (phase == PH_DEAD) break;
+                if (phase == PH_START) {
+                    double jx = 0.0, jy = 0.0;
+                    if (spp > 1) { jx = mx_u01k(key, smp, 0xFFFF, 0); jy = mx_u01k(key, smp, 0xFFFF, 1); }
+                    const V3 d0 = primary_dir(cam, (double)x + jx, (double)y + jy);
+                    if (burst < GI_X_START_BURST) {
+                        // conservative fp32 test of the scene's root box on the unnormalised
+                        // direction (slab test is scale-invariant; the padding covers rounding)
+                        const F3 iv0 = f3(__builtin_amdgcn_rcpf((float)d0.x), __builtin_amdgcn_rcpf((float)d0.y),
+                                          __builtin_amdgcn_rcpf((float)d0.z));
+                        if (!root_hit(sc, f3((float)cam.pos.x, (float)cam.pos.y, (float)cam.pos.z), iv0)) {
+                            ++nrays;   // background sample: L = 0, sums unchanged
+                            ++burst;
+                            ++smp;
+                            phase = smp < spp ? PH_START : PH_DONEPX;
+                            continue;
+                        }
+                    }
+                    o = cam.pos;
+                    d = normalize(d0);
+                    Lv = v3(0, 0, 0);
+                    T = v3(1, 1, 1);
+                    b = 0;
+                    tmax = INFINITY;
+                    tbest = INFINITY;
+                    tbest_f = INFINITY;
+                }
+                // start traversing the lane's ray (fp32 reciprocal, 1 ulp: the culling error stays
+                // far inside the 1e-5*extent box padding)
                 of = f3((float)o.x, (float)o.y, (float)o.z);
-                ivf = f3((float)inv.x, (float)inv.y, (float)inv.z);
+                ivf = f3(__builtin_amdgcn_rcpf((float)d.x), __builtin_amdgcn_rcpf((float)d.y),
+                         __builtin_amdgcn_rcpf((float)d.z));
                 dmask = (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
+                const uint32_t rm = children_mask(sc.xwnodes, of, ivf, tbest_f, dmask);
+                if (phase == PH_START) phase = PH_CLOSEST;
                 best = -1;
                 node = 0;   // root wide node
                 level = 0;
                 mlo = mhi = 0;
-                lvl_set(mlo, mhi, 0, children_mask(sc.xwnodes, of, ivf, tbest_f, dmask));
-                raying = true;
+                lvl_set(mlo, mhi, 0, rm);
+                raying = rm != 0;   // no root child hit: finished (consumed by the next handler run)
+                break;
             }
         }
+        if (STATS) {
+            const uint64_t t3 = clock64();
+            cnt.cyc_trav += t1 - t0;
+            cnt.cyc_hit += t2 - t1;
+            cnt.cyc_next += t3 - t2;
+        }
     }
+    if (STATS) cnt.cyc_all += clock64() - t_begin;
     cnt.rays += nrays;
     cnt.nodes += nnode;
     cnt.prims += nprim;
@@ -738,10 +823,23 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, const CamDev& ca
 template <bool STATS>
 __global__ __launch_bounds__(256, GI_X_MIN_WAVES) void k_mode_x(DevScene sc, CamDev cam, V3 light, TileMap m, int spp, int depth,
                                                  uint64_t seed, double* rgb, uint8_t* rgb8,
-                                                 unsigned long long* stats, unsigned* slot_counter) {
+                                                 unsigned long long* stats, unsigned* slot_counter, int handle8,
+                                                 int xflags) {
     XCounters c;
-    mode_x_wave(sc, cam, light, m, spp, depth, seed, rgb, rgb8, slot_counter, c);
+    mode_x_wave<STATS>(sc, cam, light, m, spp, depth, seed, rgb, rgb8, slot_counter, handle8, xflags, c);
     if (STATS) {
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(stats + GI_STAT_X_ITERS, (unsigned long long)c.iters);
+            atomicAdd(stats + GI_STAT_X_TRAV, (unsigned long long)c.trav);
+            atomicAdd(stats + GI_STAT_X_HANDLE, (unsigned long long)c.handle);
+            atomicAdd(stats + GI_STAT_X_HLANES, (unsigned long long)c.hlanes);
+            atomicAdd(stats + GI_STAT_X_HCLOSE, (unsigned long long)c.hclose);
+            atomicAdd(stats + GI_STAT_X_HSHADOW, (unsigned long long)c.hshadow);
+            atomicAdd(stats + GI_STAT_X_CYC_TRAV, (unsigned long long)c.cyc_trav);
+            atomicAdd(stats + GI_STAT_X_CYC_HIT, (unsigned long long)c.cyc_hit);
+            atomicAdd(stats + GI_STAT_X_CYC_NEXT, (unsigned long long)c.cyc_next);
+            atomicAdd(stats + GI_STAT_X_CYC_ALL, (unsigned long long)c.cyc_all);
+        }
         wave_add_stats(stats, c.rays, c.nodes, c.prims, c.px);
         uint64_t cb = c.box;
         for (int off = 32; off > 0; off >>= 1) cb += __shfl_xor(cb, off);
@@ -839,10 +937,24 @@ hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w,
         const dim3 pgrid((unsigned)std::min<long long>(want, resident_blocks));
         hipError_t e = hipMemsetAsync(sc.work, 0, 16 * sizeof(unsigned), stream);
         if (e != hipSuccess) return e;
+        // shading-handler threshold (eighths of the live lanes that must wait): the builder's
+        // estimate for the scene (DevScene::x_handle8), overridable for tuning with GI_X_HANDLE8
+        static int env_h8 = -1;
+        if (env_h8 == -1) {
+            const char* v = std::getenv("GI_X_HANDLE8");
+            env_h8 = v ? std::max(1, std::min(8, std::atoi(v))) : 0;
+        }
+        const int h8 = env_h8 > 0 ? env_h8 : sc.x_handle8;
+        static int env_xf = -2;   // GI_X_FLAGS overrides the builder's choice (bit 0: inline shadow)
+        if (env_xf == -2) {
+            const char* v = std::getenv("GI_X_FLAGS");
+            env_xf = v ? std::atoi(v) : -1;
+        }
+        const int xf = env_xf >= 0 ? env_xf : sc.x_flags;
         if (stats)
-            hipLaunchKernelGGL(k_mode_x<true>, pgrid, block, 0, stream, sc, cam, light, m, o.spp, o.depth, o.seed, rgb, rgb8, st, sc.work);
+            hipLaunchKernelGGL(k_mode_x<true>, pgrid, block, 0, stream, sc, cam, light, m, o.spp, o.depth, o.seed, rgb, rgb8, st, sc.work, h8, xf);
         else
-            hipLaunchKernelGGL(k_mode_x<false>, pgrid, block, 0, stream, sc, cam, light, m, o.spp, o.depth, o.seed, rgb, rgb8, st, sc.work);
+            hipLaunchKernelGGL(k_mode_x<false>, pgrid, block, 0, stream, sc, cam, light, m, o.spp, o.depth, o.seed, rgb, rgb8, st, sc.work, h8, xf);
     }
     return hipGetLastError();
 }

@@ -109,6 +109,9 @@ struct HostScene {
     std::vector<XBox> xbox;
     std::vector<XPrim> xprims;
     int32_t x_max_depth = 0;
+    int32_t x_handle8 = 6;   // Mode X handler threshold (eighths), chosen by the builder
+    int32_t x_flags = 0;     // Mode X schedule flags (DevScene::x_flags), chosen by the builder
+    double x_est_nodes = 0, x_est_prims = 0;   // SAH estimates per random ray through the root
 };
 
 // Mode X 8-wide BVH over the primitives (gi_bvh.cpp); bounds: 6 doubles (min xyz, max xyz) each.
@@ -126,7 +129,10 @@ struct DevScene {
     const XPrim* xprims;
     unsigned* work;        // 16 device counters (persistent-kernel tile queue), reset per launch
     int32_t n_rnodes, n_ents, n_xwnodes, n_xprims;
-    int32_t x_max_depth, pad;
+    int32_t x_max_depth;
+    int32_t x_handle8;     // Mode X shading-handler threshold, eighths of the live lanes (set at upload)
+    int32_t x_flags;       // Mode X schedule flags: bit 0 = continue paths from shadow rays in traversal
+    float root_lo[3], root_hi[3];   // Mode X: union of the root's fp32 child boxes (conservative)
 };
 
 }  // namespace gi

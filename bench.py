@@ -17,7 +17,8 @@ HBM.  The ray count per frame is exact: a counting launch (GI_FLAG_STATS) of the
 deterministic frame runs before the timed region.
 
 roofline: the dominant kernel (k_mode_x) against HBM: achieved = algorithmic bytes per launch
-(node records x 64 B + primitive records x 112 B + 27 B/pixel output) /
+(Mode X: wide-node records x 256 B + primitive records x 80 B + 27 B/pixel output; Mode R: 64 B
+nodes + 144 B triangles) /
 average launch time from HIP events on the launch stream; traffic = HBM bytes per launch from the
 committed rocprofv3 PMC summary when present (profiles/), else null.
 cpu_baseline: this repo's CPU port of the same integrator (oracle, test infrastructure), OpenMP,
@@ -52,15 +53,16 @@ WORKLOADS = {
     "R-C4": ("soup100000", 1920, 1080, 0, 1, 1, "reference semantics (Mode R), 100k-triangle mesh, 1920x1080"),
     "R-C3": ("cornell", 1920, 1080, 0, 1, 1, "reference semantics (Mode R), Cornell box, 1920x1080"),
     "R-main": ("main", 500, 500, 0, 1, 1, "reference semantics (Mode R), main.cpp scene, 500x500"),
+    # extra Mode X scenes (tuning / coverage; not BASELINE configs)
+    "X-main": ("main", 1920, 1080, 1, 16, 8, "Mode X, main.cpp scene, 1920x1080, depth=8, 16 spp"),
+    "X-zoo": ("zoo", 1920, 1080, 1, 16, 8, "Mode X, every entity type, 1920x1080, depth=8, 16 spp"),
+    "X-soup1000": ("soup1000", 1920, 1080, 1, 16, 8, "Mode X, 1k-triangle soup, 1920x1080, depth=8, 16 spp"),
 }
 
 
 def make_scene(name):
     from importlib import import_module
-    S = import_module("2019global_amd.scenes")
-    if name.startswith("soup"):
-        return S.soup_scene(int(name[4:]))
-    return {"cornell": S.cornell_scene, "main": S.main_scene, "sphere": S.sphere_scene}[name]()
+    return import_module("2019global_amd.scenes").named_scene(name)
 
 
 def pmc_traffic(workload: str):
@@ -160,7 +162,7 @@ def main():
             frame8 = torch.empty(w * h * 3, dtype=torch.uint8, device="cuda")
 
     # exact work counts of this rank's share of the frame (same deterministic frame, untimed)
-    stats = torch.zeros(8, dtype=torch.int64, device="cuda")
+    stats = torch.zeros(gi.STATS_N, dtype=torch.int64, device="cuda")
     dev.render_device(cam, sc.light, w, h, buf.data_ptr(), buf8.data_ptr(), sptr, stats_ptr=stats.data_ptr(), **kw)
     torch.cuda.synchronize()
     if world > 1:
@@ -235,6 +237,18 @@ def main():
                          "node_visits": st[gi.STAT_NODES], "prim_tests": st[gi.STAT_PRIMS],
                          "prim_box_tests": st[gi.STAT_PBOX]},
         }
+        if mode == 1 and st[gi.STAT_X_ITERS]:   # k_mode_x schedule (STATS launch; wave = 64 lanes)
+            it, hd = st[gi.STAT_X_ITERS], max(1, st[gi.STAT_X_HANDLE])
+            out["schedule"] = {"wave_iterations": it, "lane_trav_steps": st[gi.STAT_X_TRAV],
+                               "trav_lane_fill": round(st[gi.STAT_X_TRAV] / (64.0 * it), 4),
+                               "handler_runs": st[gi.STAT_X_HANDLE],
+                               "handler_lane_fill": round(st[gi.STAT_X_HLANES] / (64.0 * hd), 4),
+                               "handler_closest_lanes": st[gi.STAT_X_HCLOSE],
+                               "handler_shadow_lanes": st[gi.STAT_X_HSHADOW],
+                               "iterations_per_ray": round(it * 64.0 / max(1, rays_frame), 3),
+                               "cycle_share": {k: round(st[i] / max(1, st[gi.STAT_X_CYC_ALL]), 4) for k, i in
+                                               (("traverse", gi.STAT_X_CYC_TRAV), ("consume", gi.STAT_X_CYC_HIT),
+                                                ("next_ray", gi.STAT_X_CYC_NEXT))}}
         if not args.no_cpu_baseline and world == 1:
             scn = sc.to_scn()
             out["cpu_baseline"] = cpu_baseline(scn, w, h, mode, spp, depth, args.seed)

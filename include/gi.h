@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define GI_ABI_VERSION 1
+#define GI_ABI_VERSION 2
 
 typedef enum gi_status {
     GI_OK = 0,
@@ -105,7 +105,17 @@ typedef struct gi_opts {
 #define GI_STAT_PRIMS 2       /* primitive records fetched & tested in fp64 */
 #define GI_STAT_PIXELS 3
 #define GI_STAT_PBOX 4        /* Mode X primitive prefilter boxes tested (32-B fp32 records) */
-#define GI_STATS_N 8
+#define GI_STAT_X_ITERS 5     /* Mode X: wave loop iterations (per wave) */
+#define GI_STAT_X_TRAV 6      /* Mode X: lane traversal steps (sum of active lanes over iterations) */
+#define GI_STAT_X_HANDLE 7    /* Mode X: shading-handler executions (per wave) */
+#define GI_STAT_X_HLANES 8    /* Mode X: lanes running the handler (sum over executions) */
+#define GI_STAT_X_HCLOSE 9    /* Mode X: of those, lanes consuming a closest hit */
+#define GI_STAT_X_HSHADOW 10  /* Mode X: of those, lanes consuming a shadow query */
+#define GI_STAT_X_CYC_TRAV 11 /* Mode X: wave clock cycles in traversal steps */
+#define GI_STAT_X_CYC_HIT 12  /* Mode X: wave clock cycles consuming finished rays (shading) */
+#define GI_STAT_X_CYC_NEXT 13 /* Mode X: wave clock cycles starting rays (raygen, pixel fetch, root test) */
+#define GI_STAT_X_CYC_ALL 14  /* Mode X: wave clock cycles in the whole loop */
+#define GI_STATS_N 16
 
 #define GI_TILE 8             /* shard granularity: 8x8 pixel tiles, dealt round-robin to ranks */
 

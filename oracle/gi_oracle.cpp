@@ -789,19 +789,21 @@ void build_prims(const Scene& s, std::vector<Prim>& prims) {
     }
 }
 
-// Möller–Trumbore, two-sided; returns t or +inf
+// Möller–Trumbore, two-sided, with the barycentric tests on the numerators (u = un/det in [0,1],
+// v = vn/det >= 0, u + v <= 1 compared as un, vn, un+vn against 0 and det, by the sign of det);
+// t = tn/det is the only division.  Returns t or +inf.
 double mx_tri_t(const Prim& p, V3 o, V3 d, double tmin) {
     const V3 pv = cross(d, p.e2);
     const double det = dot(p.e1, pv);
     if (det == 0.0) return INFINITY;
-    const double inv = 1.0 / det;
     const V3 tv = o - p.v0;
-    const double u = dot(tv, pv) * inv;
-    if (u < 0.0 || u > 1.0) return INFINITY;
+    const double un = dot(tv, pv);
+    if (det > 0.0 ? (un < 0.0 || un > det) : (un > 0.0 || un < det)) return INFINITY;
     const V3 qv = cross(tv, p.e1);
-    const double v = dot(d, qv) * inv;
-    if (v < 0.0 || u + v > 1.0) return INFINITY;
-    const double t = dot(p.e2, qv) * inv;
+    const double vn = dot(d, qv);
+    const double uvn = un + vn;
+    if (det > 0.0 ? (vn < 0.0 || uvn > det) : (vn > 0.0 || uvn < det)) return INFINITY;
+    const double t = dot(p.e2, qv) / det;
     return (t > tmin) ? t : INFINITY;
 }
 double mx_sph_t(const Prim& p, V3 o, V3 d, double tmin) {

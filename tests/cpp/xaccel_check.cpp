@@ -42,14 +42,14 @@ static double prim_t(const XHot& p, V3 o, V3 d, double tmin) {   // the kernel's
         const V3 pv = cross(d, e2);
         const double det = dot(e1, pv);
         if (det == 0.0) return INFINITY;
-        const double inv = 1.0 / det;
         const V3 tv = o - ld3(p.a);
-        const double u = dot(tv, pv) * inv;
-        if (u < 0.0 || u > 1.0) return INFINITY;
+        const double un = dot(tv, pv);
+        if (det > 0.0 ? (un < 0.0 || un > det) : (un > 0.0 || un < det)) return INFINITY;
         const V3 qv = cross(tv, e1);
-        const double v = dot(d, qv) * inv;
-        if (v < 0.0 || u + v > 1.0) return INFINITY;
-        const double t = dot(e2, qv) * inv;
+        const double vn = dot(d, qv);
+        const double uvn = un + vn;
+        if (det > 0.0 ? (vn < 0.0 || uvn > det) : (vn > 0.0 || uvn < det)) return INFINITY;
+        const double t = dot(e2, qv) / det;
         return (t > tmin) ? t : INFINITY;
     }
     const V3 oc = o - ld3(p.a);
@@ -102,48 +102,56 @@ static void lvl_set(uint64_t& lo, uint64_t& hi, int l, uint32_t m) {
 // k_mode_x's traversal of one ray; shadow: any hit with t < tmax
 static long g_prim_tests = 0;
 static int traverse(const HostScene& s, V3 o, V3 d, bool shadow, double tmax, double& tbest, long& visits) {
-    const V3 inv = v3(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
-    const F3 of = {(float)o.x, (float)o.y, (float)o.z}, ivf = {(float)inv.x, (float)inv.y, (float)inv.z};
+    // the device uses v_rcp_f32 (1 ulp) here; the correctly rounded fp32 reciprocal stands in for it
+    const F3 of = {(float)o.x, (float)o.y, (float)o.z}, ivf = {1.0f / (float)d.x, 1.0f / (float)d.y, 1.0f / (float)d.z};
     const int dmask = (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
     tbest = shadow ? tmax : INFINITY;
     float tbest_f = shadow ? up32(tmax) : INFINITY;
     int best = -1, node = 0, level = 0;
     uint64_t mlo = 0, mhi = 0;
-    lvl_set(mlo, mhi, 0, children_mask(&s.xwnodes[0], of, ivf, tbest_f, dmask));
-    for (;;) {
-        uint32_t msk = lvl_get(mlo, mhi, level);
-        while (msk == 0 && level > 0) {
-            node = s.xwnodes[node].parent;
-            --level;
-            msk = lvl_get(mlo, mhi, level);
-        }
-        if (msk == 0) break;
+    const uint32_t rm = children_mask(&s.xwnodes[0], of, ivf, tbest_f, dmask);
+    lvl_set(mlo, mhi, 0, rm);
+    bool raying = rm != 0;
+    while (raying) {   // one iteration = one traversal step of k_mode_x
+        const uint32_t msk = lvl_get(mlo, mhi, level);
         const int k = __builtin_ctz(msk);
         lvl_set(mlo, mhi, level, msk & (msk - 1));
         const int c = k ^ dmask;
         const XWNode* nd = &s.xwnodes[node];
         const int ch = nd->child[c];
-        if (!shadow && best >= 0 && !child_hit(nd, c, of, ivf, tbest_f)) continue;
-        if (ch < 0) {
-            for (int j = 0; j < nd->cnt[c]; ++j) {
-                const XHot& h = s.xhot[~ch + j];
-                const double t = prim_t(h, o, d, 1e-7);
-                ++g_prim_tests;
-                if (shadow) {
-                    if (t < tmax) return h.prim;
-                } else if (t < tbest || (t == tbest && h.prim < best)) {
-                    tbest = t;
-                    best = h.prim;
-                    tbest_f = up32(t);
+        const bool keep = shadow || best < 0 || child_hit(nd, c, of, ivf, tbest_f);
+        if (keep) {
+            if (ch < 0) {
+                for (int j = 0; j < nd->cnt[c]; ++j) {
+                    const XHot& h = s.xhot[~ch + j];
+                    const double t = prim_t(h, o, d, 1e-7);
+                    ++g_prim_tests;
+                    if (shadow) {
+                        if (t < tmax) return h.prim;
+                    } else if (t < tbest || (t == tbest && h.prim < best)) {
+                        tbest = t;
+                        best = h.prim;
+                        tbest_f = up32(t);
+                    }
+                }
+            } else {
+                ++visits;
+                const uint32_t cm = children_mask(&s.xwnodes[ch], of, ivf, tbest_f, dmask);
+                if (cm) {
+                    node = ch;
+                    ++level;
+                    if (level > 15) { std::printf("depth overflow\n"); std::exit(3); }
+                    lvl_set(mlo, mhi, level, cm);
                 }
             }
-        } else {
-            ++visits;
-            node = ch;
-            ++level;
-            if (level > 15) { std::printf("depth overflow\n"); std::exit(3); }
-            lvl_set(mlo, mhi, level, children_mask(&s.xwnodes[ch], of, ivf, tbest_f, dmask));
         }
+        uint32_t rest = lvl_get(mlo, mhi, level);
+        while (rest == 0 && level > 0) {
+            node = s.xwnodes[node].parent;
+            --level;
+            rest = lvl_get(mlo, mhi, level);
+        }
+        if (rest == 0) raying = false;
     }
     return best;
 }
@@ -273,9 +281,10 @@ int main(int argc, char** argv) {
             ++total;
             if (shadow ? ((a >= 0) != (b >= 0)) : (a != b || !(t1 == t2 || (std::isinf(t1) && std::isinf(t2))))) ++mism;
         }
-        std::printf("scene %d: %zu prims, %zu wide nodes, %zu leaf records, depth %d; per ray: %.2f node visits, %.2f prim tests\n",
+        std::printf("scene %d: %zu prims, %zu wide nodes, %zu leaf records, depth %d; per ray: %.2f node visits, %.2f prim tests"
+                    " (SAH estimate %.2f / %.2f)\n",
                     scene, hs.xprims.size(), hs.xwnodes.size(), hs.xhot.size(), hs.x_max_depth,
-                    (double)(visits - visits0) / nrays, (double)(g_prim_tests - prims0) / nrays);
+                    (double)(visits - visits0) / nrays, (double)(g_prim_tests - prims0) / nrays, hs.x_est_nodes, hs.x_est_prims);
     }
     std::printf("rays %ld mismatches %ld wide-node visits %ld\n", total, mism, visits);
     return mism == 0 ? 0 : 1;

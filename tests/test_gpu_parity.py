@@ -238,7 +238,7 @@ def test_stats_counters(torch_cuda):
     sc = S.cornell_scene()
     d = dev_scene("cornell")
     w, h = 128, 128
-    st = torch.zeros(8, dtype=torch.int64, device="cuda")
+    st = torch.zeros(gi.STATS_N, dtype=torch.int64, device="cuda")
     buf = torch.zeros(w * h * 3, dtype=torch.float64, device="cuda")
     d.render_device(cam_of(sc), sc.light, w, h, buf.data_ptr(), stats_ptr=st.data_ptr())
     torch.cuda.synchronize()
