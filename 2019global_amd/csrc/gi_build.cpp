@@ -654,7 +654,8 @@ bool build_host_scene(const gi_scene_desc& desc, HostScene& hs, std::string& err
         for (int c = 0; c < 8; ++c) empty_slot(w, c);
         w.parent = -1;
         for (int c = 0; c < 8; ++c) w.cnt[c] = 0;
-        for (int c = 0; c < 3; ++c) w.pad[c] = 0;
+        w.exists = 0;
+        w.pad[0] = w.pad[1] = 0;
     }
     auto fill_slot = [&](XWNode& w, int c, const XNode& n, int32_t r) {
         for (int k = 0; k < 3; ++k) { w.lo[k][c] = lo32(n.mn[k]); w.hi[k][c] = hi32(n.mx[k]); }
@@ -682,6 +683,7 @@ bool build_host_scene(const gi_scene_desc& desc, HostScene& hs, std::string& err
                 }
         }
     }
+    finalize_xwnodes(hs.xwnodes);
     return true;
 }
 

@@ -170,10 +170,14 @@ void build_xbvh(const std::vector<XPrim>& prims, const std::vector<double>& boun
         blank.cnt[c] = 0;
     }
     blank.parent = -1;
-    blank.pad[0] = blank.pad[1] = blank.pad[2] = 0;
+    blank.exists = 0;
+    blank.pad[0] = blank.pad[1] = 0;
     hs.xwnodes.push_back(blank);   // root
     hs.x_max_depth = 0;
-    if (np == 0) return;
+    if (np == 0) {
+        finalize_xwnodes(hs.xwnodes);
+        return;
+    }
 
     Builder b;
     b.pb = &pb;
@@ -311,6 +315,7 @@ void build_xbvh(const std::vector<XPrim>& prims, const std::vector<double>& boun
         }
     };
     fill(0, root, 0);
+    finalize_xwnodes(hs.xwnodes);
 
     // surface-area estimates of the work per ray (a random line through the root box meets a box
     // with probability area(box) / area(root)): wide nodes entered and primitives tested

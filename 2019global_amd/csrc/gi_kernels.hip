@@ -343,19 +343,38 @@ __device__ __forceinline__ float up32(double v) {
     return f;
 }
 
+// One leaf record in registers: fetched by 5 independent 16-byte loads (one memory round trip),
+// so no load waits on a branch of the test.
+struct XHotR {
+    union {
+        int4 q[5];
+        XHot h;
+    };
+};
+__device__ __forceinline__ XHotR load_hot(const XHot* p) {
+    const int4* s = reinterpret_cast<const int4*>(p);
+    XHotR r;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) r.q[i] = s[i];
+    return r;
+}
+
+// Möller–Trumbore, two-sided, barycentric tests on the numerators (no 1/det); all products are
+// formed before the first branch.  Spheres (kind 1): the geometric quadratic.
 __device__ __forceinline__ double x_prim_t(const XHot& p, V3 o, V3 d, double tmin) {
-    if (p.kind == 0) {   // Möller–Trumbore, two-sided, barycentric tests on the numerators (no 1/det)
-        const V3 e1 = ld3(p.b), e2 = ld3(p.c);
+    if (p.kind == 0) {
+        const V3 e1 = ld3(p.b), e2 = ld3(p.c), v0 = ld3(p.a);
         const V3 pv = cross(d, e2);
         const double det = dot(e1, pv);
-        if (det == 0.0) return INFINITY;
-        const V3 tv = o - ld3(p.a);
+        const V3 tv = o - v0;
         const double un = dot(tv, pv);
-        if (det > 0.0 ? (un < 0.0 || un > det) : (un > 0.0 || un < det)) return INFINITY;
         const V3 qv = cross(tv, e1);
         const double vn = dot(d, qv);
         const double uvn = un + vn;
-        if (det > 0.0 ? (vn < 0.0 || uvn > det) : (vn > 0.0 || uvn < det)) return INFINITY;
+        const bool pos = det > 0.0;
+        const bool miss = det == 0.0 || (pos ? (un < 0.0 || un > det || vn < 0.0 || uvn > det)
+                                             : (un > 0.0 || un < det || vn > 0.0 || uvn < det));
+        if (miss) return INFINITY;
         const double t = dot(e2, qv) / det;
         return (t > tmin) ? t : INFINITY;
     }
@@ -389,12 +408,26 @@ __device__ __forceinline__ bool box32_hit(const XBox& b, F3 of, F3 ivf, float tm
     const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
     return tn <= tf;
 }
-// mask of hit, existing children with bit k for child k ^ dmask (bit order = front-to-back)
+// mask of hit, existing children with bit k for child k ^ dmask (bit order = front-to-back).
+// The node's 48 bounds are fetched by 12 independent 16-byte loads (one memory round trip) and
+// all 8 slab tests run branch-free; existence comes from the node's precomputed bit mask.
 __device__ __forceinline__ uint32_t children_mask(const XWNode* nd, F3 of, F3 ivf, float tmax, int dmask) {
+    const float4* b = reinterpret_cast<const float4*>(nd);
+    float4 q[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) q[i] = b[i];
+    const int ex = nd->exists;
+    const float* v = reinterpret_cast<const float*>(q);   // lo[3][8] then hi[3][8]
     uint32_t m = 0;
 #pragma unroll
-    for (int c = 0; c < 8; ++c)
-        if (nd->child[c] != XEMPTY && child_hit(nd, c, of, ivf, tmax)) m |= 1u << (c ^ dmask);
+    for (int c = 0; c < 8; ++c) {
+        const float tx0 = (v[c] - of.x) * ivf.x, tx1 = (v[24 + c] - of.x) * ivf.x;
+        const float ty0 = (v[8 + c] - of.y) * ivf.y, ty1 = (v[32 + c] - of.y) * ivf.y;
+        const float tz0 = (v[16 + c] - of.z) * ivf.z, tz1 = (v[40 + c] - of.z) * ivf.z;
+        const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+        const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
+        m |= (uint32_t)((tn <= tf) & ((ex >> c) & 1)) << (c ^ dmask);
+    }
     return m;
 }
 
@@ -506,10 +539,11 @@ struct XCounters {
     uint64_t cyc_trav = 0, cyc_hit = 0, cyc_next = 0, cyc_all = 0;                    // wave clock cycles
 };
 
-template <bool STATS>
-__device__ __forceinline__ void mode_x_wave(const DevScene& sc, const CamDev& cam, V3 light, const TileMap& m, int spp,
-                                            int depth, uint64_t seed, double* rgb, uint8_t* rgb8, unsigned* slot_counter,
-                                            int handle8, int xflags, XCounters& cnt) {
+template <bool STATS, typename NodeP, typename HotP>
+__device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H, const CamDev& cam, V3 light,
+                                            const TileMap& m, int spp, int depth, uint64_t seed, double* rgb,
+                                            uint8_t* rgb8, unsigned* slot_counter, int handle8, int xflags,
+                                            XCounters& cnt) {
     const int lane = threadIdx.x & 63;
     const unsigned n_slots = (unsigned)(m.n_local * (kTile * kTile));
     const bool inline_shadow = (xflags & 1) != 0;
@@ -569,24 +603,27 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, const CamDev& ca
             const int k = __builtin_ctz(msk);          // next child in front-to-back order
             lvl_set(mlo, mhi, level, msk & (msk - 1));
             const int c = k ^ dmask;
-            const XWNode* nd = sc.xwnodes + node;
+            const XWNode* nd = W + node;
             const int ch = nd->child[c];
             // a closer hit may have arrived since the mask was computed: re-cull this child
             bool keep = true;
             if (phase == PH_CLOSEST && best >= 0) keep = child_hit(nd, c, of, ivf, tbest_f);
             if (keep) {
                 if (ch < 0) {             // leaf: fp64 primitive tests (these decide the result)
-                    const XHot* hp = sc.xhot + ~ch;
+                    const XHot* hp = H + ~ch;
                     const XBox* bp = sc.xbox + ~ch;
                     const int cntl = nd->cnt[c];
+                    XHotR cur = load_hot(hp);   // records fetched one ahead of the test
                     for (int j = 0; j < cntl; ++j) {
+                        const XHotR rec = cur;
+                        cur = load_hot(hp + min(j + 1, cntl - 1));
 #if GI_X_PRIM_PREFILTER
                         ++nbox;
                         if (!box32_hit(bp[j], of, ivf, tbest_f)) continue;   // conservative fp32 cull
 #endif
                         ++nprim;
-                        const double t = x_prim_t(hp[j], o, d, MX_TMIN);
-                        const int pi = hp[j].prim;
+                        const double t = x_prim_t(rec.h, o, d, MX_TMIN);
+                        const int pi = rec.h.prim;
                         if (phase == PH_SHADOW) {
                             if (t < tmax) { best = pi; raying = false; break; }   // any hit occludes
                         } else if (t < tbest || (t == tbest && pi < best)) {
@@ -598,7 +635,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, const CamDev& ca
                     (void)bp;
                 } else {                  // descend if any of the child's 8 children is hit (fp32)
                     ++nnode;
-                    const uint32_t cm = children_mask(sc.xwnodes + ch, of, ivf, tbest_f, dmask);
+                    const uint32_t cm = children_mask(W + ch, of, ivf, tbest_f, dmask);
                     if (cm) {
                         node = ch;
                         ++level;
@@ -609,8 +646,8 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, const CamDev& ca
             if (raying) {                 // climb to the nearest level with children left
                 uint32_t rest = lvl_get(mlo, mhi, level);
                 while (rest == 0 && level > 0) {
-                    node = sc.xwnodes[node].parent;
                     --level;
+                    node = level == 0 ? 0 : W[node].parent;   // the root is node 0: no load
                     rest = lvl_get(mlo, mhi, level);
                 }
                 if (rest == 0) raying = false;   // ray finished
@@ -632,7 +669,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, const CamDev& ca
                 ivf = f3(__builtin_amdgcn_rcpf((float)d.x), __builtin_amdgcn_rcpf((float)d.y),
                          __builtin_amdgcn_rcpf((float)d.z));
                 dmask = (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
-                const uint32_t rm = children_mask(sc.xwnodes, of, ivf, tbest_f, dmask);
+                const uint32_t rm = children_mask(W, of, ivf, tbest_f, dmask);
                 best = -1;
                 node = 0;
                 level = 0;
@@ -791,7 +828,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, const CamDev& ca
                 ivf = f3(__builtin_amdgcn_rcpf((float)d.x), __builtin_amdgcn_rcpf((float)d.y),
                          __builtin_amdgcn_rcpf((float)d.z));
                 dmask = (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
-                const uint32_t rm = children_mask(sc.xwnodes, of, ivf, tbest_f, dmask);
+                const uint32_t rm = children_mask(W, of, ivf, tbest_f, dmask);
                 if (phase == PH_START) phase = PH_CLOSEST;
                 best = -1;
                 node = 0;   // root wide node
@@ -820,13 +857,31 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, const CamDev& ca
 // Persistent waves: the grid is sized to the resident capacity; every lane pulls pixel slots
 // from one device counter (SURVEY §7 hard part 4: per-ray cost varies ~10x between background
 // and scene pixels), so no lane idles behind a sibling, a workgroup or the grid tail.
-template <bool STATS>
+// LDS: small scenes (sc.x_lds_bytes > 0) keep the whole traversal structure -- wide nodes and
+// leaf records -- in LDS, copied once by each resident workgroup; every traversal load is then a
+// ds_read instead of a vector-memory round trip.
+template <bool STATS, bool LDS>
 __global__ __launch_bounds__(256, GI_X_MIN_WAVES) void k_mode_x(DevScene sc, CamDev cam, V3 light, TileMap m, int spp, int depth,
                                                  uint64_t seed, double* rgb, uint8_t* rgb8,
                                                  unsigned long long* stats, unsigned* slot_counter, int handle8,
                                                  int xflags) {
     XCounters c;
-    mode_x_wave<STATS>(sc, cam, light, m, spp, depth, seed, rgb, rgb8, slot_counter, handle8, xflags, c);
+    if (LDS) {
+        extern __shared__ int4 lds_scene[];
+        const int nw = sc.n_xwnodes * (int)(sizeof(XWNode) / sizeof(int4));
+        const int nh = sc.n_xhot * (int)(sizeof(XHot) / sizeof(int4));
+        const int4* gw = reinterpret_cast<const int4*>(sc.xwnodes);
+        const int4* gh = reinterpret_cast<const int4*>(sc.xhot);
+        for (int i = threadIdx.x; i < nw; i += blockDim.x) lds_scene[i] = gw[i];
+        for (int i = threadIdx.x; i < nh; i += blockDim.x) lds_scene[nw + i] = gh[i];
+        __syncthreads();
+        const XWNode* W = reinterpret_cast<const XWNode*>(lds_scene);
+        const XHot* H = reinterpret_cast<const XHot*>(lds_scene + nw);
+        mode_x_wave<STATS>(sc, W, H, cam, light, m, spp, depth, seed, rgb, rgb8, slot_counter, handle8, xflags, c);
+    } else {
+        mode_x_wave<STATS>(sc, sc.xwnodes, sc.xhot, cam, light, m, spp, depth, seed, rgb, rgb8, slot_counter, handle8,
+                           xflags, c);
+    }
     if (STATS) {
         if ((threadIdx.x & 63) == 0) {
             atomicAdd(stats + GI_STAT_X_ITERS, (unsigned long long)c.iters);
@@ -924,17 +979,28 @@ hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w,
         else hipLaunchKernelGGL(k_mode_r<false>, grid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st);
     } else {
         // persistent grid: as many 4-wave blocks as can be resident, each wave pulls tiles
-        static int resident_blocks = 0;
-        if (resident_blocks == 0) {
+        static int env_lds = -1;   // GI_X_LDS=0 disables the LDS-resident scene (tuning)
+        if (env_lds == -1) {
+            const char* v = std::getenv("GI_X_LDS");
+            env_lds = v ? std::atoi(v) : 1;
+        }
+        const bool lds = env_lds != 0 && sc.x_lds_bytes > 0;
+        const size_t lds_bytes = lds ? (size_t)sc.x_lds_bytes : 0;
+        static int resident_blocks[2] = {0, 0};
+        static size_t resident_lds = 0;
+        if (resident_blocks[lds] == 0 || (lds && resident_lds != lds_bytes)) {
             int dev = 0, cus = 0, per_cu = 0;
             (void)hipGetDevice(&dev);
             (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k_mode_x<false>),
-                                                              64 * kWavesPerBlock, 0);
-            resident_blocks = std::max(1, cus) * std::max(1, per_cu);
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &per_cu, lds ? reinterpret_cast<const void*>(k_mode_x<false, true>) : reinterpret_cast<const void*>(k_mode_x<false, false>),
+                64 * kWavesPerBlock, lds_bytes);
+            resident_blocks[lds] = std::max(1, cus) * std::max(1, per_cu);
+            if (lds) resident_lds = lds_bytes;
         }
+        const int resident = resident_blocks[lds];
         const long long want = (m.n_local + kWavesPerBlock - 1) / kWavesPerBlock;
-        const dim3 pgrid((unsigned)std::min<long long>(want, resident_blocks));
+        const dim3 pgrid((unsigned)std::min<long long>(want, resident));
         hipError_t e = hipMemsetAsync(sc.work, 0, 16 * sizeof(unsigned), stream);
         if (e != hipSuccess) return e;
         // shading-handler threshold (eighths of the live lanes that must wait): the builder's
@@ -951,10 +1017,14 @@ hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w,
             env_xf = v ? std::atoi(v) : -1;
         }
         const int xf = env_xf >= 0 ? env_xf : sc.x_flags;
-        if (stats)
-            hipLaunchKernelGGL(k_mode_x<true>, pgrid, block, 0, stream, sc, cam, light, m, o.spp, o.depth, o.seed, rgb, rgb8, st, sc.work, h8, xf);
-        else
-            hipLaunchKernelGGL(k_mode_x<false>, pgrid, block, 0, stream, sc, cam, light, m, o.spp, o.depth, o.seed, rgb, rgb8, st, sc.work, h8, xf);
+#define GI_LAUNCH_X(S, L) hipLaunchKernelGGL((k_mode_x<S, L>), pgrid, block, lds_bytes, stream, sc, cam, light, m, o.spp, \
+                                           o.depth, o.seed, rgb, rgb8, st, sc.work, h8, xf)
+        if (stats) {
+            if (lds) GI_LAUNCH_X(true, true); else GI_LAUNCH_X(true, false);
+        } else {
+            if (lds) GI_LAUNCH_X(false, true); else GI_LAUNCH_X(false, false);
+        }
+#undef GI_LAUNCH_X
     }
     return hipGetLastError();
 }

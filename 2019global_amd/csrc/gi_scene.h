@@ -71,7 +71,8 @@ struct XWNode {            // 256 bytes, 2 cache lines
     int32_t child[8];      // >= 0: wide node; < 0 (not XEMPTY): leaf = ~(offset into xhot[]); XEMPTY: none
     int32_t parent;        // wide node of the parent cell, -1 at the root (stackless traversal)
     uint16_t cnt[8];       // leaf children: number of xhot records
-    int32_t pad[3];
+    int32_t exists;        // bit c set iff child[c] != XEMPTY (branch-free culling)
+    int32_t pad[2];
 };
 static_assert(sizeof(XWNode) == 256, "XWNode layout");
 // Leaf primitive records, duplicated per leaf reference and stored contiguously per leaf, so a
@@ -114,6 +115,15 @@ struct HostScene {
     double x_est_nodes = 0, x_est_prims = 0;   // SAH estimates per random ray through the root
 };
 
+// Sets XWNode::exists from the child references (both Mode X builders call it last).
+inline void finalize_xwnodes(std::vector<XWNode>& w) {
+    for (XWNode& n : w) {
+        n.exists = 0;
+        for (int c = 0; c < 8; ++c)
+            if (n.child[c] != XEMPTY) n.exists |= 1 << c;
+    }
+}
+
 // Mode X 8-wide BVH over the primitives (gi_bvh.cpp); bounds: 6 doubles (min xyz, max xyz) each.
 void build_xbvh(const std::vector<XPrim>& prims, const std::vector<double>& bounds, int leaf_max, HostScene& hs);
 
@@ -132,6 +142,8 @@ struct DevScene {
     int32_t x_max_depth;
     int32_t x_handle8;     // Mode X shading-handler threshold, eighths of the live lanes (set at upload)
     int32_t x_flags;       // Mode X schedule flags: bit 0 = continue paths from shadow rays in traversal
+    int32_t n_xhot;
+    int32_t x_lds_bytes;   // > 0: xwnodes + xhot fit in LDS and are staged there by each workgroup
     float root_lo[3], root_hi[3];   // Mode X: union of the root's fp32 child boxes (conservative)
 };
 
