@@ -712,13 +712,8 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                         const V3 Tn = vmul(T, tc * 0.5);
                         T = Tn;
                         if (!(Tn.x == 0.0 && Tn.y == 0.0 && Tn.z == 0.0)) {
-                            double sx = 0, sy = 0, r2 = 0;
-                            for (int k = 0; k < 16; ++k) {
-                                const double ax = 2.0 * mx_u01k(key, smp, b, 2 + 2 * k) - 1.0;
-                                const double ay = 2.0 * mx_u01k(key, smp, b, 3 + 2 * k) - 1.0;
-                                const double q = ax * ax + ay * ay;
-                                if (q < 1.0) { sx = ax; sy = ay; r2 = q; break; }
-                            }
+                            double sx, sy, r2;   // cosine-weighted: concentric disk + Malley
+                            mx_disk(mx_u01k(key, smp, b, 2), mx_u01k(key, smp, b, 3), sx, sy, r2);
                             const double sz = gsqrt(1.0 - r2);
                             const double sg = N.z >= 0.0 ? 1.0 : -1.0;
                             const double aa = -1.0 / (sg + N.z);

@@ -233,6 +233,42 @@ GI_HD double mx_powi(double x, int p) {
 
 // Texture (material.h:65-106): 32x32 int checker, colour truncated to int (A.7); a negative
 // index (out-of-bounds UB in the reference, A.9) wraps into [0,32).
+// Mode X: point on the unit disk from (u1, u2) in [0,1)^2 by the concentric map (Shirley & Chiu
+// 1997), loop-free; sin/cos on [-pi/4, pi/4] as degree-17/16 Taylor polynomials in Horner form
+// (only +, -, * on fp64: bit-identical on the host and gfx950).  r2 = radius^2.
+GI_HD void mx_sincos_q(double p, double& sn, double& cs) {
+    const double S[8] = {-0x1.5555555555555p-3, 0x1.1111111111111p-7, -0x1.a01a01a01a01ap-13, 0x1.71de3a556c734p-19,
+    -0x1.ae64567f544e4p-26, 0x1.6124613a86d09p-33, -0x1.ae7f3e733b81fp-41, 0x1.952c77030ad4ap-49};
+    const double C[8] = {-0x1.0000000000000p-1, 0x1.5555555555555p-5, -0x1.6c16c16c16c17p-10, 0x1.a01a01a01a01ap-16,
+    -0x1.27e4fb7789f5cp-22, 0x1.1eed8eff8d898p-29, -0x1.93974a8c07c9dp-37, 0x1.ae7f3e733b81fp-45};
+    const double z = p * p;
+    double ps = S[7], pc = C[7];
+    for (int k = 6; k >= 0; --k) {
+        ps = ps * z + S[k];
+        pc = pc * z + C[k];
+    }
+    sn = p + p * (z * ps);
+    cs = 1.0 + z * pc;
+}
+GI_HD void mx_disk(double u1, double u2, double& dx, double& dy, double& r2) {
+    const double a = 2.0 * u1 - 1.0, b = 2.0 * u2 - 1.0;
+    const double QPI = 0x1.921fb54442d18p-1;   // pi/4
+    if (a == 0.0 && b == 0.0) { dx = 0.0; dy = 0.0; r2 = 0.0; return; }
+    double r, sn, cs;
+    if ((a < 0 ? -a : a) > (b < 0 ? -b : b)) {
+        r = a;
+        mx_sincos_q(QPI * (b / a), sn, cs);
+        dx = r * cs;
+        dy = r * sn;
+    } else {
+        r = b;
+        mx_sincos_q(QPI * (a / b), sn, cs);
+        dx = r * sn;
+        dy = r * cs;
+    }
+    r2 = r * r;
+}
+
 GI_HD V3 texel(V3 color, int32_t u, int32_t v) {
     // pattern[u % 32][v % 32] with C remainders: the compiled reference reads the FLAT element
     // (u%32)*32 + v%32 of the 32x32 array; inside [0,1024) that is exact, outside it reads stack

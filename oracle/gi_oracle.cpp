@@ -764,6 +764,41 @@ inline double mx_u01(uint64_t seed, uint64_t pixel, uint32_t sample, uint32_t bo
     return (double)(k >> 11) * 0x1.0p-53;
 }
 
+// Shirley-Chiu concentric map of (u1,u2) to the unit disk; sin/cos on [-pi/4, pi/4] by Taylor
+// polynomials (degree 17 / 16, Horner), fp64 +,-,* only.
+void mx_sincos_q(double p, double& sn, double& cs) {
+    static const double S[8] = {-0x1.5555555555555p-3, 0x1.1111111111111p-7, -0x1.a01a01a01a01ap-13, 0x1.71de3a556c734p-19,
+    -0x1.ae64567f544e4p-26, 0x1.6124613a86d09p-33, -0x1.ae7f3e733b81fp-41, 0x1.952c77030ad4ap-49};
+    static const double C[8] = {-0x1.0000000000000p-1, 0x1.5555555555555p-5, -0x1.6c16c16c16c17p-10, 0x1.a01a01a01a01ap-16,
+    -0x1.27e4fb7789f5cp-22, 0x1.1eed8eff8d898p-29, -0x1.93974a8c07c9dp-37, 0x1.ae7f3e733b81fp-45};
+    const double z = p * p;
+    double ps = S[7], pc = C[7];
+    for (int k = 6; k >= 0; --k) {
+        ps = ps * z + S[k];
+        pc = pc * z + C[k];
+    }
+    sn = p + p * (z * ps);
+    cs = 1.0 + z * pc;
+}
+void mx_disk(double u1, double u2, double& dx, double& dy, double& r2) {
+    const double a = 2.0 * u1 - 1.0, b = 2.0 * u2 - 1.0;
+    const double QPI = 0x1.921fb54442d18p-1;
+    if (a == 0.0 && b == 0.0) { dx = dy = r2 = 0.0; return; }
+    double r, sn, cs;
+    if (std::fabs(a) > std::fabs(b)) {
+        r = a;
+        mx_sincos_q(QPI * (b / a), sn, cs);
+        dx = r * cs;
+        dy = r * sn;
+    } else {
+        r = b;
+        mx_sincos_q(QPI * (a / b), sn, cs);
+        dx = r * sn;
+        dy = r * cs;
+    }
+    r2 = r * r;
+}
+
 struct Prim {
     int kind;     // 0 = triangle, 1 = sphere
     int ent;
@@ -955,14 +990,9 @@ void pixel_mode_x(const Scene& s, const std::vector<Prim>& prims, const Cam& c, 
             if (b == depth - 1) break;
             T = mul(T, tc * 0.5);
             if (T.x == 0.0 && T.y == 0.0 && T.z == 0.0) break;
-            // cosine-weighted direction: disk rejection sampling (<= 16 tries) + Malley's projection
-            double sx = 0, sy = 0, r2 = 0;
-            for (int k = 0; k < 16; ++k) {
-                const double ax = 2.0 * mx_u01(seed, pix, smp, b, 2 + 2 * k) - 1.0;
-                const double ay = 2.0 * mx_u01(seed, pix, smp, b, 3 + 2 * k) - 1.0;
-                const double q = ax * ax + ay * ay;
-                if (q < 1.0) { sx = ax; sy = ay; r2 = q; break; }
-            }
+            // cosine-weighted direction: concentric disk point + Malley's projection
+            double sx, sy, r2;
+            mx_disk(mx_u01(seed, pix, smp, b, 2), mx_u01(seed, pix, smp, b, 3), sx, sy, r2);
             const double sz = std::sqrt(1.0 - r2);
             const double sg = N.z >= 0.0 ? 1.0 : -1.0;   // Duff et al. 2017 orthonormal basis
             const double aa = -1.0 / (sg + N.z);
