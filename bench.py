@@ -78,20 +78,32 @@ def pmc_traffic(workload: str):
     return best
 
 
-def cpu_baseline(scn_text, w, h, mode, spp, depth, seed):
-    """The oracle (this repo's CPU port) on a bounded window of the same frame."""
+def cpu_baseline(scn_text, w, h, mode, spp, depth, seed, target_s=20.0):
+    """The oracle (this repo's CPU port, OpenMP) on a bounded, centred window of the same frame:
+    a 256x96 probe sets the rate, then a window sized for about `target_s` seconds is timed."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_util as U
     threads = max(1, min(16, os.cpu_count() or 1))
-    if mode == 1:
-        cx, cy = w // 2, int(h * 0.8)
-        win = (max(0, cx - 128), max(0, cy - 48), min(w, cx + 128), min(h, cy + 48))
-    else:
-        win = (0, 0, w, h)
-    t = time.perf_counter()
-    o = U.oracle_render(scn_text, w, h, mode=mode, spp=spp, depth=depth, seed=seed, window=win, threads=threads)
-    dt = time.perf_counter() - t
-    rays = int(o["ncand"].sum()) if mode == 1 else (win[2] - win[0]) * (win[3] - win[1])
+
+    def window(ww, wh):
+        cx, cy = w // 2, (int(h * 0.8) if mode == 1 else h // 2)
+        x0, y0 = max(0, min(w - ww, cx - ww // 2)), max(0, min(h - wh, cy - wh // 2))
+        return (x0, y0, min(w, x0 + ww), min(h, y0 + wh))
+
+    def run(win):
+        t = time.perf_counter()
+        o = U.oracle_render(scn_text, w, h, mode=mode, spp=spp, depth=depth, seed=seed, window=win, threads=threads)
+        dt = time.perf_counter() - t
+        rays = int(o["ncand"].sum()) if mode == 1 else (win[2] - win[0]) * (win[3] - win[1])
+        return rays, dt
+
+    win = window(min(w, 256), min(h, 96))
+    rays, dt = run(win)
+    scale = target_s / max(dt, 1e-3)
+    if scale > 1.5:
+        f = min(scale ** 0.5, max(w / (win[2] - win[0]), h / (win[3] - win[1])))
+        win = window(min(w, int((win[2] - win[0]) * f)), min(h, int((win[3] - win[1]) * f)))
+        rays, dt = run(win)
     return {"value": round(rays / dt / 1e6, 4), "unit": "Mray/s", "cores": threads, "kind": "port",
             "sample": f"window x[{win[0]},{win[2]}) y[{win[1]},{win[3]}) of the same frame, {rays} rays, "
                       f"{dt:.2f} s wall, OpenMP"}
