@@ -374,9 +374,8 @@ __device__ __forceinline__ double x_prim_t(const XHot& p, V3 o, V3 d, double tmi
         const bool pos = det > 0.0;
         const bool miss = det == 0.0 || (pos ? (un < 0.0 || un > det || vn < 0.0 || uvn > det)
                                              : (un > 0.0 || un < det || vn > 0.0 || uvn < det));
-        if (miss) return INFINITY;
-        const double t = dot(e2, qv) / det;
-        return (t > tmin) ? t : INFINITY;
+        const double t = dot(e2, qv) / det;   // branch-free: two tests interleave in the leaf loop
+        return (!miss && t > tmin) ? t : INFINITY;
     }
     const V3 oc = o - ld3(p.a);
     const double b = dot(oc, d);
@@ -523,9 +522,6 @@ __device__ void x_texcoord(const DevScene& sc, const REnt& e, V3 ip, int32_t& x,
 // oracle/gi_oracle.cpp), so results are bit-identical whatever the schedule.
 enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD = 4, PH_DONEPX = 5 };
 
-#ifndef GI_X_PRIM_PREFILTER
-#define GI_X_PRIM_PREFILTER 0   // fp32 AABB cull before each fp64 primitive test (measured slower: +1 dependent load)
-#endif
 #ifndef GI_X_START_BURST
 #define GI_X_START_BURST 16   // primary rays a lane may resolve by the root test per handler run
 #endif
@@ -539,7 +535,7 @@ struct XCounters {
     uint64_t cyc_trav = 0, cyc_hit = 0, cyc_next = 0, cyc_all = 0;                    // wave clock cycles
 };
 
-template <bool STATS, typename NodeP, typename HotP>
+template <bool STATS, bool PAIR, typename NodeP, typename HotP>
 __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H, const CamDev& cam, V3 light,
                                             const TileMap& m, int spp, int depth, uint64_t seed, double* rgb,
                                             uint8_t* rgb8, unsigned* slot_counter, int handle8, int xflags,
@@ -613,23 +609,46 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     const XHot* hp = H + ~ch;
                     const XBox* bp = sc.xbox + ~ch;
                     const int cntl = nd->cnt[c];
-                    XHotR cur = load_hot(hp);   // records fetched one ahead of the test
-                    for (int j = 0; j < cntl; ++j) {
-                        const XHotR rec = cur;
-                        cur = load_hot(hp + min(j + 1, cntl - 1));
-#if GI_X_PRIM_PREFILTER
-                        ++nbox;
-                        if (!box32_hit(bp[j], of, ivf, tbest_f)) continue;   // conservative fp32 cull
-#endif
-                        ++nprim;
-                        const double t = x_prim_t(rec.h, o, d, MX_TMIN);
-                        const int pi = rec.h.prim;
+                    if constexpr (!PAIR) {   // global records: fetched one ahead of the test
+                        XHotR cur = load_hot(hp);
+                        for (int j = 0; j < cntl; ++j) {
+                            const XHotR rec = cur;
+                            cur = load_hot(hp + min(j + 1, cntl - 1));
+                            ++nprim;
+                            const double t = x_prim_t(rec.h, o, d, MX_TMIN);
+                            const int pi = rec.h.prim;
+                            if (phase == PH_SHADOW) {
+                                if (t < tmax) { best = pi; raying = false; break; }   // any hit occludes
+                            } else if (t < tbest || (t == tbest && pi < best)) {
+                                tbest = t;
+                                best = pi;
+                                tbest_f = up32(t);
+                            }
+                        }
+                    } else
+                    // LDS records: tested two at a time, the two fp64 dependency chains interleave
+                    for (int j = 0; j < cntl; j += 2) {
+                        const bool two = j + 1 < cntl;
+                        const XHotR r0 = load_hot(hp + j), r1 = load_hot(hp + (two ? j + 1 : j));
+                        const double t0 = x_prim_t(r0.h, o, d, MX_TMIN);
+                        const double t1 = two ? x_prim_t(r1.h, o, d, MX_TMIN) : INFINITY;
+                        nprim += two ? 2 : 1;
                         if (phase == PH_SHADOW) {
-                            if (t < tmax) { best = pi; raying = false; break; }   // any hit occludes
-                        } else if (t < tbest || (t == tbest && pi < best)) {
-                            tbest = t;
-                            best = pi;
-                            tbest_f = up32(t);
+                            if (t0 < tmax || t1 < tmax) {   // any hit occludes
+                                best = t0 < tmax ? r0.h.prim : r1.h.prim;
+                                raying = false;
+                                break;
+                            }
+                        } else {
+                            if (t0 < tbest || (t0 == tbest && r0.h.prim < best)) {
+                                tbest = t0;
+                                best = r0.h.prim;
+                            }
+                            if (t1 < tbest || (t1 == tbest && r1.h.prim < best)) {
+                                tbest = t1;
+                                best = r1.h.prim;
+                            }
+                            tbest_f = up32(tbest);
                         }
                     }
                     (void)bp;
@@ -872,10 +891,10 @@ __global__ __launch_bounds__(256, GI_X_MIN_WAVES) void k_mode_x(DevScene sc, Cam
         __syncthreads();
         const XWNode* W = reinterpret_cast<const XWNode*>(lds_scene);
         const XHot* H = reinterpret_cast<const XHot*>(lds_scene + nw);
-        mode_x_wave<STATS>(sc, W, H, cam, light, m, spp, depth, seed, rgb, rgb8, slot_counter, handle8, xflags, c);
+        mode_x_wave<STATS, true>(sc, W, H, cam, light, m, spp, depth, seed, rgb, rgb8, slot_counter, handle8, xflags, c);
     } else {
-        mode_x_wave<STATS>(sc, sc.xwnodes, sc.xhot, cam, light, m, spp, depth, seed, rgb, rgb8, slot_counter, handle8,
-                           xflags, c);
+        mode_x_wave<STATS, false>(sc, sc.xwnodes, sc.xhot, cam, light, m, spp, depth, seed, rgb, rgb8, slot_counter,
+                                  handle8, xflags, c);
     }
     if (STATS) {
         if ((threadIdx.x & 63) == 0) {
