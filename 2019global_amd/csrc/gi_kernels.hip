@@ -439,6 +439,34 @@ __device__ __forceinline__ bool root_hit(const DevScene& sc, F3 of, F3 ivf) {
     return tn <= tf;
 }
 
+// Conservative packet test: true only if no ray through pixel (x, y)'s jitter square (corners
+// (x, y) .. (x+1, y+1): every jittered primary direction is a convex combination of the corner
+// directions) can meet the box, i.e. the box lies strictly outside one side plane of the pixel's
+// ray frustum (fp64, with a relative margin far above rounding).
+__device__ __forceinline__ bool pixel_misses_box(const CamDev& cam, int x, int y, const float* lo, const float* hi) {
+    const double fx = (double)x, fy = (double)y;
+    // box as centre (relative to the camera) and half extents: max over its corners of n.(p - o)
+    // = n.(centre - o) + sum |n_k| h_k
+    const V3 bc = v3(0.5 * ((double)lo[0] + (double)hi[0]), 0.5 * ((double)lo[1] + (double)hi[1]),
+                     0.5 * ((double)lo[2] + (double)hi[2])) - cam.pos;
+    const V3 bh = v3(0.5 * ((double)hi[0] - (double)lo[0]), 0.5 * ((double)hi[1] - (double)lo[1]),
+                     0.5 * ((double)hi[2] - (double)lo[2]));
+    const double reach = fabs(bc.x) + fabs(bc.y) + fabs(bc.z) + bh.x + bh.y + bh.z;
+    const V3 cc = primary_dir(cam, fx + 0.5, fy + 0.5);
+    V3 a = primary_dir(cam, fx, fy);
+#pragma unroll 1
+    for (int i = 0; i < 4; ++i) {
+        const V3 bnext = primary_dir(cam, fx + ((i == 0 || i == 1) ? 1.0 : 0.0), fy + ((i == 1 || i == 2) ? 1.0 : 0.0));
+        V3 n = cross(a, bnext);
+        if (dot(n, cc) < 0) n = -n;   // inside = the pixel centre's side
+        const double mx = dot(n, bc) + (fabs(n.x) * bh.x + fabs(n.y) * bh.y + fabs(n.z) * bh.z);
+        const double nl = fabs(n.x) + fabs(n.y) + fabs(n.z);
+        if (mx < -1e-9 * nl * reach) return true;
+        a = bnext;
+    }
+    return false;
+}
+
 __device__ void x_texcoord(const DevScene& sc, const REnt& e, V3 ip, int32_t& x, int32_t& y) {
     if (e.kind == K_IMP_SPHERE) {
         const double r = e.radius;
@@ -526,7 +554,7 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 #define GI_X_START_BURST 16   // primary rays a lane may resolve by the root test per handler run
 #endif
 #ifndef GI_X_MIN_WAVES
-#define GI_X_MIN_WAVES 1   // minimum waves per SIMD for k_mode_x (register budget knob)
+#define GI_X_MIN_WAVES 3   // minimum waves per SIMD for k_mode_x (register budget: <= 168 VGPRs)
 #endif
 
 struct XCounters {
@@ -798,10 +826,19 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                             phase = PH_DEAD;
                         } else if (slot_pixel(m, (long long)(sl >> 6), (int)(sl & 63), idx, x, y)) {
                             y += m.y0;
-                            key = mx_key(seed, (uint64_t)y * (uint64_t)m.w + (uint64_t)x);
-                            smp = 0;
-                            s0 = s1 = s2 = 0;
-                            phase = PH_START;
+                            if (spp > 1 && pixel_misses_box(cam, x, y, sc.root_lo, sc.root_hi)) {
+                                // every jittered primary ray of this pixel misses the scene: all
+                                // spp samples add exactly +0, the pixel is 0 (rays resolved as a packet)
+                                if (rgb) { rgb[3 * idx] = 0; rgb[3 * idx + 1] = 0; rgb[3 * idx + 2] = 0; }
+                                if (rgb8) { rgb8[3 * idx] = 0; rgb8[3 * idx + 1] = 0; rgb8[3 * idx + 2] = 0; }
+                                nrays += spp;
+                                ++npx;
+                            } else {
+                                key = mx_key(seed, (uint64_t)y * (uint64_t)m.w + (uint64_t)x);
+                                smp = 0;
+                                s0 = s1 = s2 = 0;
+                                phase = PH_START;
+                            }
                         } else if (idx >= 0 && m.shard_count > 1) {   // padding slot of a packed tile
                             if (rgb) { rgb[3 * idx] = 0; rgb[3 * idx + 1] = 0; rgb[3 * idx + 2] = 0; }
                             if (rgb8) { rgb8[3 * idx] = 0; rgb8[3 * idx + 1] = 0; rgb8[3 * idx + 2] = 0; }
