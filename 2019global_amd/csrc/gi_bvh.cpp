@@ -15,6 +15,7 @@
 // primitive tests alone decide hits (bit-exact with the oracle's brute force).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <vector>
@@ -54,7 +55,7 @@ struct Builder {
     std::vector<BNode> nodes;
     int leaf_max = 4;
     static constexpr int kBins = 32;
-    static constexpr double kTraverse = 1.0;   // SAH cost of a node visit relative to one primitive test
+    double kTraverse = 1.0;   // SAH cost of a node visit relative to one primitive test
 
     int build(int first, int count, int depth) {
         const int ni = (int)nodes.size();
@@ -182,6 +183,7 @@ void build_xbvh(const std::vector<XPrim>& prims, const std::vector<double>& boun
     Builder b;
     b.pb = &pb;
     b.leaf_max = std::max(1, leaf_max);
+    if (const char* ct = std::getenv("GI_XSAH_CT")) b.kTraverse = std::atof(ct);   // tuning knob
     b.order.resize(np);
     b.cen.resize(3 * np);
     for (size_t i = 0; i < np; ++i) {

@@ -311,3 +311,59 @@ def test_cpp_dropin_raytracer_matches_reference_run(torch_cuda, tmp_path):
     got = np.frombuffer(out.read_bytes(), np.uint8).reshape(160, 160, 3)
     z = np.load(os.path.join(GOLD, "zoo_160x160.npz"))
     assert (got == z["run_q"]).all()
+
+
+@pytest.mark.parametrize("scene,w,h,spp,depth", [("cornell", 37, 29, 3, 5), ("zoo", 45, 19, 2, 4),
+                                                  ("main", 13, 61, 1, 3)])
+def test_mode_x_ragged_frames_bit_exact(torch_cuda, scene, w, h, spp, depth):
+    """Frame sizes that are not multiples of the 8x8 tile: partial tiles, padding slots."""
+    sc = _scene(scene)
+    o = U.oracle_render(sc.to_scn(), w, h, mode=1, spp=spp, depth=depth, seed=77)
+    rgb, rgb8 = dev_scene(scene).render(cam_of(sc), sc.light, w, h, mode=gi.MODE_X, spp=spp, depth=depth, seed=77)
+    assert U.bits_equal(rgb.reshape(-1, 3), o["rgb"]).all()
+    assert (rgb8.reshape(-1, 3) == o["q"]).all()
+
+
+def test_mode_x_ray_count_equals_oracle(torch_cuda):
+    """The bench's rays/frame (GI_FLAG_STATS) is the frame's ray count as the oracle traces it ray by
+    ray -- including primary rays the device resolves by its root-box and pixel-frustum tests."""
+    torch = torch_cuda
+    sc = S.cornell_scene()
+    w, h, spp, depth = 96, 64, 4, 6
+    o = U.oracle_render(sc.to_scn(), w, h, mode=1, spp=spp, depth=depth, seed=5)
+    st = torch.zeros(gi.STATS_N, dtype=torch.int64, device="cuda")
+    buf = torch.zeros(w * h * 3, dtype=torch.float64, device="cuda")
+    dev_scene("cornell").render_device(cam_of(sc), sc.light, w, h, buf.data_ptr(), stats_ptr=st.data_ptr(),
+                                       mode=gi.MODE_X, spp=spp, depth=depth, seed=5)
+    torch.cuda.synchronize()
+    s = st.cpu().numpy()
+    assert int(s[gi.STAT_RAYS]) == int(o["ncand"].sum())
+    assert int(s[gi.STAT_PIXELS]) == w * h
+    assert U.bits_equal(buf.cpu().numpy().reshape(-1, 3), o["rgb"]).all()
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_empty_scene_and_single_pixel(torch_cuda, mode):
+    s = S.Scene(entities=[])
+    d = gi.DeviceScene.from_scene(s)
+    for w, h in ((1, 1), (9, 3)):
+        rgb, rgb8 = d.render(cam_of(s), s.light, w, h, mode=mode, spp=2 if mode else 1, depth=3)
+        assert (rgb == 0).all() and (rgb8 == 0).all()
+
+
+def test_degenerate_triangles_match_oracle(torch_cuda):
+    """Zero-area (collinear and repeated-vertex) triangles among ordinary ones, both modes."""
+    s = S.Scene(entities=[])
+    s.imp_triangle((2.0, -1.0, -1.0), (2.0, 1.0, 1.0), (2.0, 3.0, 3.0), (1, 0, 0))    # collinear
+    s.imp_triangle((3.0, 0.5, 0.5), (3.0, 0.5, 0.5), (3.0, -2.0, 1.0), (0, 1, 0))     # repeated vertex
+    s.imp_triangle((4.0, -3.0, -3.0), (4.0, 3.0, -3.0), (4.0, 0.0, 3.0), (1, 1, 0))
+    s.imp_sphere((6.0, 1.0, 1.0), 1.5, (0, 0, 1))
+    d = gi.DeviceScene.from_scene(s)
+    w, h = 40, 24
+    o = U.oracle_render(s.to_scn(), w, h)
+    rgb, rgb8 = d.render(cam_of(s), s.light, w, h)
+    assert_rel(rgb.reshape(-1, 3), o["rgb"], "mode R degenerate")
+    assert (rgb8.reshape(-1, 3) == o["q"]).all()
+    ox = U.oracle_render(s.to_scn(), w, h, mode=1, spp=2, depth=4, seed=9)
+    rgb, _ = d.render(cam_of(s), s.light, w, h, mode=gi.MODE_X, spp=2, depth=4, seed=9)
+    assert U.bits_equal(rgb.reshape(-1, 3), ox["rgb"]).all()
