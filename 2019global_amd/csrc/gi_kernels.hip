@@ -364,24 +364,24 @@ __device__ __forceinline__ XHotR load_hot(const XHot* p) {
 __device__ __forceinline__ double x_prim_t(const XHot& p, V3 o, V3 d, double tmin) {
     if (p.kind == 0) {
         const V3 e1 = ld3(p.b), e2 = ld3(p.c), v0 = ld3(p.a);
-        const V3 pv = cross(d, e2);
-        const double det = dot(e1, pv);
+        const V3 pv = fcross(d, e2);
+        const double det = fdot(e1, pv);
         const V3 tv = o - v0;
-        const double un = dot(tv, pv);
-        const V3 qv = cross(tv, e1);
-        const double vn = dot(d, qv);
+        const double un = fdot(tv, pv);
+        const V3 qv = fcross(tv, e1);
+        const double vn = fdot(d, qv);
         const double uvn = un + vn;
         const bool pos = det > 0.0;
         const bool miss = det == 0.0 || (pos ? (un < 0.0 || un > det || vn < 0.0 || uvn > det)
                                              : (un > 0.0 || un < det || vn > 0.0 || uvn < det));
-        const double t = dot(e2, qv) / det;   // branch-free: two tests interleave in the leaf loop
+        const double t = fdot(e2, qv) / det;   // branch-free: two tests interleave in the leaf loop
         return (!miss && t > tmin) ? t : INFINITY;
     }
     const V3 oc = o - ld3(p.a);
-    const double b = dot(oc, d);
+    const double b = fdot(oc, d);
     const double r = p.b[0];
-    const double c2 = dot(oc, oc) - r * r;
-    const double disc = b * b - c2;
+    const double c2 = gfma(-r, r, fdot(oc, oc));
+    const double disc = gfma(b, b, -c2);
     if (disc < 0.0) return INFINITY;
     const double sq = gsqrt(disc);
     double t = -b - sq;

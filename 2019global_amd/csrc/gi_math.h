@@ -36,6 +36,20 @@ GI_HD double gsqrt(double x) {
 #endif
 }
 GI_HD V3 normalize(V3 v) { return v * (1.0 / gsqrt(dot(v, v))); }
+// Mode X only (build-defined, not the reference's arithmetic): fused multiply-add, correctly
+// rounded on both sides (v_fma_f64 / std::fma), so the oracle restates it exactly.
+GI_HD double gfma(double a, double b, double c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_fma(a, b, c);
+#else
+    return std::fma(a, b, c);
+#endif
+}
+GI_HD double fdot(V3 a, V3 b) { return gfma(a.z, b.z, gfma(a.y, b.y, a.x * b.x)); }
+GI_HD V3 fcross(V3 x, V3 y) {
+    return v3(gfma(x.y, y.z, -(y.y * x.z)), gfma(x.z, y.x, -(y.z * x.x)), gfma(x.x, y.y, -(y.x * x.y)));
+}
+
 GI_HD double length(V3 v) { return gsqrt(dot(v, v)); }
 // pow(v.x,2)+pow(v.y,2)+pow(v.z,2) as the reference writes it (g++ folds pow(x,2) to x*x)
 GI_HD double sq3(V3 v) { return v.x * v.x + v.y * v.y + v.z * v.z; }

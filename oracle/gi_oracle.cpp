@@ -827,25 +827,31 @@ void build_prims(const Scene& s, std::vector<Prim>& prims) {
 // Möller–Trumbore, two-sided, with the barycentric tests on the numerators (u = un/det in [0,1],
 // v = vn/det >= 0, u + v <= 1 compared as un, vn, un+vn against 0 and det, by the sign of det);
 // t = tn/det is the only division.  Returns t or +inf.
+// Mode X arithmetic with fused multiply-adds (std::fma: correctly rounded, as the device's
+// v_fma_f64): dot = fma(z, z', fma(y, y', x*x')), cross components fma(a, b, -(c*d)).
+inline double fdot(V3 a, V3 b) { return std::fma(a.z, b.z, std::fma(a.y, b.y, a.x * b.x)); }
+inline V3 fcross(V3 x, V3 y) {
+    return {std::fma(x.y, y.z, -(y.y * x.z)), std::fma(x.z, y.x, -(y.z * x.x)), std::fma(x.x, y.y, -(y.x * x.y))};
+}
 double mx_tri_t(const Prim& p, V3 o, V3 d, double tmin) {
-    const V3 pv = cross(d, p.e2);
-    const double det = dot(p.e1, pv);
+    const V3 pv = fcross(d, p.e2);
+    const double det = fdot(p.e1, pv);
     if (det == 0.0) return INFINITY;
     const V3 tv = o - p.v0;
-    const double un = dot(tv, pv);
+    const double un = fdot(tv, pv);
     if (det > 0.0 ? (un < 0.0 || un > det) : (un > 0.0 || un < det)) return INFINITY;
-    const V3 qv = cross(tv, p.e1);
-    const double vn = dot(d, qv);
+    const V3 qv = fcross(tv, p.e1);
+    const double vn = fdot(d, qv);
     const double uvn = un + vn;
     if (det > 0.0 ? (vn < 0.0 || uvn > det) : (vn > 0.0 || uvn < det)) return INFINITY;
-    const double t = dot(p.e2, qv) / det;
+    const double t = fdot(p.e2, qv) / det;
     return (t > tmin) ? t : INFINITY;
 }
 double mx_sph_t(const Prim& p, V3 o, V3 d, double tmin) {
     const V3 oc = o - p.c;
-    const double b = dot(oc, d);
-    const double c2 = dot(oc, oc) - p.r * p.r;
-    const double disc = b * b - c2;
+    const double b = fdot(oc, d);
+    const double c2 = std::fma(-p.r, p.r, fdot(oc, oc));
+    const double disc = std::fma(b, b, -c2);
     if (disc < 0.0) return INFINITY;
     const double sq = std::sqrt(disc);
     double t = -b - sq;

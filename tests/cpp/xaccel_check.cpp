@@ -39,24 +39,24 @@ static double urand() {
 static double prim_t(const XHot& p, V3 o, V3 d, double tmin) {   // the kernel's x_prim_t
     if (p.kind == 0) {
         const V3 e1 = ld3(p.b), e2 = ld3(p.c);
-        const V3 pv = cross(d, e2);
-        const double det = dot(e1, pv);
+        const V3 pv = fcross(d, e2);
+        const double det = fdot(e1, pv);
         if (det == 0.0) return INFINITY;
         const V3 tv = o - ld3(p.a);
-        const double un = dot(tv, pv);
+        const double un = fdot(tv, pv);
         if (det > 0.0 ? (un < 0.0 || un > det) : (un > 0.0 || un < det)) return INFINITY;
-        const V3 qv = cross(tv, e1);
-        const double vn = dot(d, qv);
+        const V3 qv = fcross(tv, e1);
+        const double vn = fdot(d, qv);
         const double uvn = un + vn;
         if (det > 0.0 ? (vn < 0.0 || uvn > det) : (vn > 0.0 || uvn < det)) return INFINITY;
-        const double t = dot(e2, qv) / det;
+        const double t = fdot(e2, qv) / det;
         return (t > tmin) ? t : INFINITY;
     }
     const V3 oc = o - ld3(p.a);
-    const double b = dot(oc, d);
+    const double b = fdot(oc, d);
     const double r = p.b[0];
-    const double c2 = dot(oc, oc) - r * r;
-    const double disc = b * b - c2;
+    const double c2 = gfma(-r, r, fdot(oc, oc));
+    const double disc = gfma(b, b, -c2);
     if (disc < 0.0) return INFINITY;
     const double sq = std::sqrt(disc);
     double t = -b - sq;
