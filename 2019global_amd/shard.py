@@ -73,5 +73,17 @@ class FrameGather:
             self.packed_all = self.packed_all8 = self.parts = self.parts8 = None
 
     def gather(self) -> None:
+        if self.dist.get_backend() == "gloo" and self.buf.is_cuda:
+            # gloo gathers host tensors only (rehearsal path: several ranks sharing one device)
+            parts = [p.cpu() for p in self.parts] if self.rank == 0 else None
+            parts8 = [p.cpu() for p in self.parts8] if self.rank == 0 else None
+            self.dist.gather(self.buf.cpu(), parts, dst=0)
+            self.dist.gather(self.buf8.cpu(), parts8, dst=0)
+            if self.rank == 0:
+                for d, s in zip(self.parts, parts):
+                    d.copy_(s)
+                for d, s in zip(self.parts8, parts8):
+                    d.copy_(s)
+            return
         self.dist.gather(self.buf, self.parts, dst=0)
         self.dist.gather(self.buf8, self.parts8, dst=0)

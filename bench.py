@@ -138,6 +138,8 @@ def main():
     ap.add_argument("--workload", default="C3", choices=sorted(WORKLOADS))
     ap.add_argument("--seed", type=int, default=2019)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL over xGMI) for real runs; gloo rehearses N ranks sharing one GPU")
     args = ap.parse_args()
 
     import torch
@@ -150,9 +152,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
+    ndev = max(1, torch.cuda.device_count())
+    dev_index = local % ndev   # one GPU per rank; ranks share a device only in a gloo rehearsal
+    torch.cuda.set_device(dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group("gloo")
 
     scene_name, w, h, mode, spp, depth, desc = WORKLOADS[args.workload]
     sc = make_scene(scene_name)
@@ -178,7 +185,12 @@ def main():
     dev.render_device(cam, sc.light, w, h, buf.data_ptr(), buf8.data_ptr(), sptr, stats_ptr=stats.data_ptr(), **kw)
     torch.cuda.synchronize()
     if world > 1:
-        dist.all_reduce(stats)
+        if args.dist_backend == "gloo":
+            cs = stats.cpu()
+            dist.all_reduce(cs)
+            stats.copy_(cs)
+        else:
+            dist.all_reduce(stats)
     st = stats.cpu().tolist()
     rays_frame = st[gi.STAT_RAYS]
 
@@ -213,9 +225,19 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in zip(ev0, ev1)) / max(1, args.steps)
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = t.tolist()
+
+    frame_check = None
+    if world > 1 and rank == 0:   # the assembled frame against a whole frame rendered here alone
+        ref = torch.empty(w * h * 3, dtype=torch.float64, device="cuda")
+        ref8 = torch.empty(w * h * 3, dtype=torch.uint8, device="cuda")
+        dev.render_device(cam, sc.light, w, h, ref.data_ptr(), ref8.data_ptr(), sptr,
+                          **dict(kw, shard_count=1, shard_index=0))
+        torch.cuda.synchronize()
+        same = bool(torch.equal(ref.view(torch.int64), frame.view(torch.int64)) and torch.equal(ref8, frame8))
+        frame_check = "bit-identical to the single-GPU frame" if same else "MISMATCH vs single-GPU frame"
 
     if rank == 0:
         ms_frame = elapsed / args.steps * 1e3
@@ -249,6 +271,10 @@ def main():
                          "node_visits": st[gi.STAT_NODES], "prim_tests": st[gi.STAT_PRIMS],
                          "prim_box_tests": st[gi.STAT_PBOX]},
         }
+        if frame_check is not None:
+            out["frame_check"] = frame_check
+            if args.dist_backend != "nccl":
+                out["rehearsal"] = f"{args.dist_backend}: {world} ranks on {ndev} device(s)"
         if mode == 1 and st[gi.STAT_X_ITERS]:   # k_mode_x schedule (STATS launch; wave = 64 lanes)
             it, hd = st[gi.STAT_X_ITERS], max(1, st[gi.STAT_X_HANDLE])
             out["schedule"] = {"wave_iterations": it, "lane_trav_steps": st[gi.STAT_X_TRAV],
