@@ -19,8 +19,9 @@ struct CamDev {
 };
 bool build_host_scene(const gi_scene_desc& desc, HostScene& hs, std::string& err);
 long long shard_tiles(int w, int h, int shard_count);
+int x_spp_chunk();   // samples per work unit of the kernels (GI_SPP_CHUNK)
 hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w, int h, int y0, const gi_opts& o,
-                         double* rgb, uint8_t* rgb8, hipStream_t stream);
+                         double* rgb, uint8_t* rgb8, const XScratch& xs, hipStream_t stream);
 hipError_t launch_unshard(int w, int h, int shard_count, const double* packed, const uint8_t* packed8, double* rgb,
                           uint8_t* rgb8, hipStream_t stream);
 hipError_t launch_trace_ray(const DevScene& sc, V3 o, V3 d, V3 light, int32_t* out_i, double* out_d, hipStream_t stream);
@@ -33,6 +34,7 @@ struct gi_scene {
     HostScene host;
     DevScene dev;
     std::vector<void*> allocs;
+    XScratch xs;   // Mode X work list + chunk sums, grown on demand (one render in flight per scene)
     int device = -1;
     int64_t bytes = 0;
     bool mode_x_ok = true;
@@ -89,6 +91,34 @@ int check_opts(const gi_scene* s, int w, int h, const gi_opts* o) {
         if (!s->mode_x_ok) return fail(GI_ERR_SCENE, "mode X needs integer specular_power in [0, 64]");
     }
     if ((o->flags & GI_FLAG_STATS) && !o->stats) return fail(GI_ERR_ARG, "GI_FLAG_STATS without stats buffer");
+    return GI_OK;
+}
+
+// Mode X work buffers for a frame of w x h pixels cut into this call's shard (k_x_classify's list,
+// k_mode_x's chunk sums); grown, never shrunk.  hipFree synchronises with work still using them.
+int ensure_xscratch(gi_scene* s, int w, int h, const gi_opts* o) {
+    if (o->mode != GI_MODE_X) return GI_OK;
+    const long long need = shard_tiles(w, h, o->shard_count) * GI_TILE * GI_TILE;
+    const int chunks = (o->spp + x_spp_chunk() - 1) / x_spp_chunk();
+    if ((unsigned long long)need * (unsigned long long)chunks >= 0xFFFFFFFFull)
+        return fail(GI_ERR_ARG, "mode X frame too large: slots x spp chunks must stay below 2^32");
+    XScratch& x = s->xs;
+    hipError_t e;
+    if (x.cap < need) {
+        (void)hipFree(x.list);
+        (void)hipFree(x.part);
+        x = XScratch();
+        if ((e = hipMalloc((void**)&x.list, (size_t)need * sizeof(unsigned))) != hipSuccess) return hip_fail(e, "hipMalloc (work list)");
+        x.cap = need;
+    }
+    if (chunks > 1 && x.chunks < chunks) {
+        (void)hipFree(x.part);
+        x.part = nullptr;
+        x.chunks = 0;
+        if ((e = hipMalloc((void**)&x.part, (size_t)chunks * (size_t)x.cap * 3 * sizeof(double))) != hipSuccess)
+            return hip_fail(e, "hipMalloc (chunk sums)");
+        x.chunks = chunks;
+    }
     return GI_OK;
 }
 
@@ -184,6 +214,8 @@ int gi_scene_create(const gi_scene_desc* desc, gi_scene** out) {
 void gi_scene_destroy(gi_scene* s) {
     if (!s) return;
     for (void* p : s->allocs) (void)hipFree(p);
+    (void)hipFree(s->xs.list);
+    (void)hipFree(s->xs.part);
     delete s;
 }
 
@@ -211,9 +243,9 @@ int gi_render_device(gi_scene* s, const gi_camera* cam, const double light[3], i
     int rc = check_opts(s, w, h, o);
     if (rc) return rc;
     if (!cam || !light) return fail(GI_ERR_ARG, "null camera or light");
-    if ((rc = bind_device(s))) return rc;
+    if ((rc = bind_device(s)) || (rc = ensure_xscratch(s, w, h, o))) return rc;
     const hipError_t e = launch_render(s->dev, make_cam(*cam, w), v3(light[0], light[1], light[2]), w, h, 0, *o, d_rgb,
-                                       d_rgb8, static_cast<hipStream_t>(stream));
+                                       d_rgb8, s->xs, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return hip_fail(e, "render launch");
     return GI_OK;
 }
@@ -231,6 +263,7 @@ int gi_render(gi_scene* s, const gi_camera* cam, const double light[3], int w, i
     band = ((band + GI_TILE - 1) / GI_TILE) * GI_TILE;
     band = std::min(band, ((h + GI_TILE - 1) / GI_TILE) * GI_TILE);
     const size_t band_px = (size_t)w * (size_t)band;
+    if ((rc = ensure_xscratch(s, w, band, o))) return rc;
     double* d_rgb = nullptr;
     uint8_t* d_rgb8 = nullptr;
     hipError_t e;
@@ -247,7 +280,7 @@ int gi_render(gi_scene* s, const gi_camera* cam, const double light[3], int w, i
     for (int y0 = 0; y0 < h; y0 += band) {
         if (cancel && *cancel) { rc = fail(GI_ERR_CANCELLED, "cancelled"); break; }
         const int rows = std::min(band, h - y0);
-        e = launch_render(s->dev, cd, L, w, rows, y0, *o, d_rgb, d_rgb8, nullptr);
+        e = launch_render(s->dev, cd, L, w, rows, y0, *o, d_rgb, d_rgb8, s->xs, nullptr);
         if (e == hipSuccess) e = hipDeviceSynchronize();
         if (e != hipSuccess) { rc = hip_fail(e, "render"); break; }
         double* hr = rgb ? rgb + (size_t)y0 * w * 3 : scratch.data();

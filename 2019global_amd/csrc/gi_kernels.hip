@@ -563,13 +563,37 @@ struct XCounters {
     uint64_t cyc_trav = 0, cyc_hit = 0, cyc_next = 0, cyc_all = 0;                    // wave clock cycles
 };
 
+// Mode X work list (k_x_classify -> k_mode_x -> k_x_reduce).  A pixel whose every jittered primary
+// ray misses the scene's root box is resolved by the classifier (all samples add exactly +0); the
+// others are appended to `list` (their slot numbers in tile order).  k_mode_x's unit of work is one
+// (listed pixel, chunk of GI_SPP_CHUNK consecutive samples): units are numbered so that the 64
+// consecutive units of a wave are 64 listed pixels of one chunk.  With one chunk per pixel
+// (spp <= GI_SPP_CHUNK) the unit writes the pixel; otherwise it writes its chunk sum to
+// part[c][n_cap][3] and k_x_reduce adds the chunk sums in chunk order.  Splitting a pixel's samples
+// over lanes keeps every lane busy until the end of the frame (a whole 64-spp pixel per unit left
+// the kernel waiting on the last lanes' pixels: rendering 1/8 of the C3 frame took 75% of the time
+// of the whole frame).
+#ifndef GI_X_SPP_CHUNK
+#define GI_X_SPP_CHUNK GI_SPP_CHUNK   // the spec's chunk (include/gi.h); other values: A/B variants only
+#endif
+
+struct XWork {
+    const unsigned* list;    // listed pixel slots (tile order)
+    const unsigned* n_list;  // device count written by k_x_classify
+    double* part;            // chunk sums (chunks > 1)
+    unsigned n_cap;          // list capacity = part stride per chunk
+    int chunks;              // ceil(spp / GI_SPP_CHUNK)
+};
+
 template <bool STATS, bool PAIR, typename NodeP, typename HotP>
 __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H, const CamDev& cam, V3 light,
                                             const TileMap& m, int spp, int depth, uint64_t seed, double* rgb,
-                                            uint8_t* rgb8, unsigned* slot_counter, int handle8, int xflags,
-                                            XCounters& cnt) {
+                                            uint8_t* rgb8, unsigned* slot_counter, const XWork& wk, int handle8,
+                                            int xflags, XCounters& cnt) {
     const int lane = threadIdx.x & 63;
-    const unsigned n_slots = (unsigned)(m.n_local * (kTile * kTile));
+    const unsigned n_list = *wk.n_list;
+    const unsigned unit_group = 64u * (unsigned)wk.chunks;
+    const unsigned n_units = ((n_list + 63u) >> 6) * unit_group;
     const bool inline_shadow = (xflags & 1) != 0;
     uint32_t nnode = 0, nprim = 0, nrays = 0, nbox = 0, npx = 0;
     long long idx = -1;
@@ -796,7 +820,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             if (end_path) {
                 s0 = s0 + Lv.x; s1 = s1 + Lv.y; s2 = s2 + Lv.z;
                 ++smp;
-                phase = smp < spp ? PH_START : PH_DONEPX;
+                phase = (smp < spp && (smp & (GI_X_SPP_CHUNK - 1)) != 0) ? PH_START : PH_DONEPX;
             }
             if (STATS) t2 = clock64();
             // ---- the lane's next ray.  A primary ray that misses every child box of the root
@@ -806,12 +830,15 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             // GI_X_START_BURST primary rays per lane per handler run.
             int burst = 0;
             for (;;) {
-                if (phase == PH_DONEPX) {   // pixel complete
-                    const double c0 = smin(s0 / (double)spp, 1.0), c1 = smin(s1 / (double)spp, 1.0),
-                                 c2 = smin(s2 / (double)spp, 1.0);
-                    if (rgb) { rgb[3 * idx] = c0; rgb[3 * idx + 1] = c1; rgb[3 * idx + 2] = c2; }
-                    if (rgb8) quantize(c0, c1, c2, rgb8 + 3 * idx);
-                    ++npx;
+                if (phase == PH_DONEPX) {   // unit complete: the pixel, or one chunk sum of it
+                    if (wk.chunks == 1) {
+                        const double c0 = smin(s0 / (double)spp, 1.0), c1 = smin(s1 / (double)spp, 1.0),
+                                     c2 = smin(s2 / (double)spp, 1.0);
+                        if (rgb) { rgb[3 * idx] = c0; rgb[3 * idx + 1] = c1; rgb[3 * idx + 2] = c2; }
+                        if (rgb8) quantize(c0, c1, c2, rgb8 + 3 * idx);
+                    } else {
+                        wk.part[3 * idx] = s0; wk.part[3 * idx + 1] = s1; wk.part[3 * idx + 2] = s2;
+                    }
                     phase = PH_NEED;
                 }
                 const unsigned long long m_need = __ballot(phase == PH_NEED);
@@ -821,31 +848,27 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     if (lane == leader) base = atomicAdd(slot_counter, (unsigned)__popcll(m_need));
                     base = __shfl(base, leader);
                     if (phase == PH_NEED) {
-                        const unsigned sl = base + (unsigned)__popcll(m_need & ((1ull << lane) - 1));
-                        if (sl >= n_slots) {
+                        const unsigned u = base + (unsigned)__popcll(m_need & ((1ull << lane) - 1));
+                        if (u >= n_units) {
                             phase = PH_DEAD;
-                        } else if (slot_pixel(m, (long long)(sl >> 6), (int)(sl & 63), idx, x, y)) {
-                            y += m.y0;
-                            if (spp > 1 && pixel_misses_box(cam, x, y, sc.root_lo, sc.root_hi)) {
-                                // every jittered primary ray of this pixel misses the scene: all
-                                // spp samples add exactly +0, the pixel is 0 (rays resolved as a packet)
-                                if (rgb) { rgb[3 * idx] = 0; rgb[3 * idx + 1] = 0; rgb[3 * idx + 2] = 0; }
-                                if (rgb8) { rgb8[3 * idx] = 0; rgb8[3 * idx + 1] = 0; rgb8[3 * idx + 2] = 0; }
-                                nrays += spp;
-                                ++npx;
-                            } else {
+                        } else {
+                            const unsigned g = u / unit_group, r = u - g * unit_group;
+                            const unsigned c = r >> 6, i = g * 64u + (r & 63u);
+                            if (i < n_list) {   // else a padding unit of the last group: take another
+                                const unsigned ps = wk.list[i];
+                                slot_pixel(m, (long long)(ps >> 6), (int)(ps & 63), idx, x, y);
+                                y += m.y0;
+                                if (wk.chunks > 1) idx = (long long)c * wk.n_cap + i;   // chunk-sum slot
                                 key = mx_key(seed, (uint64_t)y * (uint64_t)m.w + (uint64_t)x);
-                                smp = 0;
+                                smp = (int)c * GI_X_SPP_CHUNK;
                                 s0 = s1 = s2 = 0;
                                 phase = PH_START;
+                                if (c == 0) ++npx;
                             }
-                        } else if (idx >= 0 && m.shard_count > 1) {   // padding slot of a packed tile
-                            if (rgb) { rgb[3 * idx] = 0; rgb[3 * idx + 1] = 0; rgb[3 * idx + 2] = 0; }
-                            if (rgb8) { rgb8[3 * idx] = 0; rgb8[3 * idx + 1] = 0; rgb8[3 * idx + 2] = 0; }
                         }
                     }
                 }
-                if (phase == PH_NEED) continue;   // got a padding slot: take another
+                if (phase == PH_NEED) continue;   // got a padding unit: take another
                 if (phase == PH_DEAD) break;
                 if (phase == PH_START) {
                     double jx = 0.0, jy = 0.0;
@@ -860,7 +883,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                             ++nrays;   // background sample: L = 0, sums unchanged
                             ++burst;
                             ++smp;
-                            phase = smp < spp ? PH_START : PH_DONEPX;
+                            phase = (smp < spp && (smp & (GI_X_SPP_CHUNK - 1)) != 0) ? PH_START : PH_DONEPX;
                             continue;
                         }
                     }
@@ -914,8 +937,8 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
 template <bool STATS, bool LDS>
 __global__ __launch_bounds__(256, GI_X_MIN_WAVES) void k_mode_x(DevScene sc, CamDev cam, V3 light, TileMap m, int spp, int depth,
                                                  uint64_t seed, double* rgb, uint8_t* rgb8,
-                                                 unsigned long long* stats, unsigned* slot_counter, int handle8,
-                                                 int xflags) {
+                                                 unsigned long long* stats, unsigned* slot_counter, XWork wk,
+                                                 int handle8, int xflags) {
     XCounters c;
     if (LDS) {
         extern __shared__ int4 lds_scene[];
@@ -928,10 +951,10 @@ __global__ __launch_bounds__(256, GI_X_MIN_WAVES) void k_mode_x(DevScene sc, Cam
         __syncthreads();
         const XWNode* W = reinterpret_cast<const XWNode*>(lds_scene);
         const XHot* H = reinterpret_cast<const XHot*>(lds_scene + nw);
-        mode_x_wave<STATS, true>(sc, W, H, cam, light, m, spp, depth, seed, rgb, rgb8, slot_counter, handle8, xflags, c);
+        mode_x_wave<STATS, true>(sc, W, H, cam, light, m, spp, depth, seed, rgb, rgb8, slot_counter, wk, handle8, xflags, c);
     } else {
         mode_x_wave<STATS, false>(sc, sc.xwnodes, sc.xhot, cam, light, m, spp, depth, seed, rgb, rgb8, slot_counter,
-                                  handle8, xflags, c);
+                                  wk, handle8, xflags, c);
     }
     if (STATS) {
         if ((threadIdx.x & 63) == 0) {
@@ -951,6 +974,66 @@ __global__ __launch_bounds__(256, GI_X_MIN_WAVES) void k_mode_x(DevScene sc, Cam
         for (int off = 32; off > 0; off >>= 1) cb += __shfl_xor(cb, off);
         if ((threadIdx.x & 63) == 0) atomicAdd(stats + GI_STAT_PBOX, (unsigned long long)cb);
     }
+}
+
+// Mode X pass 1: one thread per pixel slot (tile order; a wave = one 8x8 tile).  A pixel none of
+// whose jittered primary rays can meet the scene's root box (conservative fp64 frustum test) is 0:
+// every sample adds exactly +0, as in the oracle, which traces them.  Padding slots of a packed
+// tile are zeroed.  The other pixels are appended to the work list (one atomic per wave).
+template <bool STATS>
+__global__ __launch_bounds__(256) void k_x_classify(DevScene sc, CamDev cam, TileMap m, int spp, double* rgb,
+                                                     uint8_t* rgb8, unsigned* list, unsigned* n_list,
+                                                     unsigned long long* stats) {
+    const long long s = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long lt = s >> 6;
+    const int lane = threadIdx.x & 63;
+    long long idx = -1;
+    int x = 0, y = 0;
+    bool scene = false, zero = false, bg = false;
+    if (lt < m.n_local) {
+        if (slot_pixel(m, lt, lane, idx, x, y)) {
+            bg = pixel_misses_box(cam, x, y + m.y0, sc.root_lo, sc.root_hi);
+            scene = !bg;
+            zero = bg;
+        } else {
+            zero = idx >= 0 && m.shard_count > 1;   // padding slot of a packed tile
+        }
+    }
+    if (zero) {
+        if (rgb) { rgb[3 * idx] = 0; rgb[3 * idx + 1] = 0; rgb[3 * idx + 2] = 0; }
+        if (rgb8) { rgb8[3 * idx] = 0; rgb8[3 * idx + 1] = 0; rgb8[3 * idx + 2] = 0; }
+    }
+    const unsigned long long ms = __ballot(scene);
+    if (ms) {
+        const int leader = __ffsll((long long)ms) - 1;
+        unsigned base = 0;
+        if (lane == leader) base = atomicAdd(n_list, (unsigned)__popcll(ms));
+        base = __shfl(base, leader);
+        if (scene) list[base + (unsigned)__popcll(ms & ((1ull << lane) - 1))] = (unsigned)s;
+    }
+    if (STATS && (s & ~63ll) < m.n_local * 64)
+        wave_add_stats(stats, bg ? (uint64_t)spp : 0, 0, 0, bg ? 1 : 0);
+}
+
+// Mode X pass 3 (spp > GI_SPP_CHUNK): a listed pixel's chunk sums added in chunk order from +0, then
+// min(sum / spp, 1) and the 8-bit store -- the oracle's operations (pixel_mode_x).
+__global__ __launch_bounds__(256) void k_x_reduce(TileMap m, XWork wk, int spp, double* rgb, uint8_t* rgb8) {
+    const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= *wk.n_list) return;
+    const unsigned ps = wk.list[i];
+    long long idx = -1;
+    int x = 0, y = 0;
+    slot_pixel(m, (long long)(ps >> 6), (int)(ps & 63), idx, x, y);
+    double a = 0, b = 0, c = 0;
+    for (int k = 0; k < wk.chunks; ++k) {
+        const double* p = wk.part + 3 * ((size_t)k * wk.n_cap + i);
+        a = a + p[0];
+        b = b + p[1];
+        c = c + p[2];
+    }
+    const double c0 = smin(a / (double)spp, 1.0), c1 = smin(b / (double)spp, 1.0), c2 = smin(c / (double)spp, 1.0);
+    if (rgb) { rgb[3 * idx] = c0; rgb[3 * idx + 1] = c1; rgb[3 * idx + 2] = c2; }
+    if (rgb8) quantize(c0, c1, c2, rgb8 + 3 * idx);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1017,9 +1100,10 @@ TileMap make_map(int w, int h, int shard_count, int shard_index, int y0 = 0) {
 }  // namespace
 
 long long shard_tiles(int w, int h, int shard_count) { return make_map(w, h, shard_count, 0).n_local; }
+int x_spp_chunk() { return GI_X_SPP_CHUNK; }
 
 hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w, int h, int y0, const gi_opts& o,
-                         double* rgb, uint8_t* rgb8, hipStream_t stream) {
+                         double* rgb, uint8_t* rgb8, const XScratch& xs, hipStream_t stream) {
     const TileMap m = make_map(w, h, o.shard_count, o.shard_index, y0);
     if (m.n_local == 0) return hipSuccess;
     const dim3 grid((unsigned)((m.n_local + kWavesPerBlock - 1) / kWavesPerBlock)), block(64 * kWavesPerBlock);
@@ -1050,10 +1134,24 @@ hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w,
             if (lds) resident_lds = lds_bytes;
         }
         const int resident = resident_blocks[lds];
-        const long long want = (m.n_local + kWavesPerBlock - 1) / kWavesPerBlock;
+        const long long n_slots = m.n_local * (kTile * kTile);
+        const int chunks = (o.spp + GI_X_SPP_CHUNK - 1) / GI_X_SPP_CHUNK;
+        const long long want = (m.n_local * chunks + kWavesPerBlock - 1) / kWavesPerBlock;   // one wave per 64 units
         const dim3 pgrid((unsigned)std::min<long long>(want, resident));
+        if (!xs.list || (unsigned long long)xs.cap < (unsigned long long)n_slots || (chunks > 1 && (!xs.part || xs.chunks < chunks)) ||
+            (unsigned long long)n_slots * (unsigned long long)chunks >= 0xFFFFFFFFull)
+            return hipErrorInvalidValue;
         hipError_t e = hipMemsetAsync(sc.work, 0, 16 * sizeof(unsigned), stream);
         if (e != hipSuccess) return e;
+        XWork wk;
+        wk.list = xs.list;
+        wk.n_list = sc.work + 1;
+        wk.part = xs.part;
+        wk.n_cap = (unsigned)xs.cap;
+        wk.chunks = chunks;
+        const dim3 sgrid((unsigned)((n_slots + 255) / 256));
+        if (stats) hipLaunchKernelGGL(k_x_classify<true>, sgrid, dim3(256), 0, stream, sc, cam, m, o.spp, rgb, rgb8, xs.list, sc.work + 1, st);
+        else hipLaunchKernelGGL(k_x_classify<false>, sgrid, dim3(256), 0, stream, sc, cam, m, o.spp, rgb, rgb8, xs.list, sc.work + 1, st);
         // shading-handler threshold (eighths of the live lanes that must wait): the builder's
         // estimate for the scene (DevScene::x_handle8), overridable for tuning with GI_X_HANDLE8
         static int env_h8 = -1;
@@ -1069,13 +1167,14 @@ hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w,
         }
         const int xf = env_xf >= 0 ? env_xf : sc.x_flags;
 #define GI_LAUNCH_X(S, L) hipLaunchKernelGGL((k_mode_x<S, L>), pgrid, block, lds_bytes, stream, sc, cam, light, m, o.spp, \
-                                           o.depth, o.seed, rgb, rgb8, st, sc.work, h8, xf)
+                                           o.depth, o.seed, rgb, rgb8, st, sc.work, wk, h8, xf)
         if (stats) {
             if (lds) GI_LAUNCH_X(true, true); else GI_LAUNCH_X(true, false);
         } else {
             if (lds) GI_LAUNCH_X(false, true); else GI_LAUNCH_X(false, false);
         }
 #undef GI_LAUNCH_X
+        if (chunks > 1) hipLaunchKernelGGL(k_x_reduce, sgrid, dim3(256), 0, stream, m, wk, o.spp, rgb, rgb8);
     }
     return hipGetLastError();
 }

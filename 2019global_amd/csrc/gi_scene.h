@@ -147,4 +147,13 @@ struct DevScene {
     float root_lo[3], root_hi[3];   // Mode X: union of the root's fp32 child boxes (conservative)
 };
 
+// Mode X per-launch work buffers, owned by the scene handle (gi_capi.cpp) and grown on demand:
+// the list of pixel slots left after the background test and the chunk sums of spp > GI_SPP_CHUNK.
+struct XScratch {
+    unsigned* list = nullptr;   // cap entries
+    double* part = nullptr;     // chunks * cap * 3 doubles
+    long long cap = 0;          // pixel slots the buffers hold
+    int chunks = 0;             // chunk count the part buffer was sized for
+};
+
 }  // namespace gi

@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Strong-scaling probe on ONE GPU: time the render of one rank's share of the frame for
+shard_count N = 1, 2, 4, 8 (rank 0 and rank N-1 of N), i.e. the per-rank kernel time of an N-GPU
+run without the gather.  ideal = t(1) / N; the ratio shows the load-balance tail at small shares.
+
+    python profiles/shard_scaling.py [--workload C3] [--reps 3]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="C3")
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--ns", default="1,2,4,8")
+    a = ap.parse_args()
+    import torch
+    from importlib import import_module
+    import bench
+    gi = import_module("2019global_amd")
+    scene_name, w, h, mode, spp, depth, desc = bench.WORKLOADS[a.workload]
+    sc = bench.make_scene(scene_name)
+    dev = gi.DeviceScene.from_scene(sc)
+    cam = gi.Camera(sc.cam_pos, sc.cam_look, sc.focal)
+    s = torch.cuda.current_stream()
+    buf = torch.empty(w * h * 3, dtype=torch.float64, device="cuda")
+    buf8 = torch.empty(w * h * 3, dtype=torch.uint8, device="cuda")
+    res = {"workload": a.workload}
+    t1 = None
+    for n in [int(x) for x in a.ns.split(",")]:
+        for r in sorted({0, n - 1}):
+            kw = dict(mode=mode, spp=spp, depth=depth, seed=2019, shard_count=n, shard_index=r)
+            dev.render_device(cam, sc.light, w, h, buf.data_ptr(), buf8.data_ptr(), s.cuda_stream, **kw)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(a.reps):
+                dev.render_device(cam, sc.light, w, h, buf.data_ptr(), buf8.data_ptr(), s.cuda_stream, **kw)
+            e1.record(s)
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / a.reps
+            if n == 1:
+                t1 = ms
+            res[f"N{n}_rank{r}_ms"] = round(ms, 3)
+            res[f"N{n}_rank{r}_speedup"] = round(t1 / ms, 3)
+            print(json.dumps({"n": n, "rank": r, "ms": round(ms, 3), "ideal_ms": round(t1 / n, 3),
+                              "speedup": round(t1 / ms, 3)}), flush=True)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

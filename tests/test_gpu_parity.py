@@ -154,9 +154,10 @@ def test_progressive_bands_equal_whole_frame(torch_cuda):
     a, a8 = d.render(cam_of(sc), sc.light, 200, 136)
     b, b8 = d.render(cam_of(sc), sc.light, 200, 136, band_rows=16)
     assert U.bits_equal(a, b).all() and (a8 == b8).all()
-    ax, _ = d.render(cam_of(sc), sc.light, 64, 40, mode=gi.MODE_X, spp=2, depth=3, seed=9)
-    bx, _ = d.render(cam_of(sc), sc.light, 64, 40, mode=gi.MODE_X, spp=2, depth=3, seed=9, band_rows=8)
-    assert U.bits_equal(ax, bx).all()
+    for spp in (2, 11):   # 11: two sample chunks per pixel (work list + chunk sums per band)
+        ax, _ = d.render(cam_of(sc), sc.light, 64, 40, mode=gi.MODE_X, spp=spp, depth=3, seed=9)
+        bx, _ = d.render(cam_of(sc), sc.light, 64, 40, mode=gi.MODE_X, spp=spp, depth=3, seed=9, band_rows=8)
+        assert U.bits_equal(ax, bx).all()
 
 
 def test_cancel_before_start(torch_cuda):
@@ -197,6 +198,20 @@ def test_mode_x_bit_exact_vs_oracle(torch_cuda, scene, w, h, spp, depth):
     assert (rgb8.reshape(-1, 3) == o["q"]).all()
 
 
+@pytest.mark.parametrize("scene,w,h,spp,depth", [("cornell", 24, 20, 8, 3), ("cornell", 24, 20, 9, 3),
+                                                  ("cornell", 21, 13, 17, 4), ("cornell", 16, 16, 64, 8),
+                                                  ("zoo", 20, 12, 12, 3), ("soup1000", 16, 16, 24, 5)])
+def test_mode_x_spp_chunks_bit_exact(torch_cuda, scene, w, h, spp, depth):
+    """spp > GI_SPP_CHUNK: a pixel's samples are split into chunks of 8 (separate work units on the
+    device, summed in chunk order by k_x_reduce); ragged last chunks included."""
+    sc = _scene(scene)
+    o = U.oracle_render(sc.to_scn(), w, h, mode=1, spp=spp, depth=depth, seed=41)
+    rgb, rgb8 = dev_scene(scene).render(cam_of(sc), sc.light, w, h, mode=gi.MODE_X, spp=spp, depth=depth, seed=41)
+    same = U.bits_equal(rgb.reshape(-1, 3), o["rgb"]).all(1)
+    assert same.all(), f"{(~same).sum()} of {same.size} pixels differ from the oracle"
+    assert (rgb8.reshape(-1, 3) == o["q"]).all()
+
+
 def test_mode_x_cornell_window_full_depth(torch_cuda):
     # C3 frame (1920x1080, depth 8) on a window, 2 spp: parity at the config's geometry
     sc = S.cornell_scene()
@@ -209,13 +224,13 @@ def test_mode_x_cornell_window_full_depth(torch_cuda):
 
 
 @pytest.mark.parametrize("n", [2, 3, 8])
-@pytest.mark.parametrize("mode", [gi.MODE_R, gi.MODE_X])
-def test_sharded_render_equals_single(torch_cuda, n, mode):
+@pytest.mark.parametrize("mode,spp", [(gi.MODE_R, 1), (gi.MODE_X, 2), (gi.MODE_X, 19)])
+def test_sharded_render_equals_single(torch_cuda, n, mode, spp):
     torch = torch_cuda
     sc = S.cornell_scene()
     d = dev_scene("cornell")
     w, h = 203, 117
-    kw = dict(mode=mode, spp=2, depth=4, seed=3) if mode == gi.MODE_X else {}
+    kw = dict(mode=mode, spp=spp, depth=4, seed=3) if mode == gi.MODE_X else {}
     full = torch.zeros(h * w * 3, dtype=torch.float64, device="cuda")
     full8 = torch.zeros(h * w * 3, dtype=torch.uint8, device="cuda")
     d.render_device(cam_of(sc), sc.light, w, h, full.data_ptr(), full8.data_ptr(), **kw)
@@ -324,12 +339,13 @@ def test_mode_x_ragged_frames_bit_exact(torch_cuda, scene, w, h, spp, depth):
     assert (rgb8.reshape(-1, 3) == o["q"]).all()
 
 
-def test_mode_x_ray_count_equals_oracle(torch_cuda):
+@pytest.mark.parametrize("spp", [4, 12])
+def test_mode_x_ray_count_equals_oracle(torch_cuda, spp):
     """The bench's rays/frame (GI_FLAG_STATS) is the frame's ray count as the oracle traces it ray by
     ray -- including primary rays the device resolves by its root-box and pixel-frustum tests."""
     torch = torch_cuda
     sc = S.cornell_scene()
-    w, h, spp, depth = 96, 64, 4, 6
+    w, h, depth = 96, 64, 6
     o = U.oracle_render(sc.to_scn(), w, h, mode=1, spp=spp, depth=depth, seed=5)
     st = torch.zeros(gi.STATS_N, dtype=torch.int64, device="cuda")
     buf = torch.zeros(w * h * 3, dtype=torch.float64, device="cuda")
