@@ -194,9 +194,10 @@ int gi_scene_create(const gi_scene_desc* desc, gi_scene** out) {
     d.x_handle8 = h.x_handle8;
     d.x_flags = h.x_flags;
     d.n_xhot = (int32_t)h.xhot.size();
-    {   // LDS-resident traversal structure for small scenes (<= 40 KB per workgroup: three
-        // 256-thread workgroups per CU stay resident within the CU's 160 KB of LDS)
-        const size_t bytes = h.xwnodes.size() * sizeof(XWNode) + h.xhot.size() * sizeof(XHot);
+    {   // LDS-resident traversal + shading records for small scenes (<= 40 KB per workgroup:
+        // three 256-thread workgroups per CU stay resident within the CU's 160 KB of LDS)
+        const size_t bytes = h.xwnodes.size() * sizeof(XWNode) + h.xhot.size() * sizeof(XHot) +
+                             h.xprims.size() * sizeof(XPrim) + h.ents.size() * sizeof(REnt);
         d.x_lds_bytes = bytes <= 40 * 1024 ? (int32_t)bytes : 0;
     }
     for (int k = 0; k < 3; ++k) { d.root_lo[k] = INFINITY; d.root_hi[k] = -INFINITY; }

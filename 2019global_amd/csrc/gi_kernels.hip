@@ -467,7 +467,7 @@ __device__ __forceinline__ bool pixel_misses_box(const CamDev& cam, int x, int y
     return false;
 }
 
-__device__ void x_texcoord(const DevScene& sc, const REnt& e, V3 ip, int32_t& x, int32_t& y) {
+__device__ __forceinline__ void x_texcoord(const DevScene& sc, const REnt& e, V3 ip, int32_t& x, int32_t& y) {
     if (e.kind == K_IMP_SPHERE) {
         const double r = e.radius;
         const double unit_v = 2.0 * REF_PI * r / 320.0;
@@ -585,8 +585,9 @@ struct XWork {
     int chunks;              // ceil(spp / GI_SPP_CHUNK)
 };
 
-template <bool STATS, bool PAIR, typename NodeP, typename HotP>
-__device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H, const CamDev& cam, V3 light,
+template <bool STATS, bool PAIR, typename NodeP, typename HotP, typename PrimP, typename EntP>
+__device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H, PrimP XP, EntP EN,
+                                            const CamDev& cam, V3 light,
                                             const TileMap& m, int spp, int depth, uint64_t seed, double* rgb,
                                             uint8_t* rgb8, unsigned* slot_counter, const XWork& wk, int handle8,
                                             int xflags, XCounters& cnt) {
@@ -759,8 +760,8 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 if (best < 0) {
                     end_path = true;
                 } else {
-                    const XPrim& p = sc.xprims[best];   // by reference: only used fields are loaded
-                    const REnt& e = sc.ents[p.ent];
+                    const XPrim& p = XP[best];   // by reference: only used fields are loaded
+                    const REnt& e = EN[p.ent];
                     const V3 P = o + tbest * d;
                     V3 N = p.kind == 0 ? ld3(p.n) : normalize(P - ld3(p.a));
                     if (!(dot(d, N) < 0)) N = -N;
@@ -942,19 +943,30 @@ __global__ __launch_bounds__(256, GI_X_MIN_WAVES) void k_mode_x(DevScene sc, Cam
     XCounters c;
     if (LDS) {
         extern __shared__ int4 lds_scene[];
+        // traversal records and shading records (primitives, entities): the shading handler then
+        // issues no global load, so its waits never include the lane's outstanding stores
         const int nw = sc.n_xwnodes * (int)(sizeof(XWNode) / sizeof(int4));
         const int nh = sc.n_xhot * (int)(sizeof(XHot) / sizeof(int4));
+        const int np = sc.n_xprims * (int)(sizeof(XPrim) / sizeof(int4));
+        const int ne = sc.n_ents * (int)(sizeof(REnt) / sizeof(int4));
         const int4* gw = reinterpret_cast<const int4*>(sc.xwnodes);
         const int4* gh = reinterpret_cast<const int4*>(sc.xhot);
+        const int4* gp = reinterpret_cast<const int4*>(sc.xprims);
+        const int4* ge = reinterpret_cast<const int4*>(sc.ents);
         for (int i = threadIdx.x; i < nw; i += blockDim.x) lds_scene[i] = gw[i];
         for (int i = threadIdx.x; i < nh; i += blockDim.x) lds_scene[nw + i] = gh[i];
+        for (int i = threadIdx.x; i < np; i += blockDim.x) lds_scene[nw + nh + i] = gp[i];
+        for (int i = threadIdx.x; i < ne; i += blockDim.x) lds_scene[nw + nh + np + i] = ge[i];
         __syncthreads();
         const XWNode* W = reinterpret_cast<const XWNode*>(lds_scene);
         const XHot* H = reinterpret_cast<const XHot*>(lds_scene + nw);
-        mode_x_wave<STATS, true>(sc, W, H, cam, light, m, spp, depth, seed, rgb, rgb8, slot_counter, wk, handle8, xflags, c);
+        const XPrim* XP = reinterpret_cast<const XPrim*>(lds_scene + nw + nh);
+        const REnt* EN = reinterpret_cast<const REnt*>(lds_scene + nw + nh + np);
+        mode_x_wave<STATS, true>(sc, W, H, XP, EN, cam, light, m, spp, depth, seed, rgb, rgb8, slot_counter, wk, handle8,
+                                 xflags, c);
     } else {
-        mode_x_wave<STATS, false>(sc, sc.xwnodes, sc.xhot, cam, light, m, spp, depth, seed, rgb, rgb8, slot_counter,
-                                  wk, handle8, xflags, c);
+        mode_x_wave<STATS, false>(sc, sc.xwnodes, sc.xhot, sc.xprims, sc.ents, cam, light, m, spp, depth, seed, rgb,
+                                  rgb8, slot_counter, wk, handle8, xflags, c);
     }
     if (STATS) {
         if ((threadIdx.x & 63) == 0) {
