@@ -19,7 +19,6 @@ struct CamDev {
 };
 bool build_host_scene(const gi_scene_desc& desc, HostScene& hs, std::string& err);
 long long shard_tiles(int w, int h, int shard_count);
-int x_spp_chunk();   // samples per work unit of the kernels (GI_SPP_CHUNK)
 hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w, int h, int y0, const gi_opts& o,
                          double* rgb, uint8_t* rgb8, const XScratch& xs, hipStream_t stream);
 hipError_t launch_unshard(int w, int h, int shard_count, const double* packed, const uint8_t* packed8, double* rgb,
@@ -95,13 +94,12 @@ int check_opts(const gi_scene* s, int w, int h, const gi_opts* o) {
 }
 
 // Mode X work buffers for a frame of w x h pixels cut into this call's shard (k_x_classify's list,
-// k_mode_x's chunk sums); grown, never shrunk.  hipFree synchronises with work still using them.
+// k_mode_x's per-sample radiance for spp > 1); grown, never shrunk.  hipFree synchronises with
+// work still using them.
 int ensure_xscratch(gi_scene* s, int w, int h, const gi_opts* o) {
     if (o->mode != GI_MODE_X) return GI_OK;
     const long long need = shard_tiles(w, h, o->shard_count) * GI_TILE * GI_TILE;
-    const int chunks = (o->spp + x_spp_chunk() - 1) / x_spp_chunk();
-    if ((unsigned long long)need * (unsigned long long)chunks >= 0xFFFFFFFFull)
-        return fail(GI_ERR_ARG, "mode X frame too large: slots x spp chunks must stay below 2^32");
+    if ((unsigned long long)need >= 0xFFFFFFFFull) return fail(GI_ERR_ARG, "mode X frame too large: 2^32 pixel slots");
     XScratch& x = s->xs;
     hipError_t e;
     if (x.cap < need) {
@@ -111,13 +109,13 @@ int ensure_xscratch(gi_scene* s, int w, int h, const gi_opts* o) {
         if ((e = hipMalloc((void**)&x.list, (size_t)need * sizeof(unsigned))) != hipSuccess) return hip_fail(e, "hipMalloc (work list)");
         x.cap = need;
     }
-    if (chunks > 1 && x.chunks < chunks) {
+    if (o->spp > 1 && x.spp < o->spp) {
         (void)hipFree(x.part);
         x.part = nullptr;
-        x.chunks = 0;
-        if ((e = hipMalloc((void**)&x.part, (size_t)chunks * (size_t)x.cap * 3 * sizeof(double))) != hipSuccess)
-            return hip_fail(e, "hipMalloc (chunk sums)");
-        x.chunks = chunks;
+        x.spp = 0;
+        if ((e = hipMalloc((void**)&x.part, (size_t)o->spp * (size_t)x.cap * 3 * sizeof(double))) != hipSuccess)
+            return hip_fail(e, "hipMalloc (per-sample radiance)");
+        x.spp = o->spp;
     }
     return GI_OK;
 }

@@ -566,35 +566,54 @@ struct XCounters {
 // Mode X work list (k_x_classify -> k_mode_x -> k_x_reduce).  A pixel whose every jittered primary
 // ray misses the scene's root box is resolved by the classifier (all samples add exactly +0); the
 // others are appended to `list` (their slot numbers in tile order).  k_mode_x's unit of work is one
-// (listed pixel, chunk of GI_SPP_CHUNK consecutive samples): units are numbered so that the 64
-// consecutive units of a wave are 64 listed pixels of one chunk.  With one chunk per pixel
-// (spp <= GI_SPP_CHUNK) the unit writes the pixel; otherwise it writes its chunk sum to
-// part[c][n_cap][3] and k_x_reduce adds the chunk sums in chunk order.  Splitting a pixel's samples
+// (listed pixel, run of k consecutive samples), k a power of two <= 8 chosen per launch from the
+// amount of work (about 8 units per lane: k = 8 for a whole C3 frame, 1 for an 8-way shard of it).
+// Units come in blocks of 64: block b = (group g of 64 listed pixels, run c), so one block is one
+// run of 64 pixels; a wave takes a whole block with one atomic and one coalesced load of the
+// group's 64 list entries, and hands its units to lanes as they need work (no per-unit round trip).
+// With spp > 1 every sample's radiance is stored to part[pixel][sample] and k_x_reduce adds a
+// pixel's samples in sample order from +0 (the oracle's sum), so results do not depend on k, on
+// the schedule or on the shard count; with spp == 1 the unit writes the pixel.  Splitting pixels
 // over lanes keeps every lane busy until the end of the frame (a whole 64-spp pixel per unit left
-// the kernel waiting on the last lanes' pixels: rendering 1/8 of the C3 frame took 75% of the time
-// of the whole frame).
-#ifndef GI_X_SPP_CHUNK
-#define GI_X_SPP_CHUNK GI_SPP_CHUNK   // the spec's chunk (include/gi.h); other values: A/B variants only
-#endif
-
+// the kernel waiting on its last lanes: rendering 1/8 of the C3 frame took 75% of the whole frame's
+// time).
 struct XWork {
     const unsigned* list;    // listed pixel slots (tile order)
     const unsigned* n_list;  // device count written by k_x_classify
-    double* part;            // chunk sums (chunks > 1)
-    unsigned n_cap;          // list capacity = part stride per chunk
-    int chunks;              // ceil(spp / GI_SPP_CHUNK)
+    double* part;            // per-sample radiance [list index][sample][3] (spp > 1)
+    unsigned* blocks;        // device counter of blocks taken
 };
+
+#ifndef GI_X_UNITS_PER_LANE
+#define GI_X_UNITS_PER_LANE 8   // target units per lane when choosing the run length k
+#endif
+#ifndef GI_X_MAX_RUN
+#define GI_X_MAX_RUN 8          // largest run length k (samples per unit)
+#endif
 
 template <bool STATS, bool PAIR, typename NodeP, typename HotP, typename PrimP, typename EntP>
 __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H, PrimP XP, EntP EN,
                                             const CamDev& cam, V3 light,
                                             const TileMap& m, int spp, int depth, uint64_t seed, double* rgb,
-                                            uint8_t* rgb8, unsigned* slot_counter, const XWork& wk, int handle8,
+                                            uint8_t* rgb8, unsigned* blk_list, const XWork& wk, int handle8,
                                             int xflags, XCounters& cnt) {
     const int lane = threadIdx.x & 63;
     const unsigned n_list = *wk.n_list;
-    const unsigned unit_group = 64u * (unsigned)wk.chunks;
-    const unsigned n_units = ((n_list + 63u) >> 6) * unit_group;
+    // run length k: the largest power of two <= GI_X_MAX_RUN (and <= spp) that still leaves about
+    // GI_X_UNITS_PER_LANE units per lane of the grid (every wave computes the same k)
+    int k = 1;
+    {
+        const double lanes = (double)gridDim.x * (double)blockDim.x;
+        const double samples = (double)n_list * (double)spp;
+        while (2 * k <= GI_X_MAX_RUN && 2 * k <= spp && samples / (2.0 * k) >= GI_X_UNITS_PER_LANE * lanes) k *= 2;
+    }
+    const unsigned runs = (unsigned)((spp + k - 1) / k);              // units per pixel
+    const unsigned n_blocks = ((n_list + 63u) >> 6) * runs;
+    // the wave's current block lives in its LDS row: blk_list[0..63] = the group's list entries,
+    // blk_meta = {units handed out, group, run}; lanes that do not run the handler keep no copy
+    unsigned* blk_meta = blk_list + 64;
+    if (lane == 0) blk_meta[0] = 64u;
+    __builtin_amdgcn_wave_barrier();
     const bool inline_shadow = (xflags & 1) != 0;
     uint32_t nnode = 0, nprim = 0, nrays = 0, nbox = 0, npx = 0;
     long long idx = -1;
@@ -819,9 +838,14 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 }
             }
             if (end_path) {
-                s0 = s0 + Lv.x; s1 = s1 + Lv.y; s2 = s2 + Lv.z;
+                if (spp == 1) {
+                    s0 = 0.0 + Lv.x; s1 = 0.0 + Lv.y; s2 = 0.0 + Lv.z;
+                } else {   // the sample's radiance; k_x_reduce sums a pixel's samples in order
+                    double* q = wk.part + 3 * ((size_t)idx * (size_t)spp + (size_t)smp);
+                    q[0] = Lv.x; q[1] = Lv.y; q[2] = Lv.z;
+                }
                 ++smp;
-                phase = (smp < spp && (smp & (GI_X_SPP_CHUNK - 1)) != 0) ? PH_START : PH_DONEPX;
+                phase = (smp < spp && (smp & (k - 1)) != 0) ? PH_START : PH_DONEPX;
             }
             if (STATS) t2 = clock64();
             // ---- the lane's next ray.  A primary ray that misses every child box of the root
@@ -831,41 +855,71 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             // GI_X_START_BURST primary rays per lane per handler run.
             int burst = 0;
             for (;;) {
-                if (phase == PH_DONEPX) {   // unit complete: the pixel, or one chunk sum of it
-                    if (wk.chunks == 1) {
-                        const double c0 = smin(s0 / (double)spp, 1.0), c1 = smin(s1 / (double)spp, 1.0),
-                                     c2 = smin(s2 / (double)spp, 1.0);
+                if (phase == PH_DONEPX) {   // unit complete (spp == 1: write the pixel)
+                    if (spp == 1) {
+                        const double c0 = smin(s0 / 1.0, 1.0), c1 = smin(s1 / 1.0, 1.0), c2 = smin(s2 / 1.0, 1.0);
                         if (rgb) { rgb[3 * idx] = c0; rgb[3 * idx + 1] = c1; rgb[3 * idx + 2] = c2; }
                         if (rgb8) quantize(c0, c1, c2, rgb8 + 3 * idx);
-                    } else {
-                        wk.part[3 * idx] = s0; wk.part[3 * idx + 1] = s1; wk.part[3 * idx + 2] = s2;
                     }
                     phase = PH_NEED;
                 }
                 const unsigned long long m_need = __ballot(phase == PH_NEED);
                 if (m_need) {
+                    // units of the wave's current block first, then of one new block (a refill asks
+                    // for at most 64 units = one block).  The block's 64 list entries live in this
+                    // wave's LDS row (the lanes that run the handler load them; the others may be
+                    // traversing), so handing out a unit costs one ds_read.
+                    const unsigned rank = (unsigned)__popcll(m_need & ((1ull << lane) - 1));
+                    const unsigned n_need = (unsigned)__popcll(m_need);
                     const int leader = __ffsll((long long)m_need) - 1;
-                    unsigned base = 0;
-                    if (lane == leader) base = atomicAdd(slot_counter, (unsigned)__popcll(m_need));
-                    base = __shfl(base, leader);
-                    if (phase == PH_NEED) {
-                        const unsigned u = base + (unsigned)__popcll(m_need & ((1ull << lane) - 1));
-                        if (u >= n_units) {
-                            phase = PH_DEAD;
-                        } else {
-                            const unsigned g = u / unit_group, r = u - g * unit_group;
-                            const unsigned c = r >> 6, i = g * 64u + (r & 63u);
-                            if (i < n_list) {   // else a padding unit of the last group: take another
-                                const unsigned ps = wk.list[i];
-                                slot_pixel(m, (long long)(ps >> 6), (int)(ps & 63), idx, x, y);
-                                y += m.y0;
-                                if (wk.chunks > 1) idx = (long long)c * wk.n_cap + i;   // chunk-sum slot
-                                key = mx_key(seed, (uint64_t)y * (uint64_t)m.w + (uint64_t)x);
-                                smp = (int)c * GI_X_SPP_CHUNK;
-                                s0 = s1 = s2 = 0;
-                                phase = PH_START;
-                                if (c == 0) ++npx;
+                    const unsigned used = blk_meta[0];
+                    unsigned g = blk_meta[1], c = blk_meta[2];
+                    const unsigned avail = 64u - used;
+                    unsigned j = used + rank;
+                    bool have = rank < avail;
+                    unsigned ps = have ? blk_list[j] : 0u;
+                    unsigned used_new = used + n_need;
+                    if (n_need > avail) {                          // take the next block
+                        unsigned nb = 0;
+                        if (lane == leader) nb = atomicAdd(wk.blocks, 1u);
+                        nb = __shfl(nb, leader);
+                        used_new = 64u;
+                        if (nb < n_blocks) {
+                            const unsigned ng = nb / runs, nc = nb - ng * runs;
+                            const unsigned long long m_act = __ballot(true);
+                            const unsigned ra = (unsigned)__popcll(m_act & ((1ull << lane) - 1));
+                            const unsigned na = (unsigned)__popcll(m_act);
+                            __builtin_amdgcn_wave_barrier();
+                            for (unsigned e = ra; e < 64u; e += na) {
+                                const unsigned li = ng * 64u + e;
+                                blk_list[e] = li < n_list ? wk.list[li] : 0xFFFFFFFFu;
                             }
+                            __builtin_amdgcn_wave_barrier();
+                            used_new = n_need - avail;
+                            if (lane == leader) { blk_meta[1] = ng; blk_meta[2] = nc; }
+                            if (!have) {
+                                j = rank - avail;
+                                ps = blk_list[j];
+                                c = nc;
+                                g = ng;
+                                have = true;
+                            }
+                        } else if (!have && phase == PH_NEED) {
+                            phase = PH_DEAD;                        // no work left
+                        }
+                    }
+                    if (lane == leader) blk_meta[0] = used_new;
+                    __builtin_amdgcn_wave_barrier();
+                    if (phase == PH_NEED && have) {
+                        const unsigned i = g * 64u + j;            // list index
+                        if (ps != 0xFFFFFFFFu) {                   // else a padding unit: take another
+                            slot_pixel(m, (long long)(ps >> 6), (int)(ps & 63), idx, x, y);
+                            y += m.y0;
+                            if (spp > 1) idx = (long long)i;        // per-sample radiance row
+                            key = mx_key(seed, (uint64_t)y * (uint64_t)m.w + (uint64_t)x);
+                            smp = (int)c * k;
+                            phase = PH_START;
+                            if (c == 0) ++npx;
                         }
                     }
                 }
@@ -881,10 +935,16 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                         const F3 iv0 = f3(__builtin_amdgcn_rcpf((float)d0.x), __builtin_amdgcn_rcpf((float)d0.y),
                                           __builtin_amdgcn_rcpf((float)d0.z));
                         if (!root_hit(sc, f3((float)cam.pos.x, (float)cam.pos.y, (float)cam.pos.z), iv0)) {
-                            ++nrays;   // background sample: L = 0, sums unchanged
+                            ++nrays;   // background sample: L = 0
+                            if (spp > 1) {
+                                double* q = wk.part + 3 * ((size_t)idx * (size_t)spp + (size_t)smp);
+                                q[0] = 0.0; q[1] = 0.0; q[2] = 0.0;
+                            } else {
+                                s0 = s1 = s2 = 0.0;
+                            }
                             ++burst;
                             ++smp;
-                            phase = (smp < spp && (smp & (GI_X_SPP_CHUNK - 1)) != 0) ? PH_START : PH_DONEPX;
+                            phase = (smp < spp && (smp & (k - 1)) != 0) ? PH_START : PH_DONEPX;
                             continue;
                         }
                     }
@@ -938,9 +998,10 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
 template <bool STATS, bool LDS>
 __global__ __launch_bounds__(256, GI_X_MIN_WAVES) void k_mode_x(DevScene sc, CamDev cam, V3 light, TileMap m, int spp, int depth,
                                                  uint64_t seed, double* rgb, uint8_t* rgb8,
-                                                 unsigned long long* stats, unsigned* slot_counter, XWork wk,
-                                                 int handle8, int xflags) {
+                                                 unsigned long long* stats, XWork wk, int handle8, int xflags) {
     XCounters c;
+    __shared__ unsigned s_blk[kWavesPerBlock][68];   // per wave: current block's list entries + state
+    unsigned* blk = s_blk[threadIdx.x >> 6];
     if (LDS) {
         extern __shared__ int4 lds_scene[];
         // traversal records and shading records (primitives, entities): the shading handler then
@@ -962,11 +1023,11 @@ __global__ __launch_bounds__(256, GI_X_MIN_WAVES) void k_mode_x(DevScene sc, Cam
         const XHot* H = reinterpret_cast<const XHot*>(lds_scene + nw);
         const XPrim* XP = reinterpret_cast<const XPrim*>(lds_scene + nw + nh);
         const REnt* EN = reinterpret_cast<const REnt*>(lds_scene + nw + nh + np);
-        mode_x_wave<STATS, true>(sc, W, H, XP, EN, cam, light, m, spp, depth, seed, rgb, rgb8, slot_counter, wk, handle8,
+        mode_x_wave<STATS, true>(sc, W, H, XP, EN, cam, light, m, spp, depth, seed, rgb, rgb8, blk, wk, handle8,
                                  xflags, c);
     } else {
         mode_x_wave<STATS, false>(sc, sc.xwnodes, sc.xhot, sc.xprims, sc.ents, cam, light, m, spp, depth, seed, rgb,
-                                  rgb8, slot_counter, wk, handle8, xflags, c);
+                                  rgb8, blk, wk, handle8, xflags, c);
     }
     if (STATS) {
         if ((threadIdx.x & 63) == 0) {
@@ -1027,7 +1088,7 @@ __global__ __launch_bounds__(256) void k_x_classify(DevScene sc, CamDev cam, Til
         wave_add_stats(stats, bg ? (uint64_t)spp : 0, 0, 0, bg ? 1 : 0);
 }
 
-// Mode X pass 3 (spp > GI_SPP_CHUNK): a listed pixel's chunk sums added in chunk order from +0, then
+// Mode X pass 3 (spp > 1): a listed pixel's per-sample radiance added in sample order from +0, then
 // min(sum / spp, 1) and the 8-bit store -- the oracle's operations (pixel_mode_x).
 __global__ __launch_bounds__(256) void k_x_reduce(TileMap m, XWork wk, int spp, double* rgb, uint8_t* rgb8) {
     const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1037,11 +1098,11 @@ __global__ __launch_bounds__(256) void k_x_reduce(TileMap m, XWork wk, int spp, 
     int x = 0, y = 0;
     slot_pixel(m, (long long)(ps >> 6), (int)(ps & 63), idx, x, y);
     double a = 0, b = 0, c = 0;
-    for (int k = 0; k < wk.chunks; ++k) {
-        const double* p = wk.part + 3 * ((size_t)k * wk.n_cap + i);
-        a = a + p[0];
-        b = b + p[1];
-        c = c + p[2];
+    const double* p = wk.part + 3 * (size_t)i * (size_t)spp;
+    for (int s = 0; s < spp; ++s) {
+        a = a + p[3 * s];
+        b = b + p[3 * s + 1];
+        c = c + p[3 * s + 2];
     }
     const double c0 = smin(a / (double)spp, 1.0), c1 = smin(b / (double)spp, 1.0), c2 = smin(c / (double)spp, 1.0);
     if (rgb) { rgb[3 * idx] = c0; rgb[3 * idx + 1] = c1; rgb[3 * idx + 2] = c2; }
@@ -1112,7 +1173,6 @@ TileMap make_map(int w, int h, int shard_count, int shard_index, int y0 = 0) {
 }  // namespace
 
 long long shard_tiles(int w, int h, int shard_count) { return make_map(w, h, shard_count, 0).n_local; }
-int x_spp_chunk() { return GI_X_SPP_CHUNK; }
 
 hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w, int h, int y0, const gi_opts& o,
                          double* rgb, uint8_t* rgb8, const XScratch& xs, hipStream_t stream) {
@@ -1147,11 +1207,9 @@ hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w,
         }
         const int resident = resident_blocks[lds];
         const long long n_slots = m.n_local * (kTile * kTile);
-        const int chunks = (o.spp + GI_X_SPP_CHUNK - 1) / GI_X_SPP_CHUNK;
-        const long long want = (m.n_local * chunks + kWavesPerBlock - 1) / kWavesPerBlock;   // one wave per 64 units
-        const dim3 pgrid((unsigned)std::min<long long>(want, resident));
-        if (!xs.list || (unsigned long long)xs.cap < (unsigned long long)n_slots || (chunks > 1 && (!xs.part || xs.chunks < chunks)) ||
-            (unsigned long long)n_slots * (unsigned long long)chunks >= 0xFFFFFFFFull)
+        const long long want = (n_slots * std::min(o.spp, GI_X_MAX_RUN) / 64 + kWavesPerBlock - 1) / kWavesPerBlock;
+        const dim3 pgrid((unsigned)std::max<long long>(1, std::min<long long>(want, resident)));
+        if (!xs.list || (unsigned long long)xs.cap < (unsigned long long)n_slots || (o.spp > 1 && (!xs.part || xs.spp < o.spp)))
             return hipErrorInvalidValue;
         hipError_t e = hipMemsetAsync(sc.work, 0, 16 * sizeof(unsigned), stream);
         if (e != hipSuccess) return e;
@@ -1159,8 +1217,7 @@ hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w,
         wk.list = xs.list;
         wk.n_list = sc.work + 1;
         wk.part = xs.part;
-        wk.n_cap = (unsigned)xs.cap;
-        wk.chunks = chunks;
+        wk.blocks = sc.work;
         const dim3 sgrid((unsigned)((n_slots + 255) / 256));
         if (stats) hipLaunchKernelGGL(k_x_classify<true>, sgrid, dim3(256), 0, stream, sc, cam, m, o.spp, rgb, rgb8, xs.list, sc.work + 1, st);
         else hipLaunchKernelGGL(k_x_classify<false>, sgrid, dim3(256), 0, stream, sc, cam, m, o.spp, rgb, rgb8, xs.list, sc.work + 1, st);
@@ -1179,14 +1236,14 @@ hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w,
         }
         const int xf = env_xf >= 0 ? env_xf : sc.x_flags;
 #define GI_LAUNCH_X(S, L) hipLaunchKernelGGL((k_mode_x<S, L>), pgrid, block, lds_bytes, stream, sc, cam, light, m, o.spp, \
-                                           o.depth, o.seed, rgb, rgb8, st, sc.work, wk, h8, xf)
+                                           o.depth, o.seed, rgb, rgb8, st, wk, h8, xf)
         if (stats) {
             if (lds) GI_LAUNCH_X(true, true); else GI_LAUNCH_X(true, false);
         } else {
             if (lds) GI_LAUNCH_X(false, true); else GI_LAUNCH_X(false, false);
         }
 #undef GI_LAUNCH_X
-        if (chunks > 1) hipLaunchKernelGGL(k_x_reduce, sgrid, dim3(256), 0, stream, m, wk, o.spp, rgb, rgb8);
+        if (o.spp > 1) hipLaunchKernelGGL(k_x_reduce, sgrid, dim3(256), 0, stream, m, wk, o.spp, rgb, rgb8);
     }
     return hipGetLastError();
 }

@@ -148,12 +148,13 @@ struct DevScene {
 };
 
 // Mode X per-launch work buffers, owned by the scene handle (gi_capi.cpp) and grown on demand:
-// the list of pixel slots left after the background test and the chunk sums of spp > GI_SPP_CHUNK.
+// the list of pixel slots left after the background test and, for spp > 1, every listed pixel's
+// per-sample radiance (summed in sample order by k_x_reduce).
 struct XScratch {
     unsigned* list = nullptr;   // cap entries
-    double* part = nullptr;     // chunks * cap * 3 doubles
+    double* part = nullptr;     // cap * spp * 3 doubles
     long long cap = 0;          // pixel slots the buffers hold
-    int chunks = 0;             // chunk count the part buffer was sized for
+    int spp = 0;                // samples per pixel the part buffer was sized for
 };
 
 }  // namespace gi

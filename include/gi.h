@@ -118,9 +118,6 @@ typedef struct gi_opts {
 #define GI_STATS_N 16
 
 #define GI_TILE 8             /* shard granularity: 8x8 pixel tiles, dealt round-robin to ranks */
-#define GI_SPP_CHUNK 8        /* Mode X: a pixel's samples are summed in chunks of 8 consecutive samples
-                                 (each chunk from +0 in sample order, then the chunk sums in chunk
-                                 order); a chunk is the device's unit of work */
 
 typedef struct gi_scene gi_scene;
 

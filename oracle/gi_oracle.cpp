@@ -953,10 +953,7 @@ void pixel_mode_x(const Scene& s, const std::vector<Prim>& prims, const Cam& c, 
                   int spp, int depth, uint64_t seed, double* rgb, int32_t& hit0, int32_t& u0, int32_t& v0,
                   int32_t& nrays) {
     const uint64_t pix = (uint64_t)y * (uint64_t)w + (uint64_t)x;
-    // samples summed in chunks of kSppChunk (include/gi.h GI_SPP_CHUNK): each chunk from +0 in
-    // sample order, then sum = ((0 + chunk0) + chunk1) + ... in chunk order (Mode X)
-    constexpr int kSppChunk = 8;
-    double sum[3] = {0, 0, 0}, part[3] = {0, 0, 0};
+    double sum[3] = {0, 0, 0};
     hit0 = -1; u0 = v0 = 0;
     long rays = 0;
     for (int smp = 0; smp < spp; ++smp) {
@@ -1011,10 +1008,7 @@ void pixel_mode_x(const Scene& s, const std::vector<Prim>& prims, const Cam& c, 
             d = normalize((t1 * sx + t2 * sy) + N * sz);
             o = P;
         }
-        part[0] = part[0] + L.x; part[1] = part[1] + L.y; part[2] = part[2] + L.z;
-        if ((smp + 1) % kSppChunk == 0 || smp + 1 == spp) {
-            for (int k = 0; k < 3; ++k) { sum[k] = sum[k] + part[k]; part[k] = 0.0; }
-        }
+        sum[0] = sum[0] + L.x; sum[1] = sum[1] + L.y; sum[2] = sum[2] + L.z;
     }
     for (int k = 0; k < 3; ++k) rgb[k] = smin(sum[k] / (double)spp, 1.0);
     nrays = (int32_t)rays;

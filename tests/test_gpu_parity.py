@@ -154,7 +154,7 @@ def test_progressive_bands_equal_whole_frame(torch_cuda):
     a, a8 = d.render(cam_of(sc), sc.light, 200, 136)
     b, b8 = d.render(cam_of(sc), sc.light, 200, 136, band_rows=16)
     assert U.bits_equal(a, b).all() and (a8 == b8).all()
-    for spp in (2, 11):   # 11: two sample chunks per pixel (work list + chunk sums per band)
+    for spp in (2, 11):   # spp > 1: per-sample radiance rows + in-order reduce, per band
         ax, _ = d.render(cam_of(sc), sc.light, 64, 40, mode=gi.MODE_X, spp=spp, depth=3, seed=9)
         bx, _ = d.render(cam_of(sc), sc.light, 64, 40, mode=gi.MODE_X, spp=spp, depth=3, seed=9, band_rows=8)
         assert U.bits_equal(ax, bx).all()
@@ -201,15 +201,48 @@ def test_mode_x_bit_exact_vs_oracle(torch_cuda, scene, w, h, spp, depth):
 @pytest.mark.parametrize("scene,w,h,spp,depth", [("cornell", 24, 20, 8, 3), ("cornell", 24, 20, 9, 3),
                                                   ("cornell", 21, 13, 17, 4), ("cornell", 16, 16, 64, 8),
                                                   ("zoo", 20, 12, 12, 3), ("soup1000", 16, 16, 24, 5)])
-def test_mode_x_spp_chunks_bit_exact(torch_cuda, scene, w, h, spp, depth):
-    """spp > GI_SPP_CHUNK: a pixel's samples are split into chunks of 8 (separate work units on the
-    device, summed in chunk order by k_x_reduce); ragged last chunks included."""
+def test_mode_x_spp_runs_bit_exact(torch_cuda, scene, w, h, spp, depth):
+    """spp > 1: a pixel's samples are split into runs of k (separate work units on the device, each
+    sample's radiance stored and summed in sample order by k_x_reduce); odd spp included."""
     sc = _scene(scene)
     o = U.oracle_render(sc.to_scn(), w, h, mode=1, spp=spp, depth=depth, seed=41)
     rgb, rgb8 = dev_scene(scene).render(cam_of(sc), sc.light, w, h, mode=gi.MODE_X, spp=spp, depth=depth, seed=41)
     same = U.bits_equal(rgb.reshape(-1, 3), o["rgb"]).all(1)
     assert same.all(), f"{(~same).sum()} of {same.size} pixels differ from the oracle"
     assert (rgb8.reshape(-1, 3) == o["q"]).all()
+
+
+def test_mode_x_c3_config_windows_and_shards(torch_cuda):
+    """The bench's own workload: C3 = Cornell 1920x1080, depth 8, 64 spp (the device picks 8-sample
+    work units for the whole frame and 1-sample units for an 8-way shard of it).  Two windows against
+    the oracle, and the 8-shard frame against the whole frame bit for bit."""
+    torch = torch_cuda
+    sc = S.cornell_scene()
+    d = dev_scene("cornell")
+    w, h, kw = 1920, 1080, dict(mode=gi.MODE_X, spp=64, depth=8, seed=2019)
+    full = torch.zeros(w * h * 3, dtype=torch.float64, device="cuda")
+    full8 = torch.zeros(w * h * 3, dtype=torch.uint8, device="cuda")
+    d.render_device(cam_of(sc), sc.light, w, h, full.data_ptr(), full8.data_ptr(), **kw)
+    torch.cuda.synchronize()
+    f = full.cpu().numpy().reshape(h, w, 3)
+    for win in ((700, 1000, 716, 1016), (1100, 800, 1116, 816), (1180, 1040, 1196, 1056)):   # edge, wall, floor
+        o = U.oracle_render(sc.to_scn(), w, h, window=win, **{k: v for k, v in kw.items() if k != "mode"}, mode=1)
+        g = f[win[1]:win[3], win[0]:win[2]].reshape(-1, 3)
+        assert (o["hit"] >= 0).any()
+        assert U.bits_equal(g, o["rgb"]).all(), f"window {win}"
+    n = 8
+    per = gi.shard_tiles(w, h, n) * gi.TILE * gi.TILE * 3
+    packed = torch.zeros(n * per, dtype=torch.float64, device="cuda")
+    packed8 = torch.zeros(n * per, dtype=torch.uint8, device="cuda")
+    for r in range(n):
+        d.render_device(cam_of(sc), sc.light, w, h, packed.data_ptr() + r * per * 8, packed8.data_ptr() + r * per,
+                        shard_count=n, shard_index=r, **kw)
+    out = torch.zeros_like(full)
+    out8 = torch.zeros_like(full8)
+    gi.unshard_device(w, h, n, packed.data_ptr(), packed8.data_ptr(), out.data_ptr(), out8.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int64), full.view(torch.int64))
+    assert torch.equal(out8, full8)
 
 
 def test_mode_x_cornell_window_full_depth(torch_cuda):
