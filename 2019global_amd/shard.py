@@ -72,18 +72,18 @@ class FrameGather:
         else:
             self.packed_all = self.packed_all8 = self.parts = self.parts8 = None
 
-    def gather(self) -> None:
+    def gather(self, radiance: bool = True) -> None:
+        """Gathers the RGB888 frame (the reference's Image, image.h:14-16) and, unless
+        radiance=False, the fp64 radiance as well (8x the bytes: diagnostics / parity)."""
+        pairs = [(self.buf8, self.parts8)] + ([(self.buf, self.parts)] if radiance else [])
         if self.dist.get_backend() == "gloo" and self.buf.is_cuda:
             # gloo gathers host tensors only (rehearsal path: several ranks sharing one device)
-            parts = [p.cpu() for p in self.parts] if self.rank == 0 else None
-            parts8 = [p.cpu() for p in self.parts8] if self.rank == 0 else None
-            self.dist.gather(self.buf.cpu(), parts, dst=0)
-            self.dist.gather(self.buf8.cpu(), parts8, dst=0)
-            if self.rank == 0:
-                for d, s in zip(self.parts, parts):
-                    d.copy_(s)
-                for d, s in zip(self.parts8, parts8):
-                    d.copy_(s)
+            for src, dst in pairs:
+                host = [p.cpu() for p in dst] if self.rank == 0 else None
+                self.dist.gather(src.cpu(), host, dst=0)
+                if self.rank == 0:
+                    for d, s in zip(dst, host):
+                        d.copy_(s)
             return
-        self.dist.gather(self.buf, self.parts, dst=0)
-        self.dist.gather(self.buf8, self.parts8, dst=0)
+        for src, dst in pairs:
+            self.dist.gather(src, dst, dst=0)

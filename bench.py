@@ -8,7 +8,9 @@ one rank per GPU (RCCL over xGMI).  The frame's 8x8 pixel tiles are dealt round-
 ranks (tile t -> rank t % N), each rank renders its tiles into a packed buffer in HBM, and one
 ncclGather (torch.distributed.gather on the nccl backend) brings them to rank 0, which
 reassembles the frame with gi_unshard_device.  A step = one whole frame: render + gather +
-unshard; the frame is fixed as N grows ("scaling": "strong").
+unshard of the RGB888 image (the reference's output, image.h:14-16; every rank also writes its
+fp64 radiance, gathered once after the timed region for `frame_check`); the frame is fixed as N
+grows ("scaling": "strong").
 
 Default workload C3 (BASELINE.json configs[2]): Cornell box (34 ImpTriangles), 1920x1080,
 depth 8, 64 spp, Mode X (the build-defined integrator: the reference itself renders depth 1 only).
@@ -203,11 +205,10 @@ def main():
         dev.render_device(cam, sc.light, w, h, buf.data_ptr(), buf8.data_ptr(), sptr, **kw)
         if i is not None:
             ev1[i].record(stream)
-        if world > 1:   # one ncclGather of the packed tiles to rank 0, then reassembly on its GPU
-            fg.gather()
+        if world > 1:   # one ncclGather of the packed RGB888 tiles to rank 0, then reassembly on its GPU
+            fg.gather(radiance=False)
             if rank == 0:
-                gi.unshard_device(w, h, world, fg.packed_all.data_ptr(), fg.packed_all8.data_ptr(), frame.data_ptr(),
-                                  frame8.data_ptr(), sptr)
+                gi.unshard_device(w, h, world, 0, fg.packed_all8.data_ptr(), 0, frame8.data_ptr(), sptr)
 
     for _ in range(args.warmup):
         step()
@@ -230,6 +231,11 @@ def main():
         elapsed, kern_ms = t.tolist()
 
     frame_check = None
+    if world > 1:   # after timing: the last frame's fp64 radiance too, for the check below
+        fg.gather(radiance=True)
+        if rank == 0:
+            gi.unshard_device(w, h, world, fg.packed_all.data_ptr(), fg.packed_all8.data_ptr(), frame.data_ptr(),
+                              frame8.data_ptr(), sptr)
     if world > 1 and rank == 0:   # the assembled frame against a whole frame rendered here alone
         ref = torch.empty(w * h * 3, dtype=torch.float64, device="cuda")
         ref8 = torch.empty(w * h * 3, dtype=torch.uint8, device="cuda")
