@@ -42,6 +42,7 @@ LIB_PATH = os.environ.get("GI_LIB") or os.path.join(HERE, "libgi.so")   # GI_LIB
 
 MODE_R, MODE_X = 0, 1
 FLAG_STATS = 1
+FLAG_R_DFS = 2   # Mode R: reverse-DFS over the whole reference octree (A/B against the default)
 STAT_RAYS, STAT_NODES, STAT_PRIMS, STAT_PIXELS, STAT_PBOX = 0, 1, 2, 3, 4
 STAT_X_ITERS, STAT_X_TRAV, STAT_X_HANDLE, STAT_X_HLANES, STAT_X_HCLOSE, STAT_X_HSHADOW = 5, 6, 7, 8, 9, 10
 STAT_X_CYC_TRAV, STAT_X_CYC_HIT, STAT_X_CYC_NEXT, STAT_X_CYC_ALL = 11, 12, 13, 14
@@ -339,11 +340,12 @@ class DeviceScene:
         return {f: getattr(i, f) for f, _ in SceneInfo._fields_}
 
     @staticmethod
-    def opts(mode=MODE_R, spp=1, depth=1, seed=0, shard_count=1, shard_index=0, band_rows=0, stats_ptr=0) -> Opts:
+    def opts(mode=MODE_R, spp=1, depth=1, seed=0, shard_count=1, shard_index=0, band_rows=0, stats_ptr=0,
+             flags=0) -> Opts:
         o = Opts()
         o.mode, o.spp, o.depth, o.seed = mode, spp, depth, seed
         o.shard_count, o.shard_index, o.band_rows = shard_count, shard_index, band_rows
-        o.flags = FLAG_STATS if stats_ptr else 0
+        o.flags = (FLAG_STATS if stats_ptr else 0) | flags
         o.stats = stats_ptr or None
         return o
 
@@ -361,9 +363,10 @@ class DeviceScene:
         return rgb, rgb8
 
     def render_device(self, cam: Camera, light, w: int, h: int, d_rgb: int, d_rgb8: int = 0, stream: int = 0,
-                      mode=MODE_R, spp=1, depth=1, seed=0, shard_count=1, shard_index=0, stats_ptr=0) -> None:
+                      mode=MODE_R, spp=1, depth=1, seed=0, shard_count=1, shard_index=0, stats_ptr=0,
+                      flags=0) -> None:
         """Asynchronous render into device buffers (gi_render_device); pointers are ints."""
-        o = self.opts(mode, spp, depth, seed, shard_count, shard_index, stats_ptr=stats_ptr)
+        o = self.opts(mode, spp, depth, seed, shard_count, shard_index, stats_ptr=stats_ptr, flags=flags)
         _check(lib().gi_render_device(self._h, ctypes.byref(cam._c), _d3(light), w, h, ctypes.byref(o),
                                       d_rgb or None, d_rgb8 or None, stream or None), "gi_render_device")
 

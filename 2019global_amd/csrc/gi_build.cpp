@@ -524,6 +524,7 @@ bool build_host_scene(const gi_scene_desc& desc, HostScene& hs, std::string& err
     }
     hs.n_reachable = 0;
     for (char r : reach) hs.n_reachable += r;
+    build_rcand(hs);   // Mode R candidate reconstruction (gi_bvh.cpp)
 
     // Mode X primitives (every entity, in push order; ExpQuad contributes its 2 triangles)
     hs.xprims.clear();

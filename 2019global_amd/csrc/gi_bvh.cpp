@@ -347,4 +347,113 @@ void build_xbvh(const std::vector<XPrim>& prims, const std::vector<double>& boun
     hs.x_flags = long_traversal ? 0 : 1;
 }
 
+// Mode R candidate reconstruction.  The reference's pixel is the LAST candidate of
+// Octree::intersect's list (octree.h:132-155, DFS over children 0..7) whose intersect() succeeds
+// (raytracer.h:53-74, A.1).  A leaf L is in the list iff every node on its path below the root is
+// non-empty (:140) and passes the ExpBox node test (:141-146); its entities appear at list
+// position (rank of L in the static DFS order, index in L's list).  So the answer is the hitting
+// entity whose latest reachable appearance is latest -- computable from the few entities the ray's
+// LINE passes near (the reference has no t > 0 test, A.2/A.3), without walking the tree:
+//   * every entity's appearances, by decreasing (leaf rank, position);
+//   * every leaf's root path, top-down, for the reachability check;
+//   * a line BVH over the entities that appear in some leaf, each boxed by the union of its
+//     triangles' prefilter spheres (gi_math.h tri_may_hit: a line outside them cannot produce a
+//     hit; the kernel widens the boxes by a margin covering the prefilter's 1e-12|oc|^2 slack and
+//     fp32 slab rounding).  ImpSpheres (a line test with fp32 coefficients, A.2) are not boxed:
+//     every ray tests them.
+void build_rcand(HostScene& hs) {
+    const int nn = (int)hs.rnodes.size(), ne = (int)hs.ents.size();
+    // static DFS order of the leaves and their paths
+    std::vector<int64_t> leaf_rank((size_t)nn, -1);
+    std::vector<std::vector<int32_t>> paths((size_t)nn);
+    std::vector<int32_t> path;
+    int64_t next = 0;
+    std::function<void(int)> dfs = [&](int n) {
+        const RNode& r = hs.rnodes[n];
+        if (r.child0 < 0) {
+            leaf_rank[n] = next++;
+            paths[n] = path;
+            return;
+        }
+        for (int c = 0; c < 8; ++c) {
+            path.push_back(r.child0 + c);
+            dfs(r.child0 + c);
+            path.pop_back();
+        }
+    };
+    if (nn > 0) dfs(0);
+    hs.rpath_off.assign((size_t)nn + 1, 0);
+    hs.rpath.clear();
+    for (int n = 0; n < nn; ++n) {
+        hs.rpath.insert(hs.rpath.end(), paths[n].begin(), paths[n].end());
+        hs.rpath_off[n + 1] = (int32_t)hs.rpath.size();
+    }
+    // appearances per entity, latest first
+    std::vector<std::vector<std::pair<int64_t, int32_t>>> app((size_t)ne);
+    for (int n = 0; n < nn; ++n) {
+        const RNode& r = hs.rnodes[n];
+        if (r.child0 >= 0) continue;
+        for (int p = 0; p < r.ent_cnt; ++p)
+            app[hs.leaf_ents[r.ent_off + p]].push_back({(leaf_rank[n] << 32) | (int64_t)p, n});
+    }
+    hs.app_off.assign((size_t)ne + 1, 0);
+    hs.app_leaf.clear();
+    hs.app_rank.clear();
+    for (int e = 0; e < ne; ++e) {
+        std::sort(app[e].begin(), app[e].end(), [](const std::pair<int64_t, int32_t>& a,
+                                                   const std::pair<int64_t, int32_t>& b) { return a.first > b.first; });
+        for (const auto& a : app[e]) {
+            hs.app_rank.push_back(a.first);
+            hs.app_leaf.push_back(a.second);
+        }
+        hs.app_off[e + 1] = (int32_t)hs.app_rank.size();
+    }
+    // line BVH over the entities that appear somewhere
+    std::vector<XPrim> atoms;
+    std::vector<double> bounds;
+    std::vector<int32_t> atom_ent;
+    hs.r_always.clear();
+    hs.rc_ext = 0;
+    for (int e = 0; e < ne; ++e) {
+        if (app[e].empty()) continue;
+        const REnt& E = hs.ents[e];
+        if (E.kind == K_IMP_SPHERE || E.tri_count <= 0) {
+            hs.r_always.push_back(e);
+            continue;
+        }
+        double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+        bool finite = true;
+        for (int t = 0; t < E.tri_count; ++t) {
+            const TriRec& T = hs.tris[E.tri_first + t];
+            const V3 p1 = ld3(T.p1), p2 = ld3(T.p2), p3 = ld3(T.p3);
+            const V3 c = (p1 + p2 + p3) * (1.0 / 3.0);   // tri_may_hit's sphere
+            const double r2 = smax(smax(sq3(p1 - c), sq3(p2 - c)), sq3(p3 - c));
+            const double R = std::sqrt(r2 * 1.0201) * (1.0 + 1e-9) + 1e-300;
+            const double cc[3] = {c.x, c.y, c.z};
+            for (int k = 0; k < 3; ++k) {
+                mn[k] = std::min(mn[k], cc[k] - R);
+                mx[k] = std::max(mx[k], cc[k] + R);
+            }
+            finite = finite && std::isfinite(R) && std::isfinite(c.x) && std::isfinite(c.y) && std::isfinite(c.z);
+        }
+        if (!finite) {   // degenerate coordinates: no box can bound it, test it on every ray
+            hs.r_always.push_back(e);
+            continue;
+        }
+        XPrim p;
+        memset(&p, 0, sizeof p);
+        p.ent = e;
+        atoms.push_back(p);
+        for (int k = 0; k < 3; ++k) bounds.push_back(mn[k]);
+        for (int k = 0; k < 3; ++k) bounds.push_back(mx[k]);
+        for (int k = 0; k < 3; ++k) hs.rc_ext = std::max(hs.rc_ext, std::max(std::fabs(mn[k]), std::fabs(mx[k])));
+        atom_ent.push_back(e);
+    }
+    HostScene tmp;
+    build_xbvh(atoms, bounds, 4, tmp);
+    hs.rc_nodes = std::move(tmp.xwnodes);
+    hs.rc_ent.resize(tmp.xhot.size());
+    for (size_t j = 0; j < tmp.xhot.size(); ++j) hs.rc_ent[j] = atom_ent[tmp.xhot[j].prim];
+}
+
 }  // namespace gi

@@ -180,7 +180,11 @@ int gi_scene_create(const gi_scene_desc* desc, gi_scene** out) {
         (e = upload(s, h.xwnodes, &d.xwnodes)) != hipSuccess || (e = upload(s, h.xhot, &d.xhot)) != hipSuccess ||
         (e = upload(s, h.xbox, &d.xbox)) != hipSuccess ||
         (e = upload(s, h.xprims, &d.xprims)) != hipSuccess ||
-        (e = upload(s, std::vector<unsigned>(16, 0u), const_cast<const unsigned**>(&d.work))) != hipSuccess) {
+        (e = upload(s, std::vector<unsigned>(16, 0u), const_cast<const unsigned**>(&d.work))) != hipSuccess ||
+        (e = upload(s, h.app_off, &d.app_off)) != hipSuccess || (e = upload(s, h.app_leaf, &d.app_leaf)) != hipSuccess ||
+        (e = upload(s, h.app_rank, &d.app_rank)) != hipSuccess || (e = upload(s, h.rpath_off, &d.rpath_off)) != hipSuccess ||
+        (e = upload(s, h.rpath, &d.rpath)) != hipSuccess || (e = upload(s, h.rc_nodes, &d.rc_nodes)) != hipSuccess ||
+        (e = upload(s, h.rc_ent, &d.rc_ent)) != hipSuccess || (e = upload(s, h.r_always, &d.r_always)) != hipSuccess) {
         gi_scene_destroy(s);
         return hip_fail(e, "scene upload");
     }
@@ -192,6 +196,8 @@ int gi_scene_create(const gi_scene_desc* desc, gi_scene** out) {
     d.x_handle8 = h.x_handle8;
     d.x_flags = h.x_flags;
     d.n_xhot = (int32_t)h.xhot.size();
+    d.n_r_always = (int32_t)h.r_always.size();
+    d.rc_ext = (float)h.rc_ext;
     {   // LDS-resident traversal + shading records for small scenes (<= 40 KB per workgroup:
         // three 256-thread workgroups per CU stay resident within the CU's 160 KB of LDS)
         const size_t bytes = h.xwnodes.size() * sizeof(XWNode) + h.xhot.size() * sizeof(XHot) +

@@ -11,8 +11,9 @@
 //   so the kernel walks the same tree children 7..0 with a parent-pointer (stackless) traversal,
 //   scans each leaf list backwards, and stops at the first success.  Same node tests, same
 //   primitive math (gi_math.h), fewer of them.
-// Mode X (build-defined): per-pixel sample loop, closest-hit + shadow any-hit through
-//   the tight Mode X octree, front-to-back child order by ray-direction octant.
+// Mode X (build-defined): classify pass (background pixels) -> persistent path-tracing
+//   kernel over (pixel, run of samples) work units, closest-hit + shadow any-hit through the 8-wide
+//   BVH (front-to-back child slots by ray-direction octant) -> in-order per-sample reduce.
 //
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off (bit-level parity needs no FMA
 // contraction; f64 div/sqrt are correctly rounded on gfx950).
@@ -290,37 +291,6 @@ __device__ __forceinline__ V3 primary_dir(const CamDev& c, double fx, double fy)
     return (c.top_left - (c.left * fx) * c.rx) - (c.up * fy) * c.ry;
 }
 
-template <bool STATS>
-__global__ __launch_bounds__(256) void k_mode_r(DevScene sc, CamDev cam, V3 light, TileMap m, double* rgb,
-                                                 uint8_t* rgb8, unsigned long long* stats) {
-    long long idx = -1;
-    int x = 0, y = 0;
-    const long long lt = (long long)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-    const bool ok = lane_pixel(m, lt, idx, x, y);
-    y += m.y0;
-    uint32_t nnode = 0, nprim = 0;
-    if (ok) {
-        const V3 o = cam.pos;
-        const V3 d = normalize(primary_dir(cam, (double)x, (double)y));   // Ray ctor (ray.h:6)
-        RResult r;
-        trace_mode_r(sc, o, d, r, nnode, nprim);
-        double c0 = 0, c1 = 0, c2 = 0;
-        if (r.ent >= 0) {
-            const REnt e = sc.ents[r.ent];
-            int32_t u, v;
-            tex_coord(sc, e, r.P, u, v);
-            const V3 col = shade_ref(e, d, light, r.P, r.N, u, v);
-            c0 = col.x; c1 = col.y; c2 = col.z;
-        }
-        if (rgb) { rgb[3 * idx] = c0; rgb[3 * idx + 1] = c1; rgb[3 * idx + 2] = c2; }
-        if (rgb8) quantize(c0, c1, c2, rgb8 + 3 * idx);
-    } else if (idx >= 0 && m.shard_count > 1) {   // padding lanes of a packed tile
-        if (rgb) { rgb[3 * idx] = 0; rgb[3 * idx + 1] = 0; rgb[3 * idx + 2] = 0; }
-        if (rgb8) { rgb8[3 * idx] = 0; rgb8[3 * idx + 1] = 0; rgb8[3 * idx + 2] = 0; }
-    }
-    if (STATS && lt < m.n_local) wave_add_stats(stats, ok ? 1 : 0, nnode, nprim, ok ? 1 : 0);
-}
-
 // ---------------------------------------------------------------------------------------------
 // Mode X
 // ---------------------------------------------------------------------------------------------
@@ -438,6 +408,142 @@ __device__ __forceinline__ bool root_hit(const DevScene& sc, F3 of, F3 ivf) {
     const float tf = fminf(fmaxf(tx0, tx1), fminf(fmaxf(ty0, ty1), fmaxf(tz0, tz1)));
     return tn <= tf;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Mode R, candidate reconstruction (gi_bvh.cpp build_rcand).  The reference keeps the LAST hitting
+// candidate of Octree::intersect's list; a candidate's list position is (its leaf's rank in the
+// static DFS order, its index in the leaf's list), and a leaf is in the list iff every node of its
+// root path is non-empty and passes the exact ExpBox node test.  So: collect the entities whose
+// boxes the ray's LINE crosses (no t > 0 in the reference's tests, A.2/A.3) from a line BVH, test
+// each exactly (ent_hit), and keep the hitting entity whose latest reachable appearance is latest
+// (reachability = the same node tests, on that leaf's path only).  Same answer as the reference's
+// full DFS, with node tests only on the paths of hitting entities.
+// ---------------------------------------------------------------------------------------------
+// the 8 children of a line-BVH node against the whole line o + t d (t real), boxes widened by tau
+__device__ __forceinline__ uint32_t children_mask_line(const XWNode* nd, F3 of, F3 ivf, float tau) {
+    const float4* b = reinterpret_cast<const float4*>(nd);
+    float4 q[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) q[i] = b[i];
+    const int ex = nd->exists;
+    const float* v = reinterpret_cast<const float*>(q);   // lo[3][8] then hi[3][8]
+    uint32_t m = 0;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const float tx0 = ((v[c] - tau) - of.x) * ivf.x, tx1 = ((v[24 + c] + tau) - of.x) * ivf.x;
+        const float ty0 = ((v[8 + c] - tau) - of.y) * ivf.y, ty1 = ((v[32 + c] + tau) - of.y) * ivf.y;
+        const float tz0 = ((v[16 + c] - tau) - of.z) * ivf.z, tz1 = ((v[40 + c] + tau) - of.z) * ivf.z;
+        const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
+        const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+        m |= (uint32_t)((tn <= tf) & ((ex >> c) & 1)) << c;
+    }
+    return m;
+}
+
+// is leaf `leaf` in the ray's candidate list?  (octree.h:139-150 on its root path, top-down)
+__device__ __forceinline__ bool r_leaf_reachable(const DevScene& sc, int leaf, V3 o, V3 d, uint32_t& nnode) {
+    const int p1 = sc.rpath_off[leaf + 1];
+    for (int i = sc.rpath_off[leaf]; i < p1; ++i) {
+        const RNode& nd = sc.rnodes[sc.rpath[i]];
+        if (nd.ent_cnt == 0) return false;   // octree.h:140
+        ++nnode;
+        if (!box_hit(ld3(nd.mn), ld3(nd.mx), o, d)) return false;
+    }
+    return true;
+}
+
+// entity e as a candidate: exact test, then its latest reachable appearance against the best so far
+__device__ __forceinline__ void r_consider(const DevScene& sc, int e, V3 o, V3 d, long long& best, RResult& r,
+                                           uint32_t& nnode, uint32_t& nprim) {
+    const int a0 = sc.app_off[e], a1 = sc.app_off[e + 1];
+    if (a0 == a1 || sc.app_rank[a0] <= best) return;
+    V3 P, N;
+    if (!ent_hit(sc, sc.ents[e], o, d, P, N, nprim) || !(sq3(P - o) < DBL_MAX)) return;   // raytracer.h:58-65
+    for (int i = a0; i < a1; ++i) {
+        const long long rk = sc.app_rank[i];
+        if (rk <= best) return;
+        if (r_leaf_reachable(sc, sc.app_leaf[i], o, d, nnode)) {
+            best = rk;
+            r.ent = e;
+            r.P = P;
+            r.N = N;
+            return;
+        }
+    }
+}
+
+__device__ void trace_mode_r_cand(const DevScene& sc, V3 o, V3 d, float tau, RResult& r, uint32_t& nnode,
+                                  uint32_t& nprim) {
+    r.ent = -1;
+    long long best = -1;
+    for (int i = 0; i < sc.n_r_always; ++i) r_consider(sc, sc.r_always[i], o, d, best, r, nnode, nprim);
+    const XWNode* W = sc.rc_nodes;
+    const F3 of = f3((float)o.x, (float)o.y, (float)o.z);
+    const F3 ivf = f3(__builtin_amdgcn_rcpf((float)d.x), __builtin_amdgcn_rcpf((float)d.y), __builtin_amdgcn_rcpf((float)d.z));
+    uint64_t mlo = 0, mhi = 0;
+    int node = 0, level = 0;
+    const uint32_t rm = children_mask_line(W, of, ivf, tau);
+    lvl_set(mlo, mhi, 0, rm);
+    bool going = rm != 0;
+    while (going) {   // stackless: 8-bit "children left" mask per level, parent pointers
+        const uint32_t msk = lvl_get(mlo, mhi, level);
+        const int c = __builtin_ctz(msk);
+        lvl_set(mlo, mhi, level, msk & (msk - 1));
+        const XWNode* nd = W + node;
+        const int ch = nd->child[c];
+        if (ch < 0) {
+            const int cnt = nd->cnt[c];
+            for (int j = 0; j < cnt; ++j) r_consider(sc, sc.rc_ent[~ch + j], o, d, best, r, nnode, nprim);
+        } else {
+            const uint32_t cm = children_mask_line(W + ch, of, ivf, tau);
+            if (cm) {
+                node = ch;
+                ++level;
+                lvl_set(mlo, mhi, level, cm);
+            }
+        }
+        uint32_t rest = lvl_get(mlo, mhi, level);
+        while (rest == 0 && level > 0) {
+            --level;
+            node = level == 0 ? 0 : W[node].parent;
+            rest = lvl_get(mlo, mhi, level);
+        }
+        going = rest != 0;
+    }
+}
+
+template <bool STATS>
+__global__ __launch_bounds__(256) void k_mode_r(DevScene sc, CamDev cam, V3 light, TileMap m, double* rgb,
+                                                 uint8_t* rgb8, unsigned long long* stats, float tau, int dfs) {
+    long long idx = -1;
+    int x = 0, y = 0;
+    const long long lt = (long long)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    const bool ok = lane_pixel(m, lt, idx, x, y);
+    y += m.y0;
+    uint32_t nnode = 0, nprim = 0;
+    if (ok) {
+        const V3 o = cam.pos;
+        const V3 d = normalize(primary_dir(cam, (double)x, (double)y));   // Ray ctor (ray.h:6)
+        RResult r;
+        if (dfs) trace_mode_r(sc, o, d, r, nnode, nprim);   // the reference's list order, reversed (A/B)
+        else trace_mode_r_cand(sc, o, d, tau, r, nnode, nprim);
+        double c0 = 0, c1 = 0, c2 = 0;
+        if (r.ent >= 0) {
+            const REnt e = sc.ents[r.ent];
+            int32_t u, v;
+            tex_coord(sc, e, r.P, u, v);
+            const V3 col = shade_ref(e, d, light, r.P, r.N, u, v);
+            c0 = col.x; c1 = col.y; c2 = col.z;
+        }
+        if (rgb) { rgb[3 * idx] = c0; rgb[3 * idx + 1] = c1; rgb[3 * idx + 2] = c2; }
+        if (rgb8) quantize(c0, c1, c2, rgb8 + 3 * idx);
+    } else if (idx >= 0 && m.shard_count > 1) {   // padding lanes of a packed tile
+        if (rgb) { rgb[3 * idx] = 0; rgb[3 * idx + 1] = 0; rgb[3 * idx + 2] = 0; }
+        if (rgb8) { rgb8[3 * idx] = 0; rgb8[3 * idx + 1] = 0; rgb8[3 * idx + 2] = 0; }
+    }
+    if (STATS && lt < m.n_local) wave_add_stats(stats, ok ? 1 : 0, nnode, nprim, ok ? 1 : 0);
+}
+
 
 // Conservative packet test: true only if no ray through pixel (x, y)'s jitter square (corners
 // (x, y) .. (x+1, y+1): every jittered primary direction is a convex combination of the corner
@@ -1140,7 +1246,8 @@ __global__ void k_trace_ray(DevScene sc, V3 o, V3 d, V3 light, int32_t* out_i, d
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     RResult r;
     uint32_t nn = 0, np = 0;
-    trace_mode_r(sc, o, d, r, nn, np);
+    const double reach = fmax(fabs(o.x), fmax(fabs(o.y), fabs(o.z))) + (double)sc.rc_ext;
+    trace_mode_r_cand(sc, o, d, (float)(1e-5 * reach + 1e-30), r, nn, np);
     out_i[0] = r.ent;
     out_i[1] = out_i[2] = 0;
     for (int k = 0; k < 9; ++k) out_d[k] = 0;
@@ -1182,8 +1289,12 @@ hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w,
     unsigned long long* st = reinterpret_cast<unsigned long long*>(o.stats);
     const bool stats = (o.flags & GI_FLAG_STATS) && st;
     if (o.mode == GI_MODE_R) {
-        if (stats) hipLaunchKernelGGL(k_mode_r<true>, grid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st);
-        else hipLaunchKernelGGL(k_mode_r<false>, grid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st);
+        // line-BVH widening: the prefilter's 1e-12|oc|^2 slack (<= 1e-6 |oc|) and fp32 slab rounding
+        const double reach = std::max(std::fabs(cam.pos.x), std::max(std::fabs(cam.pos.y), std::fabs(cam.pos.z))) + (double)sc.rc_ext;
+        const float tau = (float)(1e-5 * reach + 1e-30);
+        const int dfs = (o.flags & GI_FLAG_R_DFS) ? 1 : 0;
+        if (stats) hipLaunchKernelGGL(k_mode_r<true>, grid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, dfs);
+        else hipLaunchKernelGGL(k_mode_r<false>, grid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, dfs);
     } else {
         // persistent grid: as many 4-wave blocks as can be resident, each wave pulls tiles
         static int env_lds = -1;   // GI_X_LDS=0 disables the LDS-resident scene (tuning)

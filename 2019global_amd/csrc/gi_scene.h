@@ -110,6 +110,16 @@ struct HostScene {
     std::vector<XBox> xbox;
     std::vector<XPrim> xprims;
     int32_t x_max_depth = 0;
+    // Mode R candidate reconstruction (gi_bvh.cpp build_rcand; DESIGN.md §5 k_mode_r)
+    std::vector<int32_t> app_off;    // per entity (n_ents + 1): its appearances in leaf lists
+    std::vector<int32_t> app_leaf;   //   leaf node of each appearance, by decreasing rank
+    std::vector<int64_t> app_rank;   //   (leaf's rank in the reference's DFS order << 32) | position
+    std::vector<int32_t> rpath_off;  // per node (n_rnodes + 1): its path below the root, top-down
+    std::vector<int32_t> rpath;      //   (filled for leaves; the leaf itself is the last entry)
+    std::vector<XWNode> rc_nodes;    // line BVH over the non-sphere entities that appear in a leaf
+    std::vector<int32_t> rc_ent;     //   entity of each leaf record
+    std::vector<int32_t> r_always;   // ImpSpheres that appear in a leaf (tested by every ray)
+    double rc_ext = 0;               // max |coordinate| of the line BVH's boxes
     int32_t x_handle8 = 6;   // Mode X handler threshold (eighths), chosen by the builder
     int32_t x_flags = 0;     // Mode X schedule flags (DevScene::x_flags), chosen by the builder
     double x_est_nodes = 0, x_est_prims = 0;   // SAH estimates per random ray through the root
@@ -126,6 +136,9 @@ inline void finalize_xwnodes(std::vector<XWNode>& w) {
 
 // Mode X 8-wide BVH over the primitives (gi_bvh.cpp); bounds: 6 doubles (min xyz, max xyz) each.
 void build_xbvh(const std::vector<XPrim>& prims, const std::vector<double>& bounds, int leaf_max, HostScene& hs);
+// Mode R candidate reconstruction structures (HostScene app_* / rpath* / rc_* / r_always) from the
+// reference octree (rnodes, leaf_ents) and the entities' triangles.
+void build_rcand(HostScene& hs);
 
 // Device view passed to kernels by value.
 struct DevScene {
@@ -145,6 +158,17 @@ struct DevScene {
     int32_t n_xhot;
     int32_t x_lds_bytes;   // > 0: xwnodes + xhot fit in LDS and are staged there by each workgroup
     float root_lo[3], root_hi[3];   // Mode X: union of the root's fp32 child boxes (conservative)
+    // Mode R candidate reconstruction (HostScene fields of the same names)
+    const int32_t* app_off;
+    const int32_t* app_leaf;
+    const int64_t* app_rank;
+    const int32_t* rpath_off;
+    const int32_t* rpath;
+    const XWNode* rc_nodes;
+    const int32_t* rc_ent;
+    const int32_t* r_always;
+    int32_t n_r_always;
+    float rc_ext;
 };
 
 // Mode X per-launch work buffers, owned by the scene handle (gi_capi.cpp) and grown on demand:

@@ -85,6 +85,8 @@ typedef enum gi_mode {
 } gi_mode;
 
 #define GI_FLAG_STATS 1u   /* accumulate work counters into opts->stats (device pointer) */
+#define GI_FLAG_R_DFS 2u   /* Mode R: walk the whole reference octree in reverse DFS order instead of
+                              reconstructing the candidate list (same result; A/B and tests) */
 
 typedef struct gi_opts {
     int32_t mode;          /* gi_mode */

@@ -416,3 +416,39 @@ def test_degenerate_triangles_match_oracle(torch_cuda):
     ox = U.oracle_render(s.to_scn(), w, h, mode=1, spp=2, depth=4, seed=9)
     rgb, _ = d.render(cam_of(s), s.light, w, h, mode=gi.MODE_X, spp=2, depth=4, seed=9)
     assert U.bits_equal(rgb.reshape(-1, 3), ox["rgb"]).all()
+
+
+@pytest.mark.parametrize("scene,w,h", [("main", 200, 200), ("cornell", 256, 160), ("zoo", 160, 160),
+                                       ("soup1000", 192, 128), ("sphere", 96, 96), ("only_expbox", 96, 96),
+                                       ("only_exprectangle", 96, 96), ("only_expcone", 96, 96)])
+def test_mode_r_candidate_reconstruction_equals_reverse_dfs(torch_cuda, scene, w, h):
+    """Mode R's default traversal (candidate reconstruction from the line BVH) against the reference
+    order walked in full (GI_FLAG_R_DFS): the same frame bit for bit, fp64 and RGB888."""
+    torch = torch_cuda
+    sc = _scene(scene)
+    d = dev_scene(scene)
+    out = []
+    for flags in (0, gi.FLAG_R_DFS):
+        a = torch.zeros(w * h * 3, dtype=torch.float64, device="cuda")
+        a8 = torch.zeros(w * h * 3, dtype=torch.uint8, device="cuda")
+        d.render_device(cam_of(sc), sc.light, w, h, a.data_ptr(), a8.data_ptr(), flags=flags)
+        out.append((a, a8))
+    torch.cuda.synchronize()
+    assert torch.equal(out[0][0].view(torch.int64), out[1][0].view(torch.int64))
+    assert torch.equal(out[0][1], out[1][1])
+
+
+def test_mode_r_soup100k_frame_equals_reverse_dfs(torch_cuda):
+    """C4's scene in Mode R (100k triangles, 59% of them lost by the reference octree): the whole
+    1920x1080 frame by candidate reconstruction equals the full reverse-DFS frame bit for bit."""
+    torch = torch_cuda
+    sc = S.soup_scene(100000)
+    d = dev_scene("soup100000")
+    w, h = 1920, 1080
+    out = []
+    for flags in (0, gi.FLAG_R_DFS):
+        a = torch.zeros(w * h * 3, dtype=torch.float64, device="cuda")
+        d.render_device(cam_of(sc), sc.light, w, h, a.data_ptr(), flags=flags)
+        out.append(a)
+    torch.cuda.synchronize()
+    assert torch.equal(out[0].view(torch.int64), out[1].view(torch.int64))
