@@ -25,7 +25,8 @@ def main(d, workload, kernel, out):
     for r in csv.DictReader(open(os.path.join(d, "trace", "run_kernel_stats.csv"))):
         stats[r["Name"]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                             "total_ns": float(r["TotalDurationNs"]), "pct": float(r["Percentage"])}
-    dom = [k for k in stats if kernel in k and "<false>" in k] or [k for k in stats if kernel in k]
+    # the timed launches: STATS=false is the kernel's first template argument (k_mode_x<false, ...>)
+    dom = [k for k in stats if kernel + "<false" in k] or [k for k in stats if kernel in k]
     dom_name = max(dom, key=lambda k: stats[k]["total_ns"])
     ctr = defaultdict(list)
     for f in sorted(glob.glob(os.path.join(d, "pmc*", "run_counter_collection.csv"))):
