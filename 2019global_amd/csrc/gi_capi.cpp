@@ -33,7 +33,7 @@ struct gi_scene {
     HostScene host;
     DevScene dev;
     std::vector<void*> allocs;
-    XScratch xs;   // Mode X work list + chunk sums, grown on demand (one render in flight per scene)
+    XScratch xs;   // Mode X work list + per-sample radiance, grown on demand (one render in flight per scene)
     int device = -1;
     int64_t bytes = 0;
     bool mode_x_ok = true;

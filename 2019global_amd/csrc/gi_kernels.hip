@@ -7,10 +7,12 @@
 // Mode R (reference semantics):
 //   The reference builds the full candidate list of Octree::intersect (octree.h:233-256, DFS over
 //   children 0..7, ExpBox node test) and keeps the LAST candidate whose intersect() succeeds
-//   (raytracer.h:53-74, A.1).  The last hit in DFS order is the first hit in reverse DFS order,
-//   so the kernel walks the same tree children 7..0 with a parent-pointer (stackless) traversal,
-//   scans each leaf list backwards, and stops at the first success.  Same node tests, same
-//   primitive math (gi_math.h), fewer of them.
+//   (raytracer.h:53-74, A.1).  The kernel reconstructs that answer from the entities the ray's line
+//   passes near (a line BVH), their exact tests and the reachability of their leaves (the same
+//   node tests on those leaves' root paths only): trace_mode_r_cand.  The reference-order walk --
+//   the last hit in DFS order is the first hit in reverse DFS order, children 7..0, leaf lists
+//   backwards, first success -- stays available (trace_mode_r, GI_FLAG_R_DFS); both give the same
+//   frame bit for bit.  Same primitive math (gi_math.h) as the reference.
 // Mode X (build-defined): classify pass (background pixels) -> persistent path-tracing
 //   kernel over (pixel, run of samples) work units, closest-hit + shadow any-hit through the 8-wide
 //   BVH (front-to-back child slots by ray-direction octant) -> in-order per-sample reduce.
@@ -1305,8 +1307,8 @@ hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w,
         const bool lds = env_lds != 0 && sc.x_lds_bytes > 0;
         const size_t lds_bytes = lds ? (size_t)sc.x_lds_bytes : 0;
         static int resident_blocks[2] = {0, 0};
-        static size_t resident_lds = 0;
-        if (resident_blocks[lds] == 0 || (lds && resident_lds != lds_bytes)) {
+        static size_t resident_lds[2] = {0, 0};
+        if (resident_blocks[lds] == 0 || resident_lds[lds] != lds_bytes) {
             int dev = 0, cus = 0, per_cu = 0;
             (void)hipGetDevice(&dev);
             (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -1314,7 +1316,7 @@ hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w,
                 &per_cu, lds ? reinterpret_cast<const void*>(k_mode_x<false, true>) : reinterpret_cast<const void*>(k_mode_x<false, false>),
                 64 * kWavesPerBlock, lds_bytes);
             resident_blocks[lds] = std::max(1, cus) * std::max(1, per_cu);
-            if (lds) resident_lds = lds_bytes;
+            resident_lds[lds] = lds_bytes;
         }
         const int resident = resident_blocks[lds];
         const long long n_slots = m.n_local * (kTile * kTile);
