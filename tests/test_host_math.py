@@ -32,3 +32,25 @@ def test_mode_x_acceleration_structure(tmp_path):
             out = subprocess.run([exe, *args], capture_output=True, text=True, env=dict(os.environ, **env))
             assert out.returncode == 0, (env, out.stdout)
             assert "mismatches 0" in out.stdout
+
+
+def test_mode_r_candidate_reconstruction_equals_reverse_dfs(tmp_path):
+    """Mode R's candidate reconstruction (line BVH + appearance ranks + leaf-path reachability, the
+    kernel's default) and the reference-order reverse DFS, both restated on the host over libgi's
+    scene builder: same hit entity and bit-identical point/normal on every ray -- random mixed scenes
+    (spheres, triangles, ExpQuad/ExpRectangle/ExpBox) and the main, Cornell, zoo, 1k- and 100k-soup
+    scenes."""
+    exe = str(tmp_path / "rcc")
+    csrc = os.path.join(U.ROOT, "2019global_amd", "csrc")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-I" + csrc,
+                    "-I" + os.path.join(U.ROOT, "include"), "-o", exe,
+                    os.path.join(U.ROOT, "tests", "cpp", "rcand_check.cpp"), os.path.join(csrc, "gi_build.cpp"),
+                    os.path.join(csrc, "gi_bvh.cpp")], check=True)
+    scns = []
+    for name in ("main", "cornell", "zoo", "soup1000", "soup100000"):
+        p = tmp_path / f"{name}.scn"
+        p.write_text(U.scenes().named_scene(name).to_scn())
+        scns.append(str(p))
+    out = subprocess.run([exe, "3000", *scns], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout
+    assert "mismatches 0" in out.stdout
