@@ -1294,7 +1294,9 @@ hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w,
         // line-BVH widening: the prefilter's 1e-12|oc|^2 slack (<= 1e-6 |oc|) and fp32 slab rounding
         const double reach = std::max(std::fabs(cam.pos.x), std::max(std::fabs(cam.pos.y), std::fabs(cam.pos.z))) + (double)sc.rc_ext;
         const float tau = (float)(1e-5 * reach + 1e-30);
-        const int dfs = (o.flags & GI_FLAG_R_DFS) ? 1 : 0;
+        // an octree that never split is one leaf: its list scanned backwards (first success) is
+        // already the least work
+        const int dfs = ((o.flags & GI_FLAG_R_DFS) || sc.n_rnodes <= 1) ? 1 : 0;
         if (stats) hipLaunchKernelGGL(k_mode_r<true>, grid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, dfs);
         else hipLaunchKernelGGL(k_mode_r<false>, grid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, dfs);
     } else {
