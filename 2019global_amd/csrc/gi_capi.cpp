@@ -203,6 +203,11 @@ int gi_scene_create(const gi_scene_desc* desc, gi_scene** out) {
         const size_t bytes = h.xwnodes.size() * sizeof(XWNode) + h.xhot.size() * sizeof(XHot) +
                              h.xprims.size() * sizeof(XPrim) + h.ents.size() * sizeof(REnt);
         d.x_lds_bytes = bytes <= 40 * 1024 ? (int32_t)bytes : 0;
+        // light shading (no acos texture mapping, no sphere primitives): 4 waves per SIMD pay off
+        d.x_waves4 = 1;
+        for (const REnt& r : h.ents)
+            if (r.kind == K_IMP_SPHERE || r.kind == K_EXP_SPHERE || r.kind == K_EXP_CONE || r.kind == K_EXP_RECTANGLE)
+                d.x_waves4 = 0;
     }
     for (int k = 0; k < 3; ++k) { d.root_lo[k] = INFINITY; d.root_hi[k] = -INFINITY; }
     if (!h.xwnodes.empty())

@@ -382,8 +382,35 @@ __device__ __forceinline__ bool box32_hit(const XBox& b, F3 of, F3 ivf, float tm
 // mask of hit, existing children with bit k for child k ^ dmask (bit order = front-to-back).
 // The node's 48 bounds are fetched by 12 independent 16-byte loads (one memory round trip) and
 // all 8 slab tests run branch-free; existence comes from the node's precomputed bit mask.
+// AXIS: the slab tests accumulate axis by axis (4 float4 live instead of 12: fewer VGPRs at the
+// node step, which lets the LDS-resident kernel run 4 waves per SIMD); otherwise all 12 loads are
+// issued at once (one memory round trip: the HBM-resident kernel's choice).  Same mask either way.
+template <bool AXIS>
 __device__ __forceinline__ uint32_t children_mask(const XWNode* nd, F3 of, F3 ivf, float tmax, int dmask) {
     const float4* b = reinterpret_cast<const float4*>(nd);
+    if constexpr (AXIS) {
+    float tn[8], tf[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) { tn[c] = 0.0f; tf[c] = tmax; }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float4 l0 = b[2 * a], l1 = b[2 * a + 1], h0 = b[6 + 2 * a], h1 = b[6 + 2 * a + 1];
+        const float lo[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
+        const float hi[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+        const float o = a == 0 ? of.x : (a == 1 ? of.y : of.z), iv = a == 0 ? ivf.x : (a == 1 ? ivf.y : ivf.z);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const float t0 = (lo[c] - o) * iv, t1 = (hi[c] - o) * iv;
+            tn[c] = fmaxf(tn[c], fminf(t0, t1));
+            tf[c] = fminf(tf[c], fmaxf(t0, t1));
+        }
+    }
+    const int ex = nd->exists;
+    uint32_t m = 0;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) m |= (uint32_t)((tn[c] <= tf[c]) & ((ex >> c) & 1)) << (c ^ dmask);
+    return m;
+    } else {
     float4 q[12];
 #pragma unroll
     for (int i = 0; i < 12; ++i) q[i] = b[i];
@@ -400,6 +427,7 @@ __device__ __forceinline__ uint32_t children_mask(const XWNode* nd, F3 of, F3 iv
         m |= (uint32_t)((tn <= tf) & ((ex >> c) & 1)) << (c ^ dmask);
     }
     return m;
+    }
 }
 
 __device__ __forceinline__ bool root_hit(const DevScene& sc, F3 of, F3 ivf) {
@@ -661,8 +689,14 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 #ifndef GI_X_START_BURST
 #define GI_X_START_BURST 16   // primary rays a lane may resolve by the root test per handler run
 #endif
+#ifndef GI_X_PAIR
+#define GI_X_PAIR 1   // LDS-resident scenes: leaf records tested two at a time (interleaved fp64 chains)
+#endif
 #ifndef GI_X_MIN_WAVES
-#define GI_X_MIN_WAVES 3   // minimum waves per SIMD for k_mode_x (register budget: <= 168 VGPRs)
+#define GI_X_MIN_WAVES 3       // minimum waves per SIMD, HBM-resident scenes (<= 168 VGPRs)
+#endif
+#ifndef GI_X_MIN_WAVES_LDS
+#define GI_X_MIN_WAVES_LDS 4   // LDS-resident scenes (<= 128 VGPRs; the few spills sit in the handler)
 #endif
 
 struct XCounters {
@@ -742,7 +776,6 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     // candidate sums L + T*lit (light visible) and L + T*dark (occluded), and T already holds the
     // next bounce's throughput (the oracle's operations, split around the shadow query)
     V3 Lv = v3(0, 0, 0), Lo = v3(0, 0, 0), T = v3(1, 1, 1);
-    double s0 = 0, s1 = 0, s2 = 0;
     V3 nextd = v3(0, 0, 0);   // carried across the shadow ray (its origin = the shadow ray's)
     bool has_next = false;
 
@@ -834,7 +867,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     (void)bp;
                 } else {                  // descend if any of the child's 8 children is hit (fp32)
                     ++nnode;
-                    const uint32_t cm = children_mask(W + ch, of, ivf, tbest_f, dmask);
+                    const uint32_t cm = children_mask<PAIR>(W + ch, of, ivf, tbest_f, dmask);
                     if (cm) {
                         node = ch;
                         ++level;
@@ -868,7 +901,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 ivf = f3(__builtin_amdgcn_rcpf((float)d.x), __builtin_amdgcn_rcpf((float)d.y),
                          __builtin_amdgcn_rcpf((float)d.z));
                 dmask = (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
-                const uint32_t rm = children_mask(W, of, ivf, tbest_f, dmask);
+                const uint32_t rm = children_mask<PAIR>(W, of, ivf, tbest_f, dmask);
                 best = -1;
                 node = 0;
                 level = 0;
@@ -946,8 +979,11 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 }
             }
             if (end_path) {
-                if (spp == 1) {
-                    s0 = 0.0 + Lv.x; s1 = 0.0 + Lv.y; s2 = 0.0 + Lv.z;
+                if (spp == 1) {   // the pixel: min((0 + L) / 1, 1), the reduce pass's operations
+                    const double c0 = smin((0.0 + Lv.x) / 1.0, 1.0), c1 = smin((0.0 + Lv.y) / 1.0, 1.0),
+                                 c2 = smin((0.0 + Lv.z) / 1.0, 1.0);
+                    if (rgb) { rgb[3 * idx] = c0; rgb[3 * idx + 1] = c1; rgb[3 * idx + 2] = c2; }
+                    if (rgb8) quantize(c0, c1, c2, rgb8 + 3 * idx);
                 } else {   // the sample's radiance; k_x_reduce sums a pixel's samples in order
                     double* q = wk.part + 3 * ((size_t)idx * (size_t)spp + (size_t)smp);
                     q[0] = Lv.x; q[1] = Lv.y; q[2] = Lv.z;
@@ -963,14 +999,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             // GI_X_START_BURST primary rays per lane per handler run.
             int burst = 0;
             for (;;) {
-                if (phase == PH_DONEPX) {   // unit complete (spp == 1: write the pixel)
-                    if (spp == 1) {
-                        const double c0 = smin(s0 / 1.0, 1.0), c1 = smin(s1 / 1.0, 1.0), c2 = smin(s2 / 1.0, 1.0);
-                        if (rgb) { rgb[3 * idx] = c0; rgb[3 * idx + 1] = c1; rgb[3 * idx + 2] = c2; }
-                        if (rgb8) quantize(c0, c1, c2, rgb8 + 3 * idx);
-                    }
-                    phase = PH_NEED;
-                }
+                if (phase == PH_DONEPX) phase = PH_NEED;   // unit complete (its samples are stored)
                 const unsigned long long m_need = __ballot(phase == PH_NEED);
                 if (m_need) {
                     // units of the wave's current block first, then of one new block (a refill asks
@@ -1047,8 +1076,9 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                             if (spp > 1) {
                                 double* q = wk.part + 3 * ((size_t)idx * (size_t)spp + (size_t)smp);
                                 q[0] = 0.0; q[1] = 0.0; q[2] = 0.0;
-                            } else {
-                                s0 = s1 = s2 = 0.0;
+                            } else {   // spp == 1: the pixel is 0
+                                if (rgb) { rgb[3 * idx] = 0.0; rgb[3 * idx + 1] = 0.0; rgb[3 * idx + 2] = 0.0; }
+                                if (rgb8) { rgb8[3 * idx] = 0; rgb8[3 * idx + 1] = 0; rgb8[3 * idx + 2] = 0; }
                             }
                             ++burst;
                             ++smp;
@@ -1071,7 +1101,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 ivf = f3(__builtin_amdgcn_rcpf((float)d.x), __builtin_amdgcn_rcpf((float)d.y),
                          __builtin_amdgcn_rcpf((float)d.z));
                 dmask = (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
-                const uint32_t rm = children_mask(W, of, ivf, tbest_f, dmask);
+                const uint32_t rm = children_mask<PAIR>(W, of, ivf, tbest_f, dmask);
                 if (phase == PH_START) phase = PH_CLOSEST;
                 best = -1;
                 node = 0;   // root wide node
@@ -1103,8 +1133,11 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
 // LDS: small scenes (sc.x_lds_bytes > 0) keep the whole traversal structure -- wide nodes and
 // leaf records -- in LDS, copied once by each resident workgroup; every traversal load is then a
 // ds_read instead of a vector-memory round trip.
-template <bool STATS, bool LDS>
-__global__ __launch_bounds__(256, GI_X_MIN_WAVES) void k_mode_x(DevScene sc, CamDev cam, V3 light, TileMap m, int spp, int depth,
+// W4: 4 waves per SIMD (<= 128 VGPRs) for LDS-resident scenes whose shading is light (triangles
+// without acos texture mapping: +7% on the Cornell box); scenes with spheres / cones / rectangles
+// keep 3 (their heavier handler spills at 128 VGPRs: -45% on the main.cpp scene at 4).
+template <bool STATS, bool LDS, bool W4>
+__global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WAVES) void k_mode_x(DevScene sc, CamDev cam, V3 light, TileMap m, int spp, int depth,
                                                  uint64_t seed, double* rgb, uint8_t* rgb8,
                                                  unsigned long long* stats, XWork wk, int handle8, int xflags) {
     XCounters c;
@@ -1131,7 +1164,7 @@ __global__ __launch_bounds__(256, GI_X_MIN_WAVES) void k_mode_x(DevScene sc, Cam
         const XHot* H = reinterpret_cast<const XHot*>(lds_scene + nw);
         const XPrim* XP = reinterpret_cast<const XPrim*>(lds_scene + nw + nh);
         const REnt* EN = reinterpret_cast<const REnt*>(lds_scene + nw + nh + np);
-        mode_x_wave<STATS, true>(sc, W, H, XP, EN, cam, light, m, spp, depth, seed, rgb, rgb8, blk, wk, handle8,
+        mode_x_wave<STATS, GI_X_PAIR != 0>(sc, W, H, XP, EN, cam, light, m, spp, depth, seed, rgb, rgb8, blk, wk, handle8,
                                  xflags, c);
     } else {
         mode_x_wave<STATS, false>(sc, sc.xwnodes, sc.xhot, sc.xprims, sc.ents, cam, light, m, spp, depth, seed, rgb,
@@ -1308,19 +1341,23 @@ hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w,
         }
         const bool lds = env_lds != 0 && sc.x_lds_bytes > 0;
         const size_t lds_bytes = lds ? (size_t)sc.x_lds_bytes : 0;
-        static int resident_blocks[2] = {0, 0};
-        static size_t resident_lds[2] = {0, 0};
-        if (resident_blocks[lds] == 0 || resident_lds[lds] != lds_bytes) {
+        const int w4 = (lds && sc.x_waves4) ? 1 : 0;
+        const int kv = 2 * (int)lds + w4;   // kernel variant
+        static int resident_blocks[4] = {0, 0, 0, 0};
+        static size_t resident_lds[4] = {0, 0, 0, 0};
+        if (resident_blocks[kv] == 0 || resident_lds[kv] != lds_bytes) {
             int dev = 0, cus = 0, per_cu = 0;
             (void)hipGetDevice(&dev);
             (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
             (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &per_cu, lds ? reinterpret_cast<const void*>(k_mode_x<false, true>) : reinterpret_cast<const void*>(k_mode_x<false, false>),
+                &per_cu, kv == 3 ? reinterpret_cast<const void*>(k_mode_x<false, true, true>)
+                         : kv == 2 ? reinterpret_cast<const void*>(k_mode_x<false, true, false>)
+                                   : reinterpret_cast<const void*>(k_mode_x<false, false, false>),
                 64 * kWavesPerBlock, lds_bytes);
-            resident_blocks[lds] = std::max(1, cus) * std::max(1, per_cu);
-            resident_lds[lds] = lds_bytes;
+            resident_blocks[kv] = std::max(1, cus) * std::max(1, per_cu);
+            resident_lds[kv] = lds_bytes;
         }
-        const int resident = resident_blocks[lds];
+        const int resident = resident_blocks[kv];
         const long long n_slots = m.n_local * (kTile * kTile);
         const long long want = (n_slots * std::min(o.spp, GI_X_MAX_RUN) / 64 + kWavesPerBlock - 1) / kWavesPerBlock;
         const dim3 pgrid((unsigned)std::max<long long>(1, std::min<long long>(want, resident)));
@@ -1350,12 +1387,12 @@ hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w,
             env_xf = v ? std::atoi(v) : -1;
         }
         const int xf = env_xf >= 0 ? env_xf : sc.x_flags;
-#define GI_LAUNCH_X(S, L) hipLaunchKernelGGL((k_mode_x<S, L>), pgrid, block, lds_bytes, stream, sc, cam, light, m, o.spp, \
+#define GI_LAUNCH_X(S, L, W) hipLaunchKernelGGL((k_mode_x<S, L, W>), pgrid, block, lds_bytes, stream, sc, cam, light, m, o.spp, \
                                            o.depth, o.seed, rgb, rgb8, st, wk, h8, xf)
         if (stats) {
-            if (lds) GI_LAUNCH_X(true, true); else GI_LAUNCH_X(true, false);
+            if (kv == 3) GI_LAUNCH_X(true, true, true); else if (kv == 2) GI_LAUNCH_X(true, true, false); else GI_LAUNCH_X(true, false, false);
         } else {
-            if (lds) GI_LAUNCH_X(false, true); else GI_LAUNCH_X(false, false);
+            if (kv == 3) GI_LAUNCH_X(false, true, true); else if (kv == 2) GI_LAUNCH_X(false, true, false); else GI_LAUNCH_X(false, false, false);
         }
 #undef GI_LAUNCH_X
         if (o.spp > 1) hipLaunchKernelGGL(k_x_reduce, sgrid, dim3(256), 0, stream, m, wk, o.spp, rgb, rgb8);

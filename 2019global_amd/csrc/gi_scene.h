@@ -157,6 +157,7 @@ struct DevScene {
     int32_t x_flags;       // Mode X schedule flags: bit 0 = continue paths from shadow rays in traversal
     int32_t n_xhot;
     int32_t x_lds_bytes;   // > 0: xwnodes + xhot fit in LDS and are staged there by each workgroup
+    int32_t x_waves4;      // LDS-resident scene with light shading: k_mode_x at 4 waves per SIMD
     float root_lo[3], root_hi[3];   // Mode X: union of the root's fp32 child boxes (conservative)
     // Mode R candidate reconstruction (HostScene fields of the same names)
     const int32_t* app_off;
