@@ -689,6 +689,9 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 #ifndef GI_X_START_BURST
 #define GI_X_START_BURST 16   // primary rays a lane may resolve by the root test per handler run
 #endif
+#ifndef GI_X_TRAV_UNROLL
+#define GI_X_TRAV_UNROLL 1   // traversal steps per loop iteration
+#endif
 #ifndef GI_X_PAIR
 #define GI_X_PAIR 1   // LDS-resident scenes: leaf records tested two at a time (interleaved fp64 chains)
 #endif
@@ -757,7 +760,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     if (lane == 0) blk_meta[0] = 64u;
     __builtin_amdgcn_wave_barrier();
     const bool inline_shadow = (xflags & 1) != 0;
-    uint32_t nnode = 0, nprim = 0, nrays = 0, nbox = 0, npx = 0;
+    uint32_t nnode = 0, nprim = 0, nrays = 0, nbox = 0, npx = 0, nsteps = 0;
     long long idx = -1;
     int x = 0, y = 0;
     uint64_t key = 0;
@@ -794,7 +797,6 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             const unsigned long long m_hs = __ballot(handle && phase == PH_SHADOW);
             if (lane == 0) {
                 ++cnt.iters;
-                cnt.trav += __popcll(m_trav);
                 if (m_h) {
                     ++cnt.handle;
                     cnt.hlanes += __popcll(m_h);
@@ -805,6 +807,12 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
         }
         const uint64_t t0 = STATS ? clock64() : 0;
         if (trav) {
+            // up to GI_X_TRAV_UNROLL steps per loop iteration: the scheduling ballots and the handler
+            // decision are paid once per iteration (a lane whose ray ends stops stepping)
+#pragma unroll 1
+            for (int u = 0; u < GI_X_TRAV_UNROLL; ++u) {
+            if (u > 0 && !raying) break;
+            if (STATS) ++nsteps;
             // ---- one traversal step (stackless: 8-bit "children left" mask per level).  Invariant:
             // the current level has a child left; the step pops it, then climbs past exhausted
             // levels, so a ray ends in the step that exhausts the root level (no empty iteration).
@@ -908,6 +916,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 mlo = mhi = 0;
                 lvl_set(mlo, mhi, 0, rm);
                 raying = rm != 0;
+            }
             }
         }
         const uint64_t t1 = STATS ? clock64() : 0;
@@ -1120,6 +1129,11 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
         }
     }
     if (STATS) cnt.cyc_all += clock64() - t_begin;
+    if (STATS) {   // lane traversal steps, summed over the wave into lane 0
+        uint64_t ns = nsteps;
+        for (int off = 32; off > 0; off >>= 1) ns += __shfl_xor(ns, off);
+        cnt.trav += ns;
+    }
     cnt.rays += nrays;
     cnt.nodes += nnode;
     cnt.prims += nprim;
