@@ -1,8 +1,9 @@
 // gi_kernels.hip — gfx950 (CDNA4) kernels for the per-pixel radiance path.
 //
-// Work decomposition: one wave64 renders one 8x8 pixel tile (lane = pixel), four waves per
-// 256-thread workgroup.  Tiles are dealt round-robin over shard ranks (tile t belongs to rank
-// t % shard_count), so the same kernel serves 1 GPU and N-GPU tile sharding.
+// Work decomposition: 8x8 pixel tiles dealt round-robin over shard ranks (tile t belongs to rank
+// t % shard_count), so the same kernels serve 1 GPU and N-GPU tile sharding; four waves per
+// 256-thread workgroup.  Mode R: one wave64 per tile (lane = pixel).  Mode X: persistent waves
+// taking (pixel, run of samples) units from a device work list.
 //
 // Mode R (reference semantics):
 //   The reference builds the full candidate list of Octree::intersect (octree.h:233-256, DFS over
