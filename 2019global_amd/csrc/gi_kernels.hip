@@ -690,6 +690,9 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 #ifndef GI_X_START_BURST
 #define GI_X_START_BURST 16   // primary rays a lane may resolve by the root test per handler run
 #endif
+#ifndef GI_X_PSL
+#define GI_X_PSL 1   // 4-wave LDS kernel: path values carried across the shadow ray kept in LDS
+#endif
 #ifndef GI_X_TRAV_UNROLL
 #define GI_X_TRAV_UNROLL 1   // traversal steps per loop iteration
 #endif
@@ -737,8 +740,8 @@ struct XWork {
 #define GI_X_MAX_RUN 8          // largest run length k (samples per unit)
 #endif
 
-template <bool STATS, bool PAIR, typename NodeP, typename HotP, typename PrimP, typename EntP>
-__device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H, PrimP XP, EntP EN,
+template <bool STATS, bool PAIR, bool PSL, typename NodeP, typename HotP, typename PrimP, typename EntP>
+__device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H, PrimP XP, EntP EN, double* ps,
                                             const CamDev& cam, V3 light,
                                             const TileMap& m, int spp, int depth, uint64_t seed, double* rgb,
                                             uint8_t* rgb8, unsigned* blk_list, const XWork& wk, int handle8,
@@ -899,8 +902,8 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             // for long ones the extra divergent root test costs more than it saves)
             if (inline_shadow && !raying && phase == PH_SHADOW && has_next) {
                 ++nrays;
-                if (best >= 0) Lv = Lo;   // occluded: ambient term only
-                d = nextd;                // o is still the hit point
+                if (best >= 0) Lv = PSL ? v3(ps[0], ps[1], ps[2]) : Lo;   // occluded: ambient term only
+                d = PSL ? v3(ps[3], ps[4], ps[5]) : nextd;                // o is still the hit point
                 ++b;
                 phase = PH_CLOSEST;
                 tmax = INFINITY;
@@ -948,6 +951,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     const V3 ls = v3(spw, spw, spw) * e.shader[2];
                     const V3 lo = (la + ldf) + ls;
                     Lo = Lv + vmul(T, v3(smin(la.x, 1.0), smin(la.y, 1.0), smin(la.z, 1.0)));
+                    if (PSL) { ps[0] = Lo.x; ps[1] = Lo.y; ps[2] = Lo.z; }
                     Lv = Lv + vmul(T, v3(smin(lo.x, 1.0), smin(lo.y, 1.0), smin(lo.z, 1.0)));
                     has_next = false;
                     if (b != depth - 1) {
@@ -963,6 +967,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                             const V3 t1 = v3(1.0 + sg * N.x * N.x * aa, sg * bb, -sg * N.x);
                             const V3 t2 = v3(bb, sg + N.y * N.y * aa, -N.y);
                             nextd = normalize((t1 * sx + t2 * sy) + N * sz);
+                            if (PSL) { ps[3] = nextd.x; ps[4] = nextd.y; ps[5] = nextd.z; }
                             has_next = true;
                         }
                     }
@@ -976,11 +981,11 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 }
             } else if (phase == PH_SHADOW) {
                 ++nrays;
-                if (best >= 0) Lv = Lo;   // occluded: ambient term only
+                if (best >= 0) Lv = PSL ? v3(ps[0], ps[1], ps[2]) : Lo;   // occluded: ambient term only
                 if (!has_next) {
                     end_path = true;
                 } else {
-                    d = nextd;   // o is still the hit point
+                    d = PSL ? v3(ps[3], ps[4], ps[5]) : nextd;   // o is still the hit point
                     ++b;
                     phase = PH_CLOSEST;
                     tmax = INFINITY;
@@ -1179,11 +1184,14 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
         const XHot* H = reinterpret_cast<const XHot*>(lds_scene + nw);
         const XPrim* XP = reinterpret_cast<const XPrim*>(lds_scene + nw + nh);
         const REnt* EN = reinterpret_cast<const REnt*>(lds_scene + nw + nh + np);
-        mode_x_wave<STATS, GI_X_PAIR != 0>(sc, W, H, XP, EN, cam, light, m, spp, depth, seed, rgb, rgb8, blk, wk, handle8,
-                                 xflags, c);
+        // 4-wave kernel: the values a path carries across its shadow ray (the occluded sum, the next
+        // direction) live in a per-lane LDS slot after the scene instead of in VGPRs / scratch
+        double* ps = reinterpret_cast<double*>(lds_scene + nw + nh + np + ne) + 6 * threadIdx.x;
+        mode_x_wave<STATS, GI_X_PAIR != 0, W4 && GI_X_PSL>(sc, W, H, XP, EN, ps, cam, light, m, spp, depth, seed, rgb,
+                                                          rgb8, blk, wk, handle8, xflags, c);
     } else {
-        mode_x_wave<STATS, false>(sc, sc.xwnodes, sc.xhot, sc.xprims, sc.ents, cam, light, m, spp, depth, seed, rgb,
-                                  rgb8, blk, wk, handle8, xflags, c);
+        mode_x_wave<STATS, false, false>(sc, sc.xwnodes, sc.xhot, sc.xprims, sc.ents, nullptr, cam, light, m, spp, depth,
+                                         seed, rgb, rgb8, blk, wk, handle8, xflags, c);
     }
     if (STATS) {
         if ((threadIdx.x & 63) == 0) {
@@ -1355,7 +1363,7 @@ hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w,
             env_lds = v ? std::atoi(v) : 1;
         }
         const bool lds = env_lds != 0 && sc.x_lds_bytes > 0;
-        const size_t lds_bytes = lds ? (size_t)sc.x_lds_bytes : 0;
+        const size_t lds_bytes = lds ? (size_t)sc.x_lds_bytes + ((sc.x_waves4 && GI_X_PSL) ? 256 * 6 * sizeof(double) : 0) : 0;
         const int w4 = (lds && sc.x_waves4) ? 1 : 0;
         const int kv = 2 * (int)lds + w4;   // kernel variant
         static int resident_blocks[4] = {0, 0, 0, 0};
