@@ -61,7 +61,7 @@ def build(verbose: bool = False, force: bool = False, variant: str = "", hip_def
         src = os.path.join(CSRC, s)
         obj = os.path.join(objdir, s + (f".{variant}" if variant else "") + ".o")
         if force or _stale(obj, [src] + hdrs):
-            _run([hipcc, f"--offload-arch={ARCH}", "-O3", *COMMON, *[f"-D{d}" for d in hip_defines],
+            _run([hipcc, f"--offload-arch={ARCH}", "-O3", "-Wshadow", *COMMON, *[f"-D{d}" for d in hip_defines],
                   "-munsafe-fp-atomics", "-c", src, "-o", obj], verbose)
         objs.append(obj)
     if force or _stale(out, objs):

@@ -741,7 +741,7 @@ struct XWork {
 #endif
 
 template <bool STATS, bool PAIR, bool PSL, typename NodeP, typename HotP, typename PrimP, typename EntP>
-__device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H, PrimP XP, EntP EN, double* ps,
+__device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H, PrimP XP, EntP EN, double* pslot,
                                             const CamDev& cam, V3 light,
                                             const TileMap& m, int spp, int depth, uint64_t seed, double* rgb,
                                             uint8_t* rgb8, unsigned* blk_list, const XWork& wk, int handle8,
@@ -821,9 +821,9 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             // the current level has a child left; the step pops it, then climbs past exhausted
             // levels, so a ray ends in the step that exhausts the root level (no empty iteration).
             const uint32_t msk = lvl_get(mlo, mhi, level);
-            const int k = __builtin_ctz(msk);          // next child in front-to-back order
+            const int kc = __builtin_ctz(msk);         // next child in front-to-back order
             lvl_set(mlo, mhi, level, msk & (msk - 1));
-            const int c = k ^ dmask;
+            const int c = kc ^ dmask;
             const XWNode* nd = W + node;
             const int ch = nd->child[c];
             // a closer hit may have arrived since the mask was computed: re-cull this child
@@ -855,22 +855,22 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     for (int j = 0; j < cntl; j += 2) {
                         const bool two = j + 1 < cntl;
                         const XHotR r0 = load_hot(hp + j), r1 = load_hot(hp + (two ? j + 1 : j));
-                        const double t0 = x_prim_t(r0.h, o, d, MX_TMIN);
-                        const double t1 = two ? x_prim_t(r1.h, o, d, MX_TMIN) : INFINITY;
+                        const double ta = x_prim_t(r0.h, o, d, MX_TMIN);
+                        const double tb = two ? x_prim_t(r1.h, o, d, MX_TMIN) : INFINITY;
                         nprim += two ? 2 : 1;
                         if (phase == PH_SHADOW) {
-                            if (t0 < tmax || t1 < tmax) {   // any hit occludes
-                                best = t0 < tmax ? r0.h.prim : r1.h.prim;
+                            if (ta < tmax || tb < tmax) {   // any hit occludes
+                                best = ta < tmax ? r0.h.prim : r1.h.prim;
                                 raying = false;
                                 break;
                             }
                         } else {
-                            if (t0 < tbest || (t0 == tbest && r0.h.prim < best)) {
-                                tbest = t0;
+                            if (ta < tbest || (ta == tbest && r0.h.prim < best)) {
+                                tbest = ta;
                                 best = r0.h.prim;
                             }
-                            if (t1 < tbest || (t1 == tbest && r1.h.prim < best)) {
-                                tbest = t1;
+                            if (tb < tbest || (tb == tbest && r1.h.prim < best)) {
+                                tbest = tb;
                                 best = r1.h.prim;
                             }
                             tbest_f = up32(tbest);
@@ -902,8 +902,8 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             // for long ones the extra divergent root test costs more than it saves)
             if (inline_shadow && !raying && phase == PH_SHADOW && has_next) {
                 ++nrays;
-                if (best >= 0) Lv = PSL ? v3(ps[0], ps[1], ps[2]) : Lo;   // occluded: ambient term only
-                d = PSL ? v3(ps[3], ps[4], ps[5]) : nextd;                // o is still the hit point
+                if (best >= 0) Lv = PSL ? v3(pslot[0], pslot[1], pslot[2]) : Lo;   // occluded: ambient term only
+                d = PSL ? v3(pslot[3], pslot[4], pslot[5]) : nextd;                // o is still the hit point
                 ++b;
                 phase = PH_CLOSEST;
                 tmax = INFINITY;
@@ -950,24 +950,27 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     const double spw = mx_powi(smax(0.0, dot(N, bis)), (int)e.spec_pow);
                     const V3 ls = v3(spw, spw, spw) * e.shader[2];
                     const V3 lo = (la + ldf) + ls;
+                    if (PSL) T = v3(pslot[6], pslot[7], pslot[8]);
                     Lo = Lv + vmul(T, v3(smin(la.x, 1.0), smin(la.y, 1.0), smin(la.z, 1.0)));
-                    if (PSL) { ps[0] = Lo.x; ps[1] = Lo.y; ps[2] = Lo.z; }
+                    if (PSL) { pslot[0] = Lo.x; pslot[1] = Lo.y; pslot[2] = Lo.z; }
                     Lv = Lv + vmul(T, v3(smin(lo.x, 1.0), smin(lo.y, 1.0), smin(lo.z, 1.0)));
                     has_next = false;
                     if (b != depth - 1) {
                         const V3 Tn = vmul(T, tc * 0.5);
                         T = Tn;
+                        if (PSL) { pslot[6] = Tn.x; pslot[7] = Tn.y; pslot[8] = Tn.z; }
                         if (!(Tn.x == 0.0 && Tn.y == 0.0 && Tn.z == 0.0)) {
                             double sx, sy, r2;   // cosine-weighted: concentric disk + Malley
-                            mx_disk(mx_u01k(key, smp, b, 2), mx_u01k(key, smp, b, 3), sx, sy, r2);
+                            const uint64_t kk = PSL ? reinterpret_cast<const uint64_t*>(pslot)[9] : key;
+                            mx_disk(mx_u01k(kk, smp, b, 2), mx_u01k(kk, smp, b, 3), sx, sy, r2);
                             const double sz = gsqrt(1.0 - r2);
                             const double sg = N.z >= 0.0 ? 1.0 : -1.0;
                             const double aa = -1.0 / (sg + N.z);
                             const double bb = N.x * N.y * aa;
-                            const V3 t1 = v3(1.0 + sg * N.x * N.x * aa, sg * bb, -sg * N.x);
-                            const V3 t2 = v3(bb, sg + N.y * N.y * aa, -N.y);
-                            nextd = normalize((t1 * sx + t2 * sy) + N * sz);
-                            if (PSL) { ps[3] = nextd.x; ps[4] = nextd.y; ps[5] = nextd.z; }
+                            const V3 bt1 = v3(1.0 + sg * N.x * N.x * aa, sg * bb, -sg * N.x);
+                            const V3 bt2 = v3(bb, sg + N.y * N.y * aa, -N.y);
+                            nextd = normalize((bt1 * sx + bt2 * sy) + N * sz);
+                            if (PSL) { pslot[3] = nextd.x; pslot[4] = nextd.y; pslot[5] = nextd.z; }
                             has_next = true;
                         }
                     }
@@ -981,11 +984,11 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 }
             } else if (phase == PH_SHADOW) {
                 ++nrays;
-                if (best >= 0) Lv = PSL ? v3(ps[0], ps[1], ps[2]) : Lo;   // occluded: ambient term only
+                if (best >= 0) Lv = PSL ? v3(pslot[0], pslot[1], pslot[2]) : Lo;   // occluded: ambient term only
                 if (!has_next) {
                     end_path = true;
                 } else {
-                    d = PSL ? v3(ps[3], ps[4], ps[5]) : nextd;   // o is still the hit point
+                    d = PSL ? v3(pslot[3], pslot[4], pslot[5]) : nextd;   // o is still the hit point
                     ++b;
                     phase = PH_CLOSEST;
                     tmax = INFINITY;
@@ -1069,6 +1072,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                             y += m.y0;
                             if (spp > 1) idx = (long long)i;        // per-sample radiance row
                             key = mx_key(seed, (uint64_t)y * (uint64_t)m.w + (uint64_t)x);
+                            if (PSL) reinterpret_cast<uint64_t*>(pslot)[9] = key;
                             smp = (int)c * k;
                             phase = PH_START;
                             if (c == 0) ++npx;
@@ -1079,7 +1083,11 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 if (phase == PH_DEAD) break;
                 if (phase == PH_START) {
                     double jx = 0.0, jy = 0.0;
-                    if (spp > 1) { jx = mx_u01k(key, smp, 0xFFFF, 0); jy = mx_u01k(key, smp, 0xFFFF, 1); }
+                    if (spp > 1) {
+                        const uint64_t kk = PSL ? reinterpret_cast<const uint64_t*>(pslot)[9] : key;
+                        jx = mx_u01k(kk, smp, 0xFFFF, 0);
+                        jy = mx_u01k(kk, smp, 0xFFFF, 1);
+                    }
                     const V3 d0 = primary_dir(cam, (double)x + jx, (double)y + jy);
                     if (burst < GI_X_START_BURST) {
                         // conservative fp32 test of the scene's root box on the unnormalised
@@ -1105,6 +1113,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     d = normalize(d0);
                     Lv = v3(0, 0, 0);
                     T = v3(1, 1, 1);
+                    if (PSL) { pslot[6] = 1.0; pslot[7] = 1.0; pslot[8] = 1.0; }
                     b = 0;
                     tmax = INFINITY;
                     tbest = INFINITY;
@@ -1184,10 +1193,11 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
         const XHot* H = reinterpret_cast<const XHot*>(lds_scene + nw);
         const XPrim* XP = reinterpret_cast<const XPrim*>(lds_scene + nw + nh);
         const REnt* EN = reinterpret_cast<const REnt*>(lds_scene + nw + nh + np);
-        // 4-wave kernel: the values a path carries across its shadow ray (the occluded sum, the next
-        // direction) live in a per-lane LDS slot after the scene instead of in VGPRs / scratch
-        double* ps = reinterpret_cast<double*>(lds_scene + nw + nh + np + ne) + 6 * threadIdx.x;
-        mode_x_wave<STATS, GI_X_PAIR != 0, W4 && GI_X_PSL>(sc, W, H, XP, EN, ps, cam, light, m, spp, depth, seed, rgb,
+        // 4-wave kernel: path values used only by the shading handler and at the shadow ray's end
+        // (occluded sum, next direction, throughput T, RNG key) live in a per-lane LDS slot after
+        // the scene instead of in VGPRs / scratch
+        double* pslot = reinterpret_cast<double*>(lds_scene + nw + nh + np + ne) + 10 * threadIdx.x;
+        mode_x_wave<STATS, GI_X_PAIR != 0, W4 && GI_X_PSL>(sc, W, H, XP, EN, pslot, cam, light, m, spp, depth, seed, rgb,
                                                           rgb8, blk, wk, handle8, xflags, c);
     } else {
         mode_x_wave<STATS, false, false>(sc, sc.xwnodes, sc.xhot, sc.xprims, sc.ents, nullptr, cam, light, m, spp, depth,
@@ -1363,7 +1373,7 @@ hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w,
             env_lds = v ? std::atoi(v) : 1;
         }
         const bool lds = env_lds != 0 && sc.x_lds_bytes > 0;
-        const size_t lds_bytes = lds ? (size_t)sc.x_lds_bytes + ((sc.x_waves4 && GI_X_PSL) ? 256 * 6 * sizeof(double) : 0) : 0;
+        const size_t lds_bytes = lds ? (size_t)sc.x_lds_bytes + ((sc.x_waves4 && GI_X_PSL) ? 256 * 10 * sizeof(double) : 0) : 0;
         const int w4 = (lds && sc.x_waves4) ? 1 : 0;
         const int kv = 2 * (int)lds + w4;   // kernel variant
         static int resident_blocks[4] = {0, 0, 0, 0};
