@@ -268,7 +268,10 @@ def main():
             "data": "synthetic (procedural scene, no external data)",
             "config": {"workload": f"{args.workload}: {desc}", "mode": "X" if mode == 1 else "R", "width": w,
                        "height": h, "spp": spp, "depth": depth, "seed": args.seed,
-                       "rays_per_frame": rays_frame, "parallelism": f"tile-shard{world}"},
+                       "rays_per_frame": rays_frame, "primary_rays_per_frame": w * h * spp,
+                       "parallelism": f"tile-shard{world}"},
+            # primary (w*h*spp) and total (primary + bounce + shadow) rays per second
+            "mray_s_primary": round(w * h * spp * args.steps / elapsed / 1e6, 3),
             "roofline": {"bound": "hbm", "kernel": "k_mode_x" if mode == 1 else "k_mode_r",
                          "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
