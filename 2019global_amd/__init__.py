@@ -43,12 +43,13 @@ LIB_PATH = os.environ.get("GI_LIB") or os.path.join(HERE, "libgi.so")   # GI_LIB
 MODE_R, MODE_X = 0, 1
 FLAG_STATS = 1
 FLAG_R_DFS = 2   # Mode R: reverse-DFS over the whole reference octree (A/B against the default)
+FLAG_TIME = 4    # HIP events around the dominant kernel; read with DeviceScene.kernel_ms()
 STAT_RAYS, STAT_NODES, STAT_PRIMS, STAT_PIXELS, STAT_PBOX = 0, 1, 2, 3, 4
 STAT_X_ITERS, STAT_X_TRAV, STAT_X_HANDLE, STAT_X_HLANES, STAT_X_HCLOSE, STAT_X_HSHADOW = 5, 6, 7, 8, 9, 10
 STAT_X_CYC_TRAV, STAT_X_CYC_HIT, STAT_X_CYC_NEXT, STAT_X_CYC_ALL = 11, 12, 13, 14
 STATS_N = 16
 TILE = 8
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class GIError(RuntimeError):
@@ -95,7 +96,7 @@ TILE_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ct
 
 EXPORTS = ["gi_abi_version", "gi_last_error", "gi_camera_init", "gi_scene_create", "gi_scene_destroy",
            "gi_scene_get_info", "gi_render", "gi_render_device", "gi_shard_tiles", "gi_unshard_device",
-           "gi_trace_ray", "gi_kat_expbox"]
+           "gi_trace_ray", "gi_kat_expbox", "gi_scene_kernel_ms"]
 
 _lib = None
 _lock = threading.Lock()
@@ -131,6 +132,7 @@ def lib():
         L.gi_unshard_device.argtypes = [i32, i32, i32, vp, vp, vp, vp, vp]
         L.gi_trace_ray.argtypes = [vp, dp, dp, dp, ctypes.POINTER(Hit), dp]
         L.gi_kat_expbox.argtypes = [i32, dp, ctypes.POINTER(ctypes.c_int32)]
+        L.gi_scene_kernel_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int64)]
         if L.gi_abi_version() != ABI_VERSION:
             raise GIError(f"libgi ABI {L.gi_abi_version()} != {ABI_VERSION}")
         _lib = L
@@ -369,6 +371,13 @@ class DeviceScene:
         o = self.opts(mode, spp, depth, seed, shard_count, shard_index, stats_ptr=stats_ptr, flags=flags)
         _check(lib().gi_render_device(self._h, ctypes.byref(cam._c), _d3(light), w, h, ctypes.byref(o),
                                       d_rgb or None, d_rgb8 or None, stream or None), "gi_render_device")
+
+    def kernel_ms(self):
+        """(average ms, launches) of the dominant kernel over the renders issued with FLAG_TIME since
+        the previous call (gi_scene_kernel_ms; waits for the last one, then resets)."""
+        ms, n = ctypes.c_float(), ctypes.c_int64()
+        _check(lib().gi_scene_kernel_ms(self._h, ctypes.byref(ms), ctypes.byref(n)), "gi_scene_kernel_ms")
+        return float(ms.value), int(n.value)
 
     def trace_ray(self, origin, direction, light):
         hit = Hit()

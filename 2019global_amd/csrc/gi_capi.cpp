@@ -20,7 +20,7 @@ struct CamDev {
 bool build_host_scene(const gi_scene_desc& desc, HostScene& hs, std::string& err);
 long long shard_tiles(int w, int h, int shard_count);
 hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w, int h, int y0, const gi_opts& o,
-                         double* rgb, uint8_t* rgb8, const XScratch& xs, hipStream_t stream);
+                         double* rgb, uint8_t* rgb8, const XScratch& xs, KTimer* kt, hipStream_t stream);
 hipError_t launch_unshard(int w, int h, int shard_count, const double* packed, const uint8_t* packed8, double* rgb,
                           uint8_t* rgb8, hipStream_t stream);
 hipError_t launch_trace_ray(const DevScene& sc, V3 o, V3 d, V3 light, int32_t* out_i, double* out_d, hipStream_t stream);
@@ -34,6 +34,7 @@ struct gi_scene {
     DevScene dev;
     std::vector<void*> allocs;
     XScratch xs;   // Mode X work list + per-sample radiance, grown on demand (one render in flight per scene)
+    KTimer kt;     // GI_FLAG_TIME events
     int device = -1;
     int64_t bytes = 0;
     bool mode_x_ok = true;
@@ -116,6 +117,39 @@ int ensure_xscratch(gi_scene* s, int w, int h, const gi_opts* o) {
         if ((e = hipMalloc((void**)&x.part, (size_t)o->spp * (size_t)x.cap * 3 * sizeof(double))) != hipSuccess)
             return hip_fail(e, "hipMalloc (per-sample radiance)");
         x.spp = o->spp;
+    }
+    return GI_OK;
+}
+
+// folds ring slot i (its end event has been recorded) into the running sum
+hipError_t fold_timer(KTimer& kt, int i) {
+    hipError_t e = hipEventSynchronize(static_cast<hipEvent_t>(kt.ev1[i]));
+    float ms = 0.f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, static_cast<hipEvent_t>(kt.ev0[i]), static_cast<hipEvent_t>(kt.ev1[i]));
+    if (e == hipSuccess) { kt.sum_ms += ms; kt.folded++; }
+    return e;
+}
+
+// GI_FLAG_TIME: create the event ring on first use; fold the pair the next launch will reuse
+int ensure_timer(gi_scene* s, const gi_opts* o) {
+    if (!(o->flags & GI_FLAG_TIME)) return GI_OK;
+    KTimer& kt = s->kt;
+    if (!kt.ev0[0]) {
+        for (int i = 0; i < KTimer::kRing; i++) {
+            hipEvent_t a = nullptr, b = nullptr;
+            hipError_t e = hipEventCreate(&a);
+            if (e == hipSuccess) e = hipEventCreate(&b);
+            if (e != hipSuccess) {
+                if (a) (void)hipEventDestroy(a);
+                return hip_fail(e, "hipEventCreate");
+            }
+            kt.ev0[i] = a;
+            kt.ev1[i] = b;
+        }
+    }
+    if (kt.recorded >= KTimer::kRing) {
+        const hipError_t e = fold_timer(kt, (int)(kt.recorded % KTimer::kRing));
+        if (e != hipSuccess) return hip_fail(e, "timer event");
     }
     return GI_OK;
 }
@@ -226,6 +260,10 @@ void gi_scene_destroy(gi_scene* s) {
     for (void* p : s->allocs) (void)hipFree(p);
     (void)hipFree(s->xs.list);
     (void)hipFree(s->xs.part);
+    for (int i = 0; i < KTimer::kRing; i++) {
+        if (s->kt.ev0[i]) (void)hipEventDestroy(static_cast<hipEvent_t>(s->kt.ev0[i]));
+        if (s->kt.ev1[i]) (void)hipEventDestroy(static_cast<hipEvent_t>(s->kt.ev1[i]));
+    }
     delete s;
 }
 
@@ -253,9 +291,9 @@ int gi_render_device(gi_scene* s, const gi_camera* cam, const double light[3], i
     int rc = check_opts(s, w, h, o);
     if (rc) return rc;
     if (!cam || !light) return fail(GI_ERR_ARG, "null camera or light");
-    if ((rc = bind_device(s)) || (rc = ensure_xscratch(s, w, h, o))) return rc;
+    if ((rc = bind_device(s)) || (rc = ensure_xscratch(s, w, h, o)) || (rc = ensure_timer(s, o))) return rc;
     const hipError_t e = launch_render(s->dev, make_cam(*cam, w), v3(light[0], light[1], light[2]), w, h, 0, *o, d_rgb,
-                                       d_rgb8, s->xs, static_cast<hipStream_t>(stream));
+                                       d_rgb8, s->xs, &s->kt, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return hip_fail(e, "render launch");
     return GI_OK;
 }
@@ -290,7 +328,7 @@ int gi_render(gi_scene* s, const gi_camera* cam, const double light[3], int w, i
     for (int y0 = 0; y0 < h; y0 += band) {
         if (cancel && *cancel) { rc = fail(GI_ERR_CANCELLED, "cancelled"); break; }
         const int rows = std::min(band, h - y0);
-        e = launch_render(s->dev, cd, L, w, rows, y0, *o, d_rgb, d_rgb8, s->xs, nullptr);
+        e = launch_render(s->dev, cd, L, w, rows, y0, *o, d_rgb, d_rgb8, s->xs, nullptr, nullptr);
         if (e == hipSuccess) e = hipDeviceSynchronize();
         if (e != hipSuccess) { rc = hip_fail(e, "render"); break; }
         double* hr = rgb ? rgb + (size_t)y0 * w * 3 : scratch.data();
@@ -303,6 +341,26 @@ int gi_render(gi_scene* s, const gi_camera* cam, const double light[3], int w, i
     (void)hipFree(d_rgb);
     (void)hipFree(d_rgb8);
     return rc;
+}
+
+int gi_scene_kernel_ms(gi_scene* s, float* avg_ms, int64_t* n) {
+    if (!s || !avg_ms) return fail(GI_ERR_ARG, "null argument");
+    KTimer& kt = s->kt;
+    if (kt.recorded == 0) return fail(GI_ERR_ARG, "no render issued with GI_FLAG_TIME since the last read");
+    int rc = bind_device(s);
+    if (rc) return rc;
+    // the unfolded pairs are the last min(recorded, kRing) slots
+    const long long first = kt.recorded > KTimer::kRing ? kt.recorded - KTimer::kRing : 0;
+    for (long long r = std::max(first, kt.folded); r < kt.recorded; r++) {
+        const hipError_t e = fold_timer(kt, (int)(r % KTimer::kRing));
+        if (e != hipSuccess) return hip_fail(e, "gi_scene_kernel_ms");
+    }
+    *avg_ms = (float)(kt.sum_ms / (double)kt.folded);
+    if (n) *n = kt.folded;
+    kt.recorded = 0;
+    kt.folded = 0;
+    kt.sum_ms = 0.0;
+    return GI_OK;
 }
 
 int gi_unshard_device(int w, int h, int shard_count, const double* d_packed, const uint8_t* d_packed8, double* d_rgb,

@@ -1350,7 +1350,14 @@ TileMap make_map(int w, int h, int shard_count, int shard_index, int y0 = 0) {
 long long shard_tiles(int w, int h, int shard_count) { return make_map(w, h, shard_count, 0).n_local; }
 
 hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w, int h, int y0, const gi_opts& o,
-                         double* rgb, uint8_t* rgb8, const XScratch& xs, hipStream_t stream) {
+                         double* rgb, uint8_t* rgb8, const XScratch& xs, KTimer* kt, hipStream_t stream) {
+    // GI_FLAG_TIME: events on the launch stream around the dominant kernel only (slot chosen by
+    // the caller, gi_capi.cpp, which folds a reused pair before this call)
+    const bool timed = (o.flags & GI_FLAG_TIME) && kt && kt->ev0[0];
+    const int slot = timed ? (int)(kt->recorded % KTimer::kRing) : 0;
+    hipEvent_t ev_begin = timed ? static_cast<hipEvent_t>(kt->ev0[slot]) : nullptr;
+    hipEvent_t ev_end = timed ? static_cast<hipEvent_t>(kt->ev1[slot]) : nullptr;
+    auto mark = [&](hipEvent_t ev) { if (timed) (void)hipEventRecord(ev, stream); };
     const TileMap m = make_map(w, h, o.shard_count, o.shard_index, y0);
     if (m.n_local == 0) return hipSuccess;
     const dim3 grid((unsigned)((m.n_local + kWavesPerBlock - 1) / kWavesPerBlock)), block(64 * kWavesPerBlock);
@@ -1363,8 +1370,10 @@ hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w,
         // an octree that never split is one leaf: its list scanned backwards (first success) is
         // already the least work
         const int dfs = ((o.flags & GI_FLAG_R_DFS) || sc.n_rnodes <= 1) ? 1 : 0;
+        mark(ev_begin);
         if (stats) hipLaunchKernelGGL(k_mode_r<true>, grid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, dfs);
         else hipLaunchKernelGGL(k_mode_r<false>, grid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, dfs);
+        mark(ev_end);
     } else {
         // persistent grid: as many 4-wave blocks as can be resident, each wave pulls tiles
         static int env_lds = -1;   // GI_X_LDS=0 disables the LDS-resident scene (tuning)
@@ -1422,14 +1431,17 @@ hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w,
         const int xf = env_xf >= 0 ? env_xf : sc.x_flags;
 #define GI_LAUNCH_X(S, L, W) hipLaunchKernelGGL((k_mode_x<S, L, W>), pgrid, block, lds_bytes, stream, sc, cam, light, m, o.spp, \
                                            o.depth, o.seed, rgb, rgb8, st, wk, h8, xf)
+        mark(ev_begin);
         if (stats) {
             if (kv == 3) GI_LAUNCH_X(true, true, true); else if (kv == 2) GI_LAUNCH_X(true, true, false); else GI_LAUNCH_X(true, false, false);
         } else {
             if (kv == 3) GI_LAUNCH_X(false, true, true); else if (kv == 2) GI_LAUNCH_X(false, true, false); else GI_LAUNCH_X(false, false, false);
         }
+        mark(ev_end);
 #undef GI_LAUNCH_X
         if (o.spp > 1) hipLaunchKernelGGL(k_x_reduce, sgrid, dim3(256), 0, stream, m, wk, o.spp, rgb, rgb8);
     }
+    if (timed) kt->recorded++;
     return hipGetLastError();
 }
 

@@ -172,6 +172,18 @@ struct DevScene {
     float rc_ext;
 };
 
+// HIP events bracketing the dominant kernel of renders issued with GI_FLAG_TIME (owned by the
+// scene handle, created on first use): a ring of kRing pairs, so frames stay asynchronous; a pair
+// about to be reused is folded into the running sum first (it ended kRing frames ago).
+struct KTimer {
+    static constexpr int kRing = 64;
+    void* ev0[kRing] = {};   // hipEvent_t
+    void* ev1[kRing] = {};
+    long long recorded = 0;  // pairs recorded since the last read
+    double sum_ms = 0.0;     // folded pairs
+    long long folded = 0;
+};
+
 // Mode X per-launch work buffers, owned by the scene handle (gi_capi.cpp) and grown on demand:
 // the list of pixel slots left after the background test and, for spp > 1, every listed pixel's
 // per-sample radiance (summed in sample order by k_x_reduce).

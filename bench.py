@@ -21,7 +21,8 @@ deterministic frame runs before the timed region.
 roofline: the dominant kernel (k_mode_x) against HBM: achieved = algorithmic bytes per launch
 (Mode X: wide-node records x 256 B + primitive records x 80 B + 27 B/pixel output; Mode R: 64 B
 nodes + 144 B triangles) /
-average launch time from HIP events on the launch stream; traffic = HBM bytes per launch from the
+average launch time of that kernel alone from HIP events recorded directly around it on the launch
+stream (GI_FLAG_TIME, read with gi_scene_kernel_ms); traffic = HBM bytes per launch from the
 committed rocprofv3 PMC summary when present (profiles/), else null.
 cpu_baseline: this repo's CPU port of the same integrator (oracle, test infrastructure), OpenMP,
 on a bounded window of the same frame; reference_cpu: the compiled reference itself (depth 1, the
@@ -202,7 +203,9 @@ def main():
     def step(i=None):
         if i is not None:
             ev0[i].record(stream)
-        dev.render_device(cam, sc.light, w, h, buf.data_ptr(), buf8.data_ptr(), sptr, **kw)
+        # timed steps: GI_FLAG_TIME adds HIP events around the dominant kernel on the same stream
+        dev.render_device(cam, sc.light, w, h, buf.data_ptr(), buf8.data_ptr(), sptr,
+                          **(kw if i is None else dict(kw, flags=kw.get("flags", 0) | gi.FLAG_TIME)))
         if i is not None:
             ev1[i].record(stream)
         if world > 1:   # one ncclGather of the packed RGB888 tiles to rank 0, then reassembly on its GPU
@@ -224,11 +227,17 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in zip(ev0, ev1)) / max(1, args.steps)
+    # device time of the whole render call (classify + dominant kernel + reduce) and of the
+    # dominant kernel alone (gi_scene_kernel_ms: the events recorded by GI_FLAG_TIME)
+    render_ms = sum(a.elapsed_time(b) for a, b in zip(ev0, ev1)) / max(1, args.steps)
+    kern_ms, kern_n = dev.kernel_ms()
+    if kern_n != args.steps:
+        raise RuntimeError(f"timed {kern_n} dominant-kernel launches, expected {args.steps}")
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
+        t = torch.tensor([elapsed, kern_ms, render_ms], dtype=torch.float64,
+                         device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = t.tolist()
+        elapsed, kern_ms, render_ms = t.tolist()
 
     frame_check = None
     if world > 1:   # after timing: the last frame's fp64 radiance too, for the check below
@@ -276,7 +285,7 @@ def main():
                          "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "alg_bytes_per_launch": int(alg),
-                         "kernel_ms": round(kern_ms, 3),
+                         "kernel_ms": round(kern_ms, 4), "render_call_ms": round(render_ms, 4),
                          "node_visits": st[gi.STAT_NODES], "prim_tests": st[gi.STAT_PRIMS],
                          "prim_box_tests": st[gi.STAT_PBOX]},
         }

@@ -16,6 +16,7 @@
  *                        multi-GPU tile sharding)
  *   gi_trace_ray         one iteration of raytracer.h:41-84 for an arbitrary ray
  *   gi_unshard_device    reassembles a frame from per-rank packed tiles after the RCCL gather
+ *   gi_scene_kernel_ms   HIP-event duration of the last timed render's dominant kernel (bench)
  *
  * Conventions: all pointers are plain C pointers; buffers are caller-owned; sizes are in elements;
  * every function returns 0 on success and a negative gi_status on error, with a thread-local
@@ -32,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GI_ABI_VERSION 2
+#define GI_ABI_VERSION 3
 
 typedef enum gi_status {
     GI_OK = 0,
@@ -87,6 +88,8 @@ typedef enum gi_mode {
 #define GI_FLAG_STATS 1u   /* accumulate work counters into opts->stats (device pointer) */
 #define GI_FLAG_R_DFS 2u   /* Mode R: walk the whole reference octree in reverse DFS order instead of
                               reconstructing the candidate list (same result; A/B and tests) */
+#define GI_FLAG_TIME 4u    /* record HIP events around the frame's dominant kernel (k_mode_r / k_mode_x)
+                              on the render's stream; averaged by gi_scene_kernel_ms */
 
 typedef struct gi_opts {
     int32_t mode;          /* gi_mode */
@@ -178,6 +181,11 @@ int gi_unshard_device(int w, int h, int shard_count, const double* d_packed, con
  * Ray ctor normalises it), light.  rgb receives the shaded colour (0 if no hit). */
 int gi_trace_ray(gi_scene* scene, const double origin[3], const double dir[3], const double light[3],
                  gi_hit* hit, double rgb[3]);
+
+/* Average duration in ms of the dominant kernel over the scene's renders issued with GI_FLAG_TIME
+ * since the previous call (waits for the last one; *n = how many, may be NULL), then resets.
+ * GI_ERR_ARG if there was none. */
+int gi_scene_kernel_ms(gi_scene* scene, float* avg_ms, int64_t* n);
 
 /* Known-answer hook: the device's ExpBox node test (entities.h:379-440 as octree.h:242-247 uses
  * it) over n host records (min[3], max[3], origin[3], dir[3]); out[i] = 0/1. */

@@ -297,6 +297,35 @@ def test_stats_counters(torch_cuda):
     assert 0 < s[gi.STAT_NODES] <= int(z["nnode"].sum())
 
 
+def test_kernel_timer_ring(torch_cuda):
+    # GI_FLAG_TIME (bench's kernel_ms): more timed frames than the 64-pair event ring, the average
+    # covers every one, never exceeds the whole render call, and the timed frame is the same frame
+    torch = torch_cuda
+    sc = S.cornell_scene()
+    d = dev_scene("cornell")
+    w, h = 96, 64
+    kw = dict(mode=gi.MODE_X, spp=4, depth=3, seed=5)
+    ref = torch.zeros(w * h * 3, dtype=torch.float64, device="cuda")
+    d.render_device(cam_of(sc), sc.light, w, h, ref.data_ptr(), **kw)
+    buf = torch.zeros_like(ref)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = 70
+    e0.record()
+    for _ in range(n):
+        d.render_device(cam_of(sc), sc.light, w, h, buf.data_ptr(), flags=gi.FLAG_TIME, **kw)
+    e1.record()
+    ms, cnt = d.kernel_ms()
+    torch.cuda.synchronize()
+    assert cnt == n
+    assert 0.0 < ms <= e0.elapsed_time(e1) / n * 1.05
+    assert torch.equal(buf.view(torch.int64), ref.view(torch.int64))
+    with pytest.raises(gi.GIError):   # read resets: nothing timed since
+        d.kernel_ms()
+    d.render_device(cam_of(sc), sc.light, w, h, buf.data_ptr(), flags=gi.FLAG_TIME)   # Mode R
+    ms_r, cnt_r = d.kernel_ms()
+    assert cnt_r == 1 and ms_r > 0.0
+
+
 def test_soup100k_full_frame_properties(torch_cuda):
     # C4 at full 1920x1080: the golden window sample above pins values; here the whole frame is
     # rendered and checked for size-independent properties: sharding invariance and determinism.
