@@ -203,9 +203,10 @@ def main():
     def step(i=None):
         if i is not None:
             ev0[i].record(stream)
-        # timed steps: GI_FLAG_TIME adds HIP events around the dominant kernel on the same stream
+        # GI_FLAG_TIME adds HIP events around the dominant kernel on the same stream (warmup steps
+        # too: the event ring is created on first use, outside the timed region)
         dev.render_device(cam, sc.light, w, h, buf.data_ptr(), buf8.data_ptr(), sptr,
-                          **(kw if i is None else dict(kw, flags=kw.get("flags", 0) | gi.FLAG_TIME)))
+                          **dict(kw, flags=kw.get("flags", 0) | gi.FLAG_TIME))
         if i is not None:
             ev1[i].record(stream)
         if world > 1:   # one ncclGather of the packed RGB888 tiles to rank 0, then reassembly on its GPU
@@ -216,6 +217,8 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    if args.warmup:
+        dev.kernel_ms()   # drops the warmup launches' timings
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
