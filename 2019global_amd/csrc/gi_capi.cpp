@@ -29,12 +29,29 @@ hipError_t launch_box_kat(int n, const double* recs, int32_t* out, hipStream_t s
 
 using namespace gi;
 
+// gi_render's band pipeline, owned by the scene handle and created on first use: band i renders
+// into device slot i % 2 on `render` while band i-1 is copied to pinned staging on `copy`; the
+// host then copies a finished band into the caller's buffers (or hands the staging to the
+// callback).  Slots are reused only after their copy has completed (event `copied`).
+struct HostPath {
+    static constexpr int kSlots = 2;
+    hipStream_t render = nullptr, copy = nullptr;
+    hipEvent_t rendered[kSlots] = {}, copied[kSlots] = {};
+    double* d_rgb[kSlots] = {};
+    uint8_t* d_rgb8[kSlots] = {};
+    double* h_rgb[kSlots] = {};    // pinned
+    uint8_t* h_rgb8[kSlots] = {};  // pinned
+    size_t cap_px = 0;             // pixels per slot
+    int n_alloc = 0;               // slots allocated (1 for whole-frame renders)
+};
+
 struct gi_scene {
     HostScene host;
     DevScene dev;
     std::vector<void*> allocs;
     XScratch xs;   // Mode X work list + per-sample radiance, grown on demand (one render in flight per scene)
     KTimer kt;     // GI_FLAG_TIME events
+    HostPath hp;   // gi_render's band pipeline (streams, device band slots, pinned staging)
     int device = -1;
     int64_t bytes = 0;
     bool mode_x_ok = true;
@@ -154,6 +171,53 @@ int ensure_timer(gi_scene* s, const gi_opts* o) {
     return GI_OK;
 }
 
+void free_hostpath_buffers(HostPath& hp) {
+    for (int i = 0; i < HostPath::kSlots; i++) {
+        (void)hipFree(hp.d_rgb[i]);
+        (void)hipFree(hp.d_rgb8[i]);
+        (void)hipHostFree(hp.h_rgb[i]);
+        (void)hipHostFree(hp.h_rgb8[i]);
+        hp.d_rgb[i] = nullptr;
+        hp.d_rgb8[i] = nullptr;
+        hp.h_rgb[i] = nullptr;
+        hp.h_rgb8[i] = nullptr;
+    }
+    hp.cap_px = 0;
+    hp.n_alloc = 0;
+}
+
+// streams and events on first use; `slots` band slots of `px` pixels (grown, never shrunk)
+int ensure_hostpath(gi_scene* s, size_t px, int slots) {
+    HostPath& hp = s->hp;
+    hipError_t e = hipSuccess;
+    if (!hp.render) {
+        if ((e = hipStreamCreateWithFlags(&hp.render, hipStreamNonBlocking)) != hipSuccess) return hip_fail(e, "hipStreamCreate");
+        if ((e = hipStreamCreateWithFlags(&hp.copy, hipStreamNonBlocking)) != hipSuccess) return hip_fail(e, "hipStreamCreate");
+        for (int i = 0; i < HostPath::kSlots; i++) {
+            if ((e = hipEventCreateWithFlags(&hp.rendered[i], hipEventDisableTiming)) != hipSuccess ||
+                (e = hipEventCreateWithFlags(&hp.copied[i], hipEventDisableTiming)) != hipSuccess)
+                return hip_fail(e, "hipEventCreate");
+        }
+    }
+    if (hp.cap_px < px || hp.n_alloc < slots) {
+        px = std::max(px, hp.cap_px);
+        slots = std::max(slots, hp.n_alloc);
+        free_hostpath_buffers(hp);
+        for (int i = 0; i < slots; i++) {
+            if ((e = hipMalloc((void**)&hp.d_rgb[i], px * 3 * sizeof(double))) != hipSuccess ||
+                (e = hipMalloc((void**)&hp.d_rgb8[i], px * 3)) != hipSuccess ||
+                (e = hipHostMalloc((void**)&hp.h_rgb[i], px * 3 * sizeof(double), hipHostMallocDefault)) != hipSuccess ||
+                (e = hipHostMalloc((void**)&hp.h_rgb8[i], px * 3, hipHostMallocDefault)) != hipSuccess) {
+                free_hostpath_buffers(hp);
+                return hip_fail(e, "band buffers");
+            }
+        }
+        hp.cap_px = px;
+        hp.n_alloc = slots;
+    }
+    return GI_OK;
+}
+
 int bind_device(const gi_scene* s) {
     int cur = -1;
     hipError_t e = hipGetDevice(&cur);
@@ -264,6 +328,16 @@ void gi_scene_destroy(gi_scene* s) {
         if (s->kt.ev0[i]) (void)hipEventDestroy(static_cast<hipEvent_t>(s->kt.ev0[i]));
         if (s->kt.ev1[i]) (void)hipEventDestroy(static_cast<hipEvent_t>(s->kt.ev1[i]));
     }
+    HostPath& hp = s->hp;
+    if (hp.render) (void)hipStreamSynchronize(hp.render);
+    if (hp.copy) (void)hipStreamSynchronize(hp.copy);
+    free_hostpath_buffers(hp);
+    for (int i = 0; i < HostPath::kSlots; i++) {
+        if (hp.rendered[i]) (void)hipEventDestroy(hp.rendered[i]);
+        if (hp.copied[i]) (void)hipEventDestroy(hp.copied[i]);
+    }
+    if (hp.render) (void)hipStreamDestroy(hp.render);
+    if (hp.copy) (void)hipStreamDestroy(hp.copy);
     delete s;
 }
 
@@ -311,35 +385,55 @@ int gi_render(gi_scene* s, const gi_camera* cam, const double light[3], int w, i
     band = ((band + GI_TILE - 1) / GI_TILE) * GI_TILE;
     band = std::min(band, ((h + GI_TILE - 1) / GI_TILE) * GI_TILE);
     const size_t band_px = (size_t)w * (size_t)band;
-    if ((rc = ensure_xscratch(s, w, band, o))) return rc;
-    double* d_rgb = nullptr;
-    uint8_t* d_rgb8 = nullptr;
-    hipError_t e;
-    if ((e = hipMalloc((void**)&d_rgb, band_px * 3 * sizeof(double))) != hipSuccess) return hip_fail(e, "hipMalloc");
-    if ((e = hipMalloc((void**)&d_rgb8, band_px * 3)) != hipSuccess) {
-        (void)hipFree(d_rgb);
-        return hip_fail(e, "hipMalloc");
-    }
-    std::vector<double> scratch(rgb ? 0 : band_px * 3);
-    std::vector<uint8_t> scratch8(rgb8 ? 0 : band_px * 3);
+    const int n_bands = (h + band - 1) / band;
+    if ((rc = ensure_xscratch(s, w, band, o)) || (rc = ensure_hostpath(s, band_px, std::min(n_bands, HostPath::kSlots))))
+        return rc;
+    HostPath& hp = s->hp;
     const CamDev cd = make_cam(*cam, w);
     const V3 L = v3(light[0], light[1], light[2]);
-    rc = GI_OK;
-    for (int y0 = 0; y0 < h; y0 += band) {
-        if (cancel && *cancel) { rc = fail(GI_ERR_CANCELLED, "cancelled"); break; }
-        const int rows = std::min(band, h - y0);
-        e = launch_render(s->dev, cd, L, w, rows, y0, *o, d_rgb, d_rgb8, s->xs, nullptr, nullptr);
-        if (e == hipSuccess) e = hipDeviceSynchronize();
-        if (e != hipSuccess) { rc = hip_fail(e, "render"); break; }
-        double* hr = rgb ? rgb + (size_t)y0 * w * 3 : scratch.data();
-        uint8_t* hr8 = rgb8 ? rgb8 + (size_t)y0 * w * 3 : scratch8.data();
+    const bool want_rgb = rgb || cb, want_rgb8 = rgb8 || cb;
+    // a whole-frame call copies straight into the caller's buffers (no staging, nothing to overlap)
+    const bool direct = n_bands == 1;
+    double* const dst_rgb = direct && rgb ? rgb : hp.h_rgb[0];
+    uint8_t* const dst_rgb8 = direct && rgb8 ? rgb8 : hp.h_rgb8[0];
+    // band i: render into slot i % 2 (after that slot's previous copy), then copy to its staging
+    auto issue = [&](int i) -> hipError_t {
+        const int k = i % HostPath::kSlots, y0 = i * band, rows = std::min(band, h - y0);
         const size_t n = (size_t)w * rows * 3;
-        if ((rgb || cb) && (e = hipMemcpy(hr, d_rgb, n * sizeof(double), hipMemcpyDeviceToHost)) != hipSuccess) { rc = hip_fail(e, "copy back"); break; }
-        if ((rgb8 || cb) && (e = hipMemcpy(hr8, d_rgb8, n, hipMemcpyDeviceToHost)) != hipSuccess) { rc = hip_fail(e, "copy back"); break; }
+        hipError_t e = hipSuccess;
+        if (i >= HostPath::kSlots) e = hipStreamWaitEvent(hp.render, hp.copied[k], 0);
+        if (e == hipSuccess) e = launch_render(s->dev, cd, L, w, rows, y0, *o, hp.d_rgb[k], hp.d_rgb8[k], s->xs, nullptr, hp.render);
+        if (e == hipSuccess) e = hipEventRecord(hp.rendered[k], hp.render);
+        if (e == hipSuccess) e = hipStreamWaitEvent(hp.copy, hp.rendered[k], 0);
+        double* const to = i == 0 ? dst_rgb : hp.h_rgb[k];
+        uint8_t* const to8 = i == 0 ? dst_rgb8 : hp.h_rgb8[k];
+        if (e == hipSuccess && want_rgb) e = hipMemcpyAsync(to, hp.d_rgb[k], n * sizeof(double), hipMemcpyDeviceToHost, hp.copy);
+        if (e == hipSuccess && want_rgb8) e = hipMemcpyAsync(to8, hp.d_rgb8[k], n, hipMemcpyDeviceToHost, hp.copy);
+        if (e == hipSuccess) e = hipEventRecord(hp.copied[k], hp.copy);
+        return e;
+    };
+    rc = GI_OK;
+    hipError_t e = hipSuccess;
+    if (cancel && *cancel) rc = fail(GI_ERR_CANCELLED, "cancelled");
+    else if ((e = issue(0)) != hipSuccess) rc = hip_fail(e, "render");
+    for (int i = 0; rc == GI_OK && i < n_bands; i++) {
+        // the next band goes to the GPU before this one is delivered; cancel is polled between bands
+        if (i + 1 < n_bands) {
+            if (cancel && *cancel) { rc = fail(GI_ERR_CANCELLED, "cancelled"); break; }
+            if ((e = issue(i + 1)) != hipSuccess) { rc = hip_fail(e, "render"); break; }
+        }
+        const int k = i % HostPath::kSlots, y0 = i * band, rows = std::min(band, h - y0);
+        const size_t n = (size_t)w * rows * 3;
+        if ((e = hipEventSynchronize(hp.copied[k])) != hipSuccess) { rc = hip_fail(e, "render"); break; }
+        const double* hr = i == 0 ? dst_rgb : hp.h_rgb[k];
+        const uint8_t* hr8 = i == 0 ? dst_rgb8 : hp.h_rgb8[k];
+        if (rgb && hr != rgb) { std::memcpy(rgb + (size_t)y0 * w * 3, hr, n * sizeof(double)); hr = rgb + (size_t)y0 * w * 3; }
+        if (rgb8 && hr8 != rgb8) { std::memcpy(rgb8 + (size_t)y0 * w * 3, hr8, n); hr8 = rgb8 + (size_t)y0 * w * 3; }
         if (cb) cb(user, y0, rows, hr8, hr);
     }
-    (void)hipFree(d_rgb);
-    (void)hipFree(d_rgb8);
+    // nothing of this call stays in flight (a cancelled or failed call drains its bands)
+    const hipError_t e1 = hipStreamSynchronize(hp.render), e2 = hipStreamSynchronize(hp.copy);
+    if (rc == GI_OK && (e1 != hipSuccess || e2 != hipSuccess)) rc = hip_fail(e1 != hipSuccess ? e1 : e2, "render");
     return rc;
 }
 

@@ -133,6 +133,25 @@ def reference_cpu(scn_text, w, h):
             "sample": f"depth 1 (the reference's only depth), every {stride}th pixel, {r['rays']} rays"}
 
 
+def host_path(dev, cam, light, w, h, mode, spp, depth, seed, reps=3):
+    """gi_render with host buffers (the drop-in RayTracer's path): render + PCIe copy-back, ms per
+    frame.  Reported beside `value`, never as it (inputs are not HBM-resident here)."""
+    import numpy as np
+    rgb = np.empty((h, w, 3), np.float64)
+    rgb8 = np.empty((h, w, 3), np.uint8)
+    res = {}
+    for name, out, band in (("rgb8", (None, rgb8), 0), ("rgb8+fp64", (rgb, rgb8), 0),
+                            ("rgb8_bands32", (None, rgb8), 32)):
+        dev.render(cam, light, w, h, mode=mode, spp=spp, depth=depth, seed=seed, band_rows=band, out=out)   # warm
+        t = time.perf_counter()
+        for _ in range(reps):
+            dev.render(cam, light, w, h, mode=mode, spp=spp, depth=depth, seed=seed, band_rows=band, out=out)
+        res[name] = round((time.perf_counter() - t) / reps * 1e3, 3)
+    return {"ms_per_frame": res, "note": "gi_render into host buffers: PCIe copy-back included (rgb8 = the "
+            "reference Image's RGB888; +fp64 radiance; bands32 = 32-row progressive bands as the drop-in "
+            "RayTracer::run uses); not `value`"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -308,6 +327,8 @@ def main():
                                "cycle_share": {k: round(st[i] / max(1, st[gi.STAT_X_CYC_ALL]), 4) for k, i in
                                                (("traverse", gi.STAT_X_CYC_TRAV), ("consume", gi.STAT_X_CYC_HIT),
                                                 ("next_ray", gi.STAT_X_CYC_NEXT))}}
+        if world == 1:
+            out["host_path"] = host_path(dev, cam, sc.light, w, h, mode, spp, depth, args.seed)
         if not args.no_cpu_baseline and world == 1:
             scn = sc.to_scn()
             out["cpu_baseline"] = cpu_baseline(scn, w, h, mode, spp, depth, args.seed)

@@ -160,6 +160,68 @@ def test_progressive_bands_equal_whole_frame(torch_cuda):
         assert U.bits_equal(ax, bx).all()
 
 
+def test_band_pipeline_outputs_and_callbacks(torch_cuda):
+    """gi_render's two-slot band pipeline: caller-owned outputs (either one alone), band callbacks
+    in row order with the final rows, slot buffers grown between calls, device path equality."""
+    import torch
+    sc = S.cornell_scene()
+    d = dev_scene("cornell")
+    cam = cam_of(sc)
+    w, h = 96, 75   # ragged last band
+    a, a8 = d.render(cam, sc.light, w, h, mode=gi.MODE_X, spp=3, depth=4, seed=5)
+    dr = torch.empty(w * h * 3, dtype=torch.float64, device="cuda")
+    dr8 = torch.empty(w * h * 3, dtype=torch.uint8, device="cuda")
+    d.render_device(cam, sc.light, w, h, dr.data_ptr(), dr8.data_ptr(), mode=gi.MODE_X, spp=3, depth=4, seed=5)
+    torch.cuda.synchronize()
+    assert U.bits_equal(a.reshape(-1), dr.cpu().numpy()).all() and (a8.reshape(-1) == dr8.cpu().numpy()).all()
+    seen = []
+
+    def cb(user, y0, rows, p8, p):
+        got8 = np.ctypeslib.as_array(p8, shape=(rows * w * 3,)).copy()
+        got = np.ctypeslib.as_array(p, shape=(rows * w * 3,)).copy()
+        seen.append((y0, rows, got, got8))
+
+    for band in (8, 16, 24, 0):
+        only8 = np.zeros((h, w, 3), np.uint8)
+        seen.clear()
+        _, r8 = d.render(cam, sc.light, w, h, mode=gi.MODE_X, spp=3, depth=4, seed=5, band_rows=band,
+                         out=(None, only8), callback=cb)
+        assert r8 is only8 and (only8 == a8).all()
+        step = band if band else 80
+        assert [s[0] for s in seen] == list(range(0, h, step))
+        assert sum(s[1] for s in seen) == h
+        for y0, rows, got, got8 in seen:   # callbacks see the final rows (fp64 staged without a caller buffer)
+            assert U.bits_equal(got, a[y0:y0 + rows].reshape(-1)).all()
+            assert (got8 == a8[y0:y0 + rows].reshape(-1)).all()
+        onlyf = np.zeros((h, w, 3), np.float64)
+        rf, _ = d.render(cam, sc.light, w, h, mode=gi.MODE_X, spp=3, depth=4, seed=5, band_rows=band, out=(onlyf, None))
+        assert rf is onlyf and U.bits_equal(onlyf, a).all()
+    big, big8 = d.render(cam, sc.light, 3 * w, 2 * h, band_rows=40)   # slots grow (Mode R)
+    whole, whole8 = d.render(cam, sc.light, 3 * w, 2 * h)
+    assert U.bits_equal(big, whole).all() and (big8 == whole8).all()
+
+
+def test_cancel_mid_frame_keeps_delivered_bands(torch_cuda):
+    import ctypes
+    sc = S.cornell_scene()
+    d = dev_scene("cornell")
+    cam = cam_of(sc)
+    full, full8 = d.render(cam, sc.light, 64, 64)
+    flag = ctypes.c_int(0)
+    got = []
+
+    def cb(user, y0, rows, p8, p):
+        got.append(y0)
+        flag.value = 1   # cancel after the first delivered band
+    part8 = np.zeros((64, 64, 3), np.uint8)
+    with pytest.raises(gi.GIError, match="-4"):
+        d.render(cam, sc.light, 64, 64, band_rows=8, cancel=flag, callback=cb, out=(None, part8))
+    assert got == [0]
+    assert (part8[:8] == full8[:8]).all()
+    again, again8 = d.render(cam, sc.light, 64, 64)   # the scene is usable after a cancelled call
+    assert U.bits_equal(again, full).all() and (again8 == full8).all()
+
+
 def test_cancel_before_start(torch_cuda):
     import ctypes
     sc = S.cornell_scene()
