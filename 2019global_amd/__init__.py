@@ -49,7 +49,7 @@ STAT_X_ITERS, STAT_X_TRAV, STAT_X_HANDLE, STAT_X_HLANES, STAT_X_HCLOSE, STAT_X_H
 STAT_X_CYC_TRAV, STAT_X_CYC_HIT, STAT_X_CYC_NEXT, STAT_X_CYC_ALL = 11, 12, 13, 14
 STATS_N = 16
 TILE = 8
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class GIError(RuntimeError):
@@ -60,7 +60,7 @@ class GIError(RuntimeError):
 class EntityDesc(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_int32), ("has_material", ctypes.c_int32), ("args", ctypes.c_double * 11),
                 ("mat_color", ctypes.c_double * 3), ("mat_shader", ctypes.c_double * 3),
-                ("mat_specular_power", ctypes.c_double)]
+                ("mat_specular_power", ctypes.c_double), ("mat_reflectivity", ctypes.c_double)]
 
 
 class SceneDesc(ctypes.Structure):
@@ -150,12 +150,15 @@ def _d3(v) -> ctypes.Array:
 
 # ---- reference-shaped API ---------------------------------------------------------------------
 class Material:
-    """Material(color[, shader]) (material.h:13-20); specular_power (material.h:29)."""
+    """Material(color[, shader]) (material.h:13-20); specular_power (material.h:29).
+    reflectivity: Mode X only (no reference counterpart) -- probability that a bounce is a mirror
+    reflection instead of a diffuse sample; 0 = the reference's diffuse-only material."""
 
-    def __init__(self, color, shader=(0.1, 0.7, 1.0), specular_power: float = 5.0):
+    def __init__(self, color, shader=(0.1, 0.7, 1.0), specular_power: float = 5.0, reflectivity: float = 0.0):
         self.color = tuple(float(c) for c in color)
         self.shader_parameters = tuple(float(c) for c in shader)
         self.specular_power = float(specular_power)
+        self.reflectivity = float(reflectivity)
 
 
 class _Entity:
@@ -184,6 +187,7 @@ class _Entity:
                 d.mat_color[i] = m.color[i]
                 d.mat_shader[i] = m.shader_parameters[i]
             d.mat_specular_power = m.specular_power
+            d.mat_reflectivity = m.reflectivity
 
 
 class ImpSphere(_Entity):
@@ -268,7 +272,8 @@ class Octree:
         o = cls(s.octree_min, s.octree_max)
         for e in s.entities:
             ent = _Entity(e.args, None if e.material is None else
-                          Material(e.material.color, e.material.shader, e.material.specular_power))
+                          Material(e.material.color, e.material.shader, e.material.specular_power,
+                                   e.material.reflectivity))
             ent.kind = e.kind
             o.push_back(ent)
         return o

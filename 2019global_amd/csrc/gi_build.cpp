@@ -263,6 +263,11 @@ bool build_entity(const gi_entity_desc& d, BEnt& e, std::string& err) {
         set_color(e.rec, d.mat_color);
         e.rec.shader[0] = d.mat_shader[0]; e.rec.shader[1] = d.mat_shader[1]; e.rec.shader[2] = d.mat_shader[2];
         e.rec.spec_pow = d.mat_specular_power;
+        if (!(d.mat_reflectivity >= 0.0 && d.mat_reflectivity <= 1.0)) {   // NaN fails too
+            err = "mat_reflectivity must lie in [0, 1]";
+            return false;
+        }
+        e.rec.refl = d.mat_reflectivity;
     }
     return true;
 }

@@ -955,7 +955,15 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     if (PSL) { pslot[0] = Lo.x; pslot[1] = Lo.y; pslot[2] = Lo.z; }
                     Lv = Lv + vmul(T, v3(smin(lo.x, 1.0), smin(lo.y, 1.0), smin(lo.z, 1.0)));
                     has_next = false;
-                    if (b != depth - 1) {
+                    // mirror bounce with probability e.refl (uniform dim 4): T unchanged, d reflected
+                    // about the facing normal; otherwise the diffuse bounce below
+                    const bool mirror = b != depth - 1 && e.refl > 0.0 &&
+                                        mx_u01k(PSL ? reinterpret_cast<const uint64_t*>(pslot)[9] : key, smp, b, 4) < e.refl;
+                    if (mirror) {
+                        nextd = normalize(d - N * (2.0 * dot(d, N)));
+                        if (PSL) { pslot[3] = nextd.x; pslot[4] = nextd.y; pslot[5] = nextd.z; }
+                        has_next = true;
+                    } else if (b != depth - 1) {
                         const V3 Tn = vmul(T, tc * 0.5);
                         T = Tn;
                         if (PSL) { pslot[6] = Tn.x; pslot[7] = Tn.y; pslot[8] = Tn.z; }

@@ -37,7 +37,7 @@ struct REnt {              // 208 bytes
     double spec_pow;
     float height, pad1;    // ExpCube / ExpCone height
     double sin_theta;      // ExpCone: sin(cone_theta), cone_theta = float atan(radius/height) (:950-953)
-    double pad2;
+    double refl;           // Mode X mirror-reflection probability (gi_entity_desc::mat_reflectivity)
 };
 static_assert(sizeof(REnt) == 208, "REnt layout");
 

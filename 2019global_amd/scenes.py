@@ -56,11 +56,14 @@ _NARGS = {IMP_SPHERE: 7, IMP_TRIANGLE: 9, EXP_QUAD: 9, EXP_SPHERE: 7, EXP_CUBE: 
 
 @dataclass
 class Material:
-    """``Material(color[, shader])`` (material.h:13-20) plus ``specular_power`` (material.h:29)."""
+    """``Material(color[, shader])`` (material.h:13-20) plus ``specular_power`` (material.h:29).
+    ``reflectivity`` is Mode X only (no reference counterpart): the probability that a bounce is a
+    mirror reflection; written to .scn as an 8th material value only when non-zero."""
 
     color: Vec3
     shader: Vec3 = (0.1, 0.7, 1.0)
     specular_power: float = 5.0
+    reflectivity: float = 0.0
 
 
 @dataclass
@@ -125,7 +128,8 @@ class Scene:
             out.append(_KW[e.kind] + " " + " ".join(r(a) for a in e.args))
             if e.material is not None:
                 m = e.material
-                out.append("material " + " ".join(r(float(v)) for v in (*m.color, *m.shader, m.specular_power)))
+                vals = (*m.color, *m.shader, m.specular_power) + ((m.reflectivity,) if m.reflectivity else ())
+                out.append("material " + " ".join(r(float(v)) for v in vals))
         return "\n".join(out) + "\n"
 
     def digest(self) -> str:
@@ -154,6 +158,8 @@ def parse_scn(text: str) -> Scene:
                 m.shader = tuple(v[3:6])
             if len(v) >= 7:
                 m.specular_power = v[6]
+            if len(v) >= 8:
+                m.reflectivity = v[7]
             s.entities[-1].material = m
         elif kw in _KIND:
             k = _KIND[kw]
@@ -213,6 +219,21 @@ def cornell_scene() -> Scene:
     _block(s, (5.0, -3.5, -5.0), (7.5, -1.0, -2.0), W)                 # short block
     _block(s, (6.5, 0.5, -5.0), (9.0, 3.0, 0.5), W)                    # tall block
     assert len(s.entities) == 34
+    return s
+
+
+def cornell_mirror_scene() -> Scene:
+    """Mode X mirror-bounce coverage (Material.reflectivity, no reference counterpart; not a BASELINE
+    config): the Cornell box with a perfect-mirror tall block, a half-mirror back wall and a
+    mirror-like ImpSphere in front of the short block."""
+    s = cornell_scene()
+    s.name = "cornell_mirror"
+    for e in s.entities[:2]:                       # back wall
+        e.material.reflectivity = 0.5
+    for e in s.entities[22:34]:                    # tall block
+        e.material.reflectivity = 1.0
+    sp = s.imp_sphere((4.0, -2.0, -3.5), 1.5, (1, 1, 0))
+    sp.material = Material((1.0, 1.0, 0.0), reflectivity=0.8)
     return s
 
 
@@ -297,4 +318,5 @@ CONFIG_SCENES = {
     "sphere": sphere_scene,
     "cornell": cornell_scene,
     "zoo": zoo_scene,
+    "cornell_mirror": cornell_mirror_scene,
 }

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GI_ABI_VERSION 3
+#define GI_ABI_VERSION 4
 
 typedef enum gi_status {
     GI_OK = 0,
@@ -63,6 +63,10 @@ typedef struct gi_entity_desc {
     double mat_color[3];
     double mat_shader[3];       /* Material::shader_parameters (material.h:27) */
     double mat_specular_power;  /* Material::specular_power (material.h:29) */
+    double mat_reflectivity;    /* Mode X only (the reference has no mirrors): probability in [0, 1] that a
+                                   bounce leaves by mirror reflection instead of a diffuse sample (DESIGN.md
+                                   "Mode X"); 0 (value-initialised descriptors) = diffuse only.  Mode R
+                                   ignores it. */
 } gi_entity_desc;
 
 typedef struct gi_scene_desc {

@@ -141,6 +141,10 @@ class RayTracer {
     }
 
     bool upload() {
+        if (gi_abi_version() != GI_ABI_VERSION) {   // gi.h's structs must match the loaded libgi
+            std::fprintf(stderr, "gi: libgi ABI %d, built against %d\n", gi_abi_version(), GI_ABI_VERSION);
+            return false;
+        }
         std::vector<gi_entity_desc> ents;
         for (const Entity* e : _scene->entities()) {
             gi_entity_desc d;

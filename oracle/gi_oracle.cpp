@@ -56,6 +56,7 @@ struct Mat {
     V3 color{1, 0, 0};
     V3 shader{0.1, 0.7, 1.0};   // material.h:27
     double spec_pow = 5.0;      // material.h:29
+    double refl = 0.0;          // Mode X only: mirror-reflection probability (no reference counterpart)
 };
 
 // ImpTriangle (entities.h:136-306): members initialised in declaration order.
@@ -663,6 +664,7 @@ bool parse(const char* text, Scene& s) {
             m.color = {v[0], v[1], v[2]};
             if (v.size() >= 6) m.shader = {v[3], v[4], v[5]};
             if (v.size() >= 7) m.spec_pow = v[6];
+            if (v.size() >= 8) m.refl = v[7];
             s.ents.back().mat = m;
         } else { g_err = "unsupported scene line: " + line; return false; }
     }
@@ -994,6 +996,12 @@ void pixel_mode_x(const Scene& s, const std::vector<Prim>& prims, const Cam& c, 
             loc = {smin(loc.x, 1.0), smin(loc.y, 1.0), smin(loc.z, 1.0)};
             L = L + mul(T, loc);
             if (b == depth - 1) break;
+            // mirror bounce with probability refl (uniform dim 4): T unchanged, d reflected about N
+            if (e.mat.refl > 0.0 && mx_u01(seed, pix, smp, b, 4) < e.mat.refl) {
+                d = normalize(d - N * (2.0 * dot(d, N)));
+                o = P;
+                continue;
+            }
             T = mul(T, tc * 0.5);
             if (T.x == 0.0 && T.y == 0.0 && T.z == 0.0) break;
             // cosine-weighted direction: concentric disk point + Malley's projection
@@ -1032,6 +1040,8 @@ int gio_render(const char* scn, int w, int h, int mode, int spp, int depth, uint
             if (!(e.mat.spec_pow >= 0 && e.mat.spec_pow <= 64 && e.mat.spec_pow == (double)(int)e.mat.spec_pow)) {
                 g_err = "mode X needs integer specular_power in [0,64]"; return -3;
             }
+        for (const Ent& e : s.ents)
+            if (!(e.mat.refl >= 0.0 && e.mat.refl <= 1.0)) { g_err = "reflectivity must lie in [0, 1]"; return -3; }
     }
     std::vector<Prim> prims;
     if (mode == 1) build_prims(s, prims);

@@ -160,6 +160,49 @@ def test_progressive_bands_equal_whole_frame(torch_cuda):
         assert U.bits_equal(ax, bx).all()
 
 
+def _mirror_variants():
+    tri = S.cornell_scene()             # triangles only: the 4-wave LDS kernel
+    tri.name = "cornell_mirror_tris"
+    for e in tri.entities[10:22]:       # short block: half mirror
+        e.material.reflectivity = 0.5
+    for e in tri.entities[22:34]:       # tall block: mirror
+        e.material.reflectivity = 1.0
+    soup = S.soup_scene(1000)           # HBM-resident records
+    for i, e in enumerate(soup.entities):
+        if i % 3 == 0:   # (the soup's entities share one Material object)
+            e.material = S.Material((1.0, 1.0, 1.0), reflectivity=0.7)
+    return {"cornell_mirror": S.named_scene("cornell_mirror"), "cornell_mirror_tris": tri, "soup1000_mirror": soup}
+
+
+@pytest.mark.parametrize("name,w,h,spp,depth", [("cornell_mirror", 48, 40, 4, 6), ("cornell_mirror_tris", 40, 40, 3, 8),
+                                                 ("soup1000_mirror", 40, 40, 2, 8)])
+def test_mode_x_mirror_bounces_bit_exact(torch_cuda, name, w, h, spp, depth):
+    """Material reflectivity (Mode X mirror spawn): GPU frames equal the oracle bit for bit,
+    and the mirrors change the frame (against the same scene with reflectivity 0)."""
+    sc = _mirror_variants()[name]
+    o = U.oracle_render(sc.to_scn(), w, h, mode=1, spp=spp, depth=depth, seed=77)
+    d = gi.DeviceScene.from_scene(sc)
+    rgb, rgb8 = d.render(cam_of(sc), sc.light, w, h, mode=gi.MODE_X, spp=spp, depth=depth, seed=77)
+    same = U.bits_equal(rgb.reshape(-1, 3), o["rgb"]).all(1)
+    assert same.all(), f"{(~same).sum()} of {same.size} pixels differ from the oracle"
+    assert (rgb8.reshape(-1, 3) == o["q"]).all()
+    if name.startswith("soup"):
+        return   # the white soup's lit pixels saturate at 1 either way
+    for e in sc.entities:
+        if e.material is not None:
+            e.material.reflectivity = 0.0
+    plain, _ = gi.DeviceScene.from_scene(sc).render(cam_of(sc), sc.light, w, h, mode=gi.MODE_X, spp=spp, depth=depth,
+                                                      seed=77)
+    assert not U.bits_equal(plain, rgb).all()
+
+
+def test_reflectivity_out_of_range_is_a_scene_error(torch_cuda):
+    sc = S.cornell_scene()
+    sc.entities[0].material.reflectivity = 1.5
+    with pytest.raises(gi.GIError, match="-3"):
+        gi.DeviceScene.from_scene(sc)
+
+
 def test_band_pipeline_outputs_and_callbacks(torch_cuda):
     """gi_render's two-slot band pipeline: caller-owned outputs (either one alone), band callbacks
     in row order with the final rows, slot buffers grown between calls, device path equality."""
