@@ -37,9 +37,24 @@ def test_library_built_and_exports_header_symbols():
 def test_library_loads_and_abi_version():
     L = gi.lib()
     assert L.gi_abi_version() == gi.ABI_VERSION
-    assert ctypes.sizeof(gi.EntityDesc) == 152
+    assert ctypes.sizeof(gi.EntityDesc) == 160
     assert ctypes.sizeof(gi.Opts) == 48
     assert ctypes.sizeof(gi.CameraDesc) == 80
+
+
+def test_ctypes_layouts_match_header(tmp_path):
+    """The Python mirror's structs against include/gi.h as the C compiler lays them out."""
+    import subprocess
+    src = tmp_path / "sz.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "gi.h"\n'
+                   'int main(void) { printf("%zu %zu %zu %zu %zu\\n", sizeof(gi_entity_desc), '
+                   'offsetof(gi_entity_desc, mat_reflectivity), sizeof(gi_opts), sizeof(gi_camera), '
+                   'sizeof(gi_scene_desc)); return 0; }\n')
+    exe = tmp_path / "sz"
+    subprocess.run(["gcc", "-I", os.path.join(U.ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert got == [ctypes.sizeof(gi.EntityDesc), gi.EntityDesc.mat_reflectivity.offset, ctypes.sizeof(gi.Opts),
+                   ctypes.sizeof(gi.CameraDesc), ctypes.sizeof(gi.SceneDesc)]
 
 
 def test_library_has_gfx950_code_object():
