@@ -300,6 +300,7 @@ __device__ __forceinline__ V3 primary_dir(const CamDev& c, double fx, double fy)
 struct F3 {
     float x, y, z;
 };
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ F3 f3(float x, float y, float z) { F3 r; r.x = x; r.y = y; r.z = z; return r; }
 __device__ __forceinline__ uint32_t lvl_get(uint64_t lo, uint64_t hi, int l) {
     return (uint32_t)((l < 8 ? lo >> (8 * l) : hi >> (8 * (l - 8))) & 0xFF);
@@ -363,11 +364,24 @@ __device__ __forceinline__ double x_prim_t(const XHot& p, V3 o, V3 d, double tmi
     return (t > tmin) ? t : INFINITY;
 }
 
-// fp32 slab test of child c of a wide node against [0, tmax]; boxes are outward-rounded + padded
+// fp32 slab test of child c of a wide node against [0, tmax]; boxes are outward-rounded + padded.
+// Slab distances as (b - o) * iv = fma(b, iv, -o*iv): one fma per plane.  Its error in position,
+// ~2^-24 (|o| + |b - o|), is the subtraction form's order and far inside the 1e-5 * extent padding
+// for origins within the scene's extent (bounce origins; the camera of every scene here).
+// fp32 reciprocal direction (1 ulp), clamped to +-1e30 so that an axis-parallel ray gives finite
+// plane distances (fma(b, inf, -(o * inf)) would be inf - inf = NaN); with |b - o| >= the box
+// padding the clamped distances still exceed any t of the scene, so culling stays conservative
+__device__ __forceinline__ F3 inv_dir(V3 d) {
+    return f3(__builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf((float)d.x), -1e30f, 1e30f),
+              __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf((float)d.y), -1e30f, 1e30f),
+              __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf((float)d.z), -1e30f, 1e30f));
+}
+__device__ __forceinline__ F3 neg_oiv(F3 of, F3 ivf) { return f3(-(of.x * ivf.x), -(of.y * ivf.y), -(of.z * ivf.z)); }
 __device__ __forceinline__ bool child_hit(const XWNode* nd, int c, F3 of, F3 ivf, float tmax) {
-    const float tx0 = (nd->lo[0][c] - of.x) * ivf.x, tx1 = (nd->hi[0][c] - of.x) * ivf.x;
-    const float ty0 = (nd->lo[1][c] - of.y) * ivf.y, ty1 = (nd->hi[1][c] - of.y) * ivf.y;
-    const float tz0 = (nd->lo[2][c] - of.z) * ivf.z, tz1 = (nd->hi[2][c] - of.z) * ivf.z;
+    const F3 no = neg_oiv(of, ivf);
+    const float tx0 = __builtin_fmaf(nd->lo[0][c], ivf.x, no.x), tx1 = __builtin_fmaf(nd->hi[0][c], ivf.x, no.x);
+    const float ty0 = __builtin_fmaf(nd->lo[1][c], ivf.y, no.y), ty1 = __builtin_fmaf(nd->hi[1][c], ivf.y, no.y);
+    const float tz0 = __builtin_fmaf(nd->lo[2][c], ivf.z, no.z), tz1 = __builtin_fmaf(nd->hi[2][c], ivf.z, no.z);
     const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
     const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
     return tn <= tf;
@@ -380,6 +394,13 @@ __device__ __forceinline__ bool box32_hit(const XBox& b, F3 of, F3 ivf, float tm
     const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
     return tn <= tf;
 }
+// bit c of m moved to bit c ^ dm (three conditional swaps of bit groups)
+__device__ __forceinline__ uint32_t xor_permute8(uint32_t m, int dm) {
+    m = (dm & 1) ? (((m << 1) & 0xAAu) | ((m >> 1) & 0x55u)) : m;
+    m = (dm & 2) ? (((m << 2) & 0xCCu) | ((m >> 2) & 0x33u)) : m;
+    m = (dm & 4) ? (((m << 4) & 0xF0u) | ((m >> 4) & 0x0Fu)) : m;
+    return m;
+}
 // mask of hit, existing children with bit k for child k ^ dmask (bit order = front-to-back).
 // The node's 48 bounds are fetched by 12 independent 16-byte loads (one memory round trip) and
 // all 8 slab tests run branch-free; existence comes from the node's precomputed bit mask.
@@ -389,6 +410,7 @@ __device__ __forceinline__ bool box32_hit(const XBox& b, F3 of, F3 ivf, float tm
 template <bool AXIS>
 __device__ __forceinline__ uint32_t children_mask(const XWNode* nd, F3 of, F3 ivf, float tmax, int dmask) {
     const float4* b = reinterpret_cast<const float4*>(nd);
+    const F3 no = neg_oiv(of, ivf);
     if constexpr (AXIS) {
     float tn[8], tf[8];
 #pragma unroll
@@ -396,21 +418,24 @@ __device__ __forceinline__ uint32_t children_mask(const XWNode* nd, F3 of, F3 iv
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         const float4 l0 = b[2 * a], l1 = b[2 * a + 1], h0 = b[6 + 2 * a], h1 = b[6 + 2 * a + 1];
-        const float lo[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
-        const float hi[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-        const float o = a == 0 ? of.x : (a == 1 ? of.y : of.z), iv = a == 0 ? ivf.x : (a == 1 ? ivf.y : ivf.z);
+        const float o = a == 0 ? no.x : (a == 1 ? no.y : no.z), iv = a == 0 ? ivf.x : (a == 1 ? ivf.y : ivf.z);
+        // children in pairs: one packed fma (v_pk_fma_f32) gives two children's plane distances
+        const f32x2 lo[4] = {f32x2{l0.x, l0.y}, f32x2{l0.z, l0.w}, f32x2{l1.x, l1.y}, f32x2{l1.z, l1.w}};
+        const f32x2 hi[4] = {f32x2{h0.x, h0.y}, f32x2{h0.z, h0.w}, f32x2{h1.x, h1.y}, f32x2{h1.z, h1.w}};
+        const f32x2 iv2 = {iv, iv}, o2 = {o, o};
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const float t0 = (lo[c] - o) * iv, t1 = (hi[c] - o) * iv;
-            tn[c] = fmaxf(tn[c], fminf(t0, t1));
-            tf[c] = fminf(tf[c], fmaxf(t0, t1));
+        for (int q = 0; q < 4; ++q) {
+            const f32x2 t0 = __builtin_elementwise_fma(lo[q], iv2, o2), t1 = __builtin_elementwise_fma(hi[q], iv2, o2);
+            tn[2 * q] = fmaxf(tn[2 * q], fminf(t0.x, t1.x));
+            tf[2 * q] = fminf(tf[2 * q], fmaxf(t0.x, t1.x));
+            tn[2 * q + 1] = fmaxf(tn[2 * q + 1], fminf(t0.y, t1.y));
+            tf[2 * q + 1] = fminf(tf[2 * q + 1], fmaxf(t0.y, t1.y));
         }
     }
-    const int ex = nd->exists;
     uint32_t m = 0;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) m |= (uint32_t)((tn[c] <= tf[c]) & ((ex >> c) & 1)) << (c ^ dmask);
-    return m;
+    for (int c = 0; c < 8; ++c) m |= tn[c] <= tf[c] ? 1u << c : 0u;
+    return xor_permute8(m & (uint32_t)nd->exists, dmask);
     } else {
     float4 q[12];
 #pragma unroll
@@ -420,14 +445,14 @@ __device__ __forceinline__ uint32_t children_mask(const XWNode* nd, F3 of, F3 iv
     uint32_t m = 0;
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
-        const float tx0 = (v[c] - of.x) * ivf.x, tx1 = (v[24 + c] - of.x) * ivf.x;
-        const float ty0 = (v[8 + c] - of.y) * ivf.y, ty1 = (v[32 + c] - of.y) * ivf.y;
-        const float tz0 = (v[16 + c] - of.z) * ivf.z, tz1 = (v[40 + c] - of.z) * ivf.z;
+        const float tx0 = __builtin_fmaf(v[c], ivf.x, no.x), tx1 = __builtin_fmaf(v[24 + c], ivf.x, no.x);
+        const float ty0 = __builtin_fmaf(v[8 + c], ivf.y, no.y), ty1 = __builtin_fmaf(v[32 + c], ivf.y, no.y);
+        const float tz0 = __builtin_fmaf(v[16 + c], ivf.z, no.z), tz1 = __builtin_fmaf(v[40 + c], ivf.z, no.z);
         const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
         const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
-        m |= (uint32_t)((tn <= tf) & ((ex >> c) & 1)) << (c ^ dmask);
+        m |= tn <= tf ? 1u << c : 0u;
     }
-    return m;
+    return xor_permute8(m & (uint32_t)ex, dmask);
     }
 }
 
@@ -910,8 +935,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 tbest = INFINITY;
                 tbest_f = INFINITY;
                 of = f3((float)o.x, (float)o.y, (float)o.z);
-                ivf = f3(__builtin_amdgcn_rcpf((float)d.x), __builtin_amdgcn_rcpf((float)d.y),
-                         __builtin_amdgcn_rcpf((float)d.z));
+                ivf = inv_dir(d);
                 dmask = (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
                 const uint32_t rm = children_mask<PAIR>(W, of, ivf, tbest_f, dmask);
                 best = -1;
@@ -1130,8 +1154,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 // start traversing the lane's ray (fp32 reciprocal, 1 ulp: the culling error stays
                 // far inside the 1e-5*extent box padding)
                 of = f3((float)o.x, (float)o.y, (float)o.z);
-                ivf = f3(__builtin_amdgcn_rcpf((float)d.x), __builtin_amdgcn_rcpf((float)d.y),
-                         __builtin_amdgcn_rcpf((float)d.z));
+                ivf = inv_dir(d);
                 dmask = (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
                 const uint32_t rm = children_mask<PAIR>(W, of, ivf, tbest_f, dmask);
                 if (phase == PH_START) phase = PH_CLOSEST;

@@ -79,10 +79,14 @@ static float up32(double v) {
     return f;
 }
 struct F3 { float x, y, z; };
+// the kernel's inv_dir: reciprocal clamped to +-1e30 (finite plane distances for axis-parallel rays)
+static float inv_clamp(float v) { return std::fmin(std::fmax(1.0f / v, -1e30f), 1e30f); }
+// the kernel's form: plane distance fma(b, iv, -(o * iv))
 static bool child_hit(const XWNode* nd, int c, F3 of, F3 ivf, float tmax) {
-    const float tx0 = (nd->lo[0][c] - of.x) * ivf.x, tx1 = (nd->hi[0][c] - of.x) * ivf.x;
-    const float ty0 = (nd->lo[1][c] - of.y) * ivf.y, ty1 = (nd->hi[1][c] - of.y) * ivf.y;
-    const float tz0 = (nd->lo[2][c] - of.z) * ivf.z, tz1 = (nd->hi[2][c] - of.z) * ivf.z;
+    const float nx = -(of.x * ivf.x), ny = -(of.y * ivf.y), nz = -(of.z * ivf.z);
+    const float tx0 = std::fmaf(nd->lo[0][c], ivf.x, nx), tx1 = std::fmaf(nd->hi[0][c], ivf.x, nx);
+    const float ty0 = std::fmaf(nd->lo[1][c], ivf.y, ny), ty1 = std::fmaf(nd->hi[1][c], ivf.y, ny);
+    const float tz0 = std::fmaf(nd->lo[2][c], ivf.z, nz), tz1 = std::fmaf(nd->hi[2][c], ivf.z, nz);
     const float tn = std::fmax(std::fmax(std::fmin(tx0, tx1), std::fmin(ty0, ty1)), std::fmax(std::fmin(tz0, tz1), 0.0f));
     const float tf = std::fmin(std::fmin(std::fmax(tx0, tx1), std::fmax(ty0, ty1)), std::fmin(std::fmax(tz0, tz1), tmax));
     return tn <= tf;
@@ -103,7 +107,7 @@ static void lvl_set(uint64_t& lo, uint64_t& hi, int l, uint32_t m) {
 static long g_prim_tests = 0;
 static int traverse(const HostScene& s, V3 o, V3 d, bool shadow, double tmax, double& tbest, long& visits) {
     // the device uses v_rcp_f32 (1 ulp) here; the correctly rounded fp32 reciprocal stands in for it
-    const F3 of = {(float)o.x, (float)o.y, (float)o.z}, ivf = {1.0f / (float)d.x, 1.0f / (float)d.y, 1.0f / (float)d.z};
+    const F3 of = {(float)o.x, (float)o.y, (float)o.z}, ivf = {inv_clamp((float)d.x), inv_clamp((float)d.y), inv_clamp((float)d.z)};
     const int dmask = (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
     tbest = shadow ? tmax : INFINITY;
     float tbest_f = shadow ? up32(tmax) : INFINITY;
