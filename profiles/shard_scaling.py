@@ -47,12 +47,20 @@ def main():
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / a.reps
             kms, _ = dev.kernel_ms()   # the dominant kernel alone (k_mode_x)
+            st_t = torch.zeros(gi.STATS_N, dtype=torch.int64, device="cuda")
+            dev.render_device(cam, sc.light, w, h, buf.data_ptr(), buf8.data_ptr(), s.cuda_stream,
+                              stats_ptr=st_t.data_ptr(), **kw)
+            st = st_t.cpu().tolist()
+            it, rays = st[gi.STAT_X_ITERS], max(1, st[gi.STAT_RAYS])
+            sched = {"rays": rays, "wave_iters_per_kray": round(it * 1e3 / rays, 3),
+                     "trav_lane_fill": round(st[gi.STAT_X_TRAV] / max(1, 64.0 * it), 4),
+                     "handler_lane_fill": round(st[gi.STAT_X_HLANES] / max(1, 64.0 * st[gi.STAT_X_HANDLE]), 4)}
             if n == 1:
                 t1 = ms
             res[f"N{n}_rank{r}_ms"] = round(ms, 3)
             res[f"N{n}_rank{r}_speedup"] = round(t1 / ms, 3)
             print(json.dumps({"n": n, "rank": r, "ms": round(ms, 3), "kernel_ms": round(kms, 3),
-                              "ideal_ms": round(t1 / n, 3), "speedup": round(t1 / ms, 3)}), flush=True)
+                              "ideal_ms": round(t1 / n, 3), "speedup": round(t1 / ms, 3), **sched}), flush=True)
     print(json.dumps(res))
 
 
