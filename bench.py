@@ -160,6 +160,8 @@ def main():
     ap.add_argument("--workload", default="C3", choices=sorted(WORKLOADS))
     ap.add_argument("--seed", type=int, default=2019)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-path", action="store_true",
+                    help="skip the host-buffer gi_render timings (profiling runs: only the timed frames launch)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI) for real runs; gloo rehearses N ranks sharing one GPU")
     args = ap.parse_args()
@@ -327,7 +329,7 @@ def main():
                                "cycle_share": {k: round(st[i] / max(1, st[gi.STAT_X_CYC_ALL]), 4) for k, i in
                                                (("traverse", gi.STAT_X_CYC_TRAV), ("consume", gi.STAT_X_CYC_HIT),
                                                 ("next_ray", gi.STAT_X_CYC_NEXT))}}
-        if world == 1:
+        if world == 1 and not args.no_host_path:
             out["host_path"] = host_path(dev, cam, sc.light, w, h, mode, spp, depth, args.seed)
         if not args.no_cpu_baseline and world == 1:
             scn = sc.to_scn()

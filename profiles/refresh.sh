@@ -16,4 +16,13 @@ for W in C3 C4; do
   python3 profiles/summarize.py gpurun_out/prof_${w}_$TAG $W k_mode_x $OUT/${TAG}_${w}_pmc.json || exit 1
   cp gpurun_out/prof_${w}_$TAG/trace/run_kernel_stats.csv $OUT/${TAG}_${w}_kernel_stats.csv
 done
+for W in C4 C5; do
+  w=$(echo $W | tr A-Z a-z)
+  timeout -k 10 300 python bench.py --workload $W --no-cpu-baseline > $OUT/bench_$w.json 2> $OUT/bench_$w.err || { tail -5 $OUT/bench_$w.err; exit 1; }
+done
+timeout -k 10 300 python profiles/shard_scaling.py > $OUT/shard_scaling_c3.log 2>&1 || { tail -5 $OUT/shard_scaling_c3.log; exit 1; }
+grep '^{"n"' $OUT/shard_scaling_c3.log > $OUT/${TAG}_shard_scaling_c3.jsonl
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \
+  bench.py --gpus 2 --dist-backend gloo --steps 3 --warmup 1 > $OUT/${TAG}_rehearsal_n2_gloo.log 2>&1 || { tail -5 $OUT/${TAG}_rehearsal_n2_gloo.log; exit 1; }
+tail -1 $OUT/${TAG}_rehearsal_n2_gloo.log
 echo refresh done

@@ -9,13 +9,13 @@ export TMPDIR=/tmp
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $R/bench.py --no-cpu-baseline "$@" > $OUT/trace.log 2>&1 || exit $?
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $R/bench.py --no-cpu-baseline --no-host-path "$@" > $OUT/trace.log 2>&1 || exit $?
 i=0
 for P in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS" \
          "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY" \
          "SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE" \
          "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
-  timeout -k 10 600 rocprofv3 --pmc $P --output-format csv -d $OUT/pmc$i -o run -- python3 $R/bench.py --no-cpu-baseline "$@" > $OUT/pmc$i.log 2>&1 || { echo "pmc pass $i failed: $P"; exit 1; }
+  timeout -k 10 600 rocprofv3 --pmc $P --output-format csv -d $OUT/pmc$i -o run -- python3 $R/bench.py --no-cpu-baseline --no-host-path "$@" > $OUT/pmc$i.log 2>&1 || { echo "pmc pass $i failed: $P"; exit 1; }
 done
 echo done

@@ -317,6 +317,19 @@ def test_mode_x_spp_runs_bit_exact(torch_cuda, scene, w, h, spp, depth):
     assert (rgb8.reshape(-1, 3) == o["q"]).all()
 
 
+@pytest.mark.parametrize("scene,w,h,spp,depth", [("cornell", 512, 512, 1, 4),          # BASELINE configs[1] (C2)
+                                                  ("cornell_mirror", 256, 256, 4, 8)])
+def test_mode_x_whole_frame_bit_exact(torch_cuda, scene, w, h, spp, depth):
+    """Every pixel of a whole frame against the oracle (C2 is the bench's C2 workload)."""
+    sc = _scene(scene)
+    o = U.oracle_render(sc.to_scn(), w, h, mode=1, spp=spp, depth=depth, seed=2019, threads=16)
+    rgb, rgb8 = dev_scene(scene).render(cam_of(sc), sc.light, w, h, mode=gi.MODE_X, spp=spp, depth=depth, seed=2019)
+    same = U.bits_equal(rgb.reshape(-1, 3), o["rgb"]).all(1)
+    assert same.all(), f"{(~same).sum()} of {same.size} pixels differ from the oracle"
+    assert (rgb8.reshape(-1, 3) == o["q"]).all()
+    assert (o["hit"] >= 0).mean() > 0.5
+
+
 def test_mode_x_c3_config_windows_and_shards(torch_cuda):
     """The bench's own workload: C3 = Cornell 1920x1080, depth 8, 64 spp (the device picks 8-sample
     work units for the whole frame and 1-sample units for an 8-way shard of it).  Two windows against
