@@ -762,7 +762,11 @@ struct XWork {
 #define GI_X_UNITS_PER_LANE 8   // target units per lane when choosing the run length k
 #endif
 #ifndef GI_X_MAX_RUN
-#define GI_X_MAX_RUN 8          // largest run length k (samples per unit)
+// largest run length k (samples per unit).  1: every unit is one sample -- measured fastest on the
+// BASELINE Mode X workloads (C3 7.45 -> 6.72 ms, C5 338 -> 328 ms, X-zoo 7.7 -> 6.0 ms against k = 8;
+// fewer wave iterations and fuller handler runs); scenes whose samples are mostly cheap background
+// rays pay for the per-unit fetch instead (X-main 0.47 -> 0.72 ms) and are better served by 8
+#define GI_X_MAX_RUN 1
 #endif
 
 template <bool STATS, bool PAIR, bool PSL, typename NodeP, typename HotP, typename PrimP, typename EntP>
@@ -1432,7 +1436,8 @@ hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w,
         }
         const int resident = resident_blocks[kv];
         const long long n_slots = m.n_local * (kTile * kTile);
-        const long long want = (n_slots * std::min(o.spp, GI_X_MAX_RUN) / 64 + kWavesPerBlock - 1) / kWavesPerBlock;
+        // up to one lane per (pixel slot, sample): single-sample units can occupy that many lanes
+        const long long want = (n_slots * (long long)o.spp / 64 + kWavesPerBlock - 1) / kWavesPerBlock;
         const dim3 pgrid((unsigned)std::max<long long>(1, std::min<long long>(want, resident)));
         if (!xs.list || (unsigned long long)xs.cap < (unsigned long long)n_slots || (o.spp > 1 && (!xs.part || xs.spp < o.spp)))
             return hipErrorInvalidValue;
