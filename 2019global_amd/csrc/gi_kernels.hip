@@ -268,7 +268,8 @@ __device__ __forceinline__ bool lane_pixel(const TileMap& m, long long lt, long 
     if (lt >= m.n_local) return false;
     const long long t = (long long)m.shard_index + lt * m.shard_count;
     if (t >= m.n_tiles) { out_idx = -1; return false; }
-    const int ty = (int)(t / m.tiles_x), tx = (int)(t % m.tiles_x);
+    const unsigned tu = (unsigned)t, tyu = tu / (unsigned)m.tiles_x;   // 32-bit: see slot_pixel
+    const int ty = (int)tyu, tx = (int)(tu - tyu * (unsigned)m.tiles_x);
     x = tx * kTile + (lane & 7);
     y = ty * kTile + (lane >> 3);
     if (m.shard_count == 1) out_idx = (long long)y * m.w + x;
@@ -281,7 +282,10 @@ __device__ __forceinline__ bool slot_pixel(const TileMap& m, long long lt, int j
     out_idx = -1;
     const long long t = (long long)m.shard_index + lt * m.shard_count;
     if (t >= m.n_tiles) return false;
-    const int ty = (int)(t / m.tiles_x), tx = (int)(t % m.tiles_x);
+    // tile counts stay below 2^32 (check_opts caps a frame at 2^34 pixels, i.e. 2^28 tiles), so
+    // the tile row / column come from a 32-bit division (a 64-bit one is a long software routine)
+    const unsigned tu = (unsigned)t, tyu = tu / (unsigned)m.tiles_x;
+    const int ty = (int)tyu, tx = (int)(tu - tyu * (unsigned)m.tiles_x);
     x = tx * kTile + (j & 7);
     y = ty * kTile + (j >> 3);
     if (m.shard_count == 1) out_idx = (long long)y * m.w + x;
