@@ -781,13 +781,15 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                                             int xflags, XCounters& cnt) {
     const int lane = threadIdx.x & 63;
     const unsigned n_list = *wk.n_list;
-    // run length k: the largest power of two <= GI_X_MAX_RUN (and <= spp) that still leaves about
+    // run length k: the largest power of two <= the launch's maximum (xflags bits 8-10: log2, from
+    // GI_X_MAX_RUN or the environment variable of that name) and <= spp that still leaves about
     // GI_X_UNITS_PER_LANE units per lane of the grid (every wave computes the same k)
     int k = 1;
     {
         const double lanes = (double)gridDim.x * (double)blockDim.x;
         const double samples = (double)n_list * (double)spp;
-        while (2 * k <= GI_X_MAX_RUN && 2 * k <= spp && samples / (2.0 * k) >= GI_X_UNITS_PER_LANE * lanes) k *= 2;
+        const int max_run = 1 << ((xflags >> 8) & 7);
+        while (2 * k <= max_run && 2 * k <= spp && samples / (2.0 * k) >= GI_X_UNITS_PER_LANE * lanes) k *= 2;
     }
     const unsigned runs = (unsigned)((spp + k - 1) / k);              // units per pixel
     const unsigned n_blocks = ((n_list + 63u) >> 6) * runs;
@@ -1468,7 +1470,17 @@ hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w,
             const char* v = std::getenv("GI_X_FLAGS");
             env_xf = v ? std::atoi(v) : -1;
         }
-        const int xf = env_xf >= 0 ? env_xf : sc.x_flags;
+        // maximum run length (samples per work unit), log2 in bits 8-10; GI_X_MAX_RUN=<power of two>
+        // in the environment overrides the build's default (scenes of cheap background samples
+        // such as the main.cpp scene prefer 8)
+        static int env_run = -1;
+        if (env_run == -1) {
+            const char* v = std::getenv("GI_X_MAX_RUN");
+            int r = v ? std::max(1, std::min(128, std::atoi(v))) : GI_X_MAX_RUN, lg = 0;
+            while ((2 << lg) <= r) ++lg;
+            env_run = lg;
+        }
+        const int xf = (env_xf >= 0 ? env_xf : sc.x_flags) | (env_run << 8);
 #define GI_LAUNCH_X(S, L, W) hipLaunchKernelGGL((k_mode_x<S, L, W>), pgrid, block, lds_bytes, stream, sc, cam, light, m, o.spp, \
                                            o.depth, o.seed, rgb, rgb8, st, wk, h8, xf)
         mark(ev_begin);

@@ -330,6 +330,31 @@ def test_mode_x_whole_frame_bit_exact(torch_cuda, scene, w, h, spp, depth):
     assert (o["hit"] >= 0).mean() > 0.5
 
 
+def test_mode_x_multi_sample_units_bit_exact(torch_cuda, tmp_path):
+    """GI_X_MAX_RUN=8 (k-sample work units, read once per process: a child process renders) gives
+    the same frame bit for bit as the default one-sample units and as the oracle."""
+    import subprocess
+    import sys
+    sc = S.cornell_scene()
+    # 512 x 512 x 96 spp: ~90 listed samples per lane of the resident grid, so k = 8 is chosen
+    w, h, kw = 512, 512, dict(spp=96, depth=3, seed=11)
+    out = tmp_path / "k8.npy"
+    code = ("import sys, numpy as np; sys.path.insert(0, %r); sys.path.insert(0, %r); import oracle_util as U; "
+            "gi = U.pkg(); S = U.scenes(); sc = S.cornell_scene(); "
+            "d = gi.DeviceScene.from_scene(sc); "
+            "rgb, _ = d.render(gi.Camera(sc.cam_pos, sc.cam_look, sc.focal), sc.light, %d, %d, mode=gi.MODE_X, "
+            "spp=%d, depth=%d, seed=%d); np.save(%r, rgb)") % (U.ROOT, os.path.join(U.ROOT, "tests"), w, h,
+                                                                kw["spp"], kw["depth"], kw["seed"], str(out))
+    subprocess.run([sys.executable, "-c", code], check=True, timeout=120, env=dict(os.environ, GI_X_MAX_RUN="8"))
+    k8 = np.load(out)
+    k1, _ = dev_scene("cornell").render(cam_of(sc), sc.light, w, h, mode=gi.MODE_X, **kw)
+    assert U.bits_equal(k8, k1).all()
+    win = (240, 300, 264, 316)
+    o = U.oracle_render(sc.to_scn(), w, h, mode=1, window=win, **kw)
+    assert (o["hit"] >= 0).all()
+    assert U.bits_equal(k1[win[1]:win[3], win[0]:win[2]].reshape(-1, 3), o["rgb"]).all()
+
+
 def test_mode_x_c3_config_windows_and_shards(torch_cuda):
     """The bench's own workload: C3 = Cornell 1920x1080, depth 8, 64 spp (the device picks 8-sample
     work units for the whole frame and 1-sample units for an 8-way shard of it).  Two windows against
