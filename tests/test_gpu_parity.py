@@ -400,11 +400,12 @@ def test_mode_x_cornell_window_full_depth(torch_cuda):
 
 
 @pytest.mark.parametrize("n", [2, 3, 8])
-@pytest.mark.parametrize("mode,spp", [(gi.MODE_R, 1), (gi.MODE_X, 2), (gi.MODE_X, 19)])
-def test_sharded_render_equals_single(torch_cuda, n, mode, spp):
+@pytest.mark.parametrize("mode,spp,scene", [(gi.MODE_R, 1, "cornell"), (gi.MODE_X, 2, "cornell"),
+                                            (gi.MODE_X, 19, "cornell"), (gi.MODE_X, 5, "cornell_mirror")])
+def test_sharded_render_equals_single(torch_cuda, n, mode, spp, scene):
     torch = torch_cuda
-    sc = S.cornell_scene()
-    d = dev_scene("cornell")
+    sc = _scene(scene)
+    d = dev_scene(scene)
     w, h = 203, 117
     kw = dict(mode=mode, spp=spp, depth=4, seed=3) if mode == gi.MODE_X else {}
     full = torch.zeros(h * w * 3, dtype=torch.float64, device="cuda")
