@@ -54,7 +54,6 @@ struct gi_scene {
     HostPath hp;   // gi_render's band pipeline (streams, device band slots, pinned staging)
     int device = -1;
     int64_t bytes = 0;
-    bool mode_x_ok = true;
 };
 
 namespace {
@@ -105,7 +104,6 @@ int check_opts(const gi_scene* s, int w, int h, const gi_opts* o) {
     if (o->shard_count < 1 || o->shard_index < 0 || o->shard_index >= o->shard_count) return fail(GI_ERR_ARG, "bad shard");
     if (o->mode == GI_MODE_X) {
         if (o->spp < 1 || o->depth < 1 || o->depth > 0xFFFF) return fail(GI_ERR_ARG, "mode X needs spp >= 1, 1 <= depth <= 65535");
-        if (!s->mode_x_ok) return fail(GI_ERR_SCENE, "mode X needs integer specular_power in [0, 64]");
     }
     if ((o->flags & GI_FLAG_STATS) && !o->stats) return fail(GI_ERR_ARG, "GI_FLAG_STATS without stats buffer");
     return GI_OK;
@@ -268,8 +266,6 @@ int gi_scene_create(const gi_scene_desc* desc, gi_scene** out) {
         delete s;
         return fail(GI_ERR_SCENE, err);
     }
-    for (const REnt& r : s->host.ents)
-        if (!(r.spec_pow >= 0 && r.spec_pow <= 64 && r.spec_pow == std::floor(r.spec_pow))) s->mode_x_ok = false;
     DevScene& d = s->dev;
     memset(&d, 0, sizeof d);
     const HostScene& h = s->host;

@@ -981,7 +981,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     const V3 la = tc * e.shader[0];
                     const V3 ldf = (smax(0.0, dot(N, Ld)) * (tc * 0.5)) * e.shader[1];
                     const V3 bis = normalize(normalize(-d) + Ld);
-                    const double spw = mx_powi(smax(0.0, dot(N, bis)), (int)e.spec_pow);
+                    const double spw = mx_pow(smax(0.0, dot(N, bis)), e.spec_pow);
                     const V3 ls = v3(spw, spw, spw) * e.shader[2];
                     const V3 lo = (la + ldf) + ls;
                     if (PSL) T = v3(pslot[6], pslot[7], pslot[8]);

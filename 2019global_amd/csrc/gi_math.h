@@ -244,6 +244,51 @@ GI_HD double mx_powi(double x, int p) {
     }
     return r;
 }
+// x^p for any specular power (Material::specular_power is any double, material.h:29): integer p in
+// [0, 64] by square-and-multiply (mx_powi); otherwise exp(p * ln x) with ln from the atanh series of
+// the mantissa and exp from a Taylor polynomial, 2^n applied through the exponent bits -- only
+// +, -, *, / and exact bit operations on fp64, so host and gfx950 agree bit for bit (DESIGN.md
+// "Mode X").  Relative error ~1e-15 against the true power (x in [0, 1] at the call site).
+GI_HD double mx_bits_to_f64(uint64_t b) { double d; __builtin_memcpy(&d, &b, 8); return d; }
+GI_HD uint64_t mx_f64_to_bits(double d) { uint64_t b; __builtin_memcpy(&b, &d, 8); return b; }
+GI_HD double mx_ln(double x) {   // x > 0, finite
+    int e = 0;
+    if (x < 0x1.0p-1022) { x = x * 0x1.0p+54; e = -54; }   // subnormal: exact rescale
+    const uint64_t b = mx_f64_to_bits(x);
+    e += (int)((b >> 52) & 0x7FF) - 1023;
+    double m = mx_bits_to_f64((b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);   // [1, 2)
+    if (m > 1.4142135623730951) { m = m * 0.5; e += 1; }                               // [0.707, 1.414]
+    const double s = (m - 1.0) / (m + 1.0), z = s * s;
+    double q = 1.0 / 25.0;
+    q = q * z + 1.0 / 23.0; q = q * z + 1.0 / 21.0; q = q * z + 1.0 / 19.0; q = q * z + 1.0 / 17.0;
+    q = q * z + 1.0 / 15.0; q = q * z + 1.0 / 13.0; q = q * z + 1.0 / 11.0; q = q * z + 1.0 / 9.0;
+    q = q * z + 1.0 / 7.0; q = q * z + 1.0 / 5.0; q = q * z + 1.0 / 3.0; q = q * z + 1.0;
+    const double de = (double)e;
+    return de * 0x1.62e42fee00000p-1 + (de * 0x1.a39ef35793c76p-33 + 2.0 * s * q);
+}
+GI_HD double mx_exp(double y) {
+    if (!(y > -746.0)) return y != y ? y : 0.0;
+    if (y > 710.0) return __builtin_inf();
+    const int n = (int)(y * 0x1.71547652b82fep+0 + (y >= 0.0 ? 0.5 : -0.5));   // round(y / ln 2)
+    const double dn = (double)n;
+    const double r = (y - dn * 0x1.62e42fee00000p-1) - dn * 0x1.a39ef35793c76p-33;   // |r| <~ 0.35
+    double q = 1.0 / 355687428096000.0;   // 1/17!
+    q = q * r + 1.0 / 20922789888000.0; q = q * r + 1.0 / 1307674368000.0; q = q * r + 1.0 / 87178291200.0;
+    q = q * r + 1.0 / 6227020800.0; q = q * r + 1.0 / 479001600.0; q = q * r + 1.0 / 39916800.0;
+    q = q * r + 1.0 / 3628800.0; q = q * r + 1.0 / 362880.0; q = q * r + 1.0 / 40320.0; q = q * r + 1.0 / 5040.0;
+    q = q * r + 1.0 / 720.0; q = q * r + 1.0 / 120.0; q = q * r + 1.0 / 24.0; q = q * r + 1.0 / 6.0;
+    q = q * r + 0.5; q = q * r + 1.0; q = q * r + 1.0;
+    if (n >= -1022) return q * mx_bits_to_f64((uint64_t)(n + 1023) << 52);
+    return (q * mx_bits_to_f64((uint64_t)(n + 1023 + 54) << 52)) * 0x1.0p-54;   // subnormal result
+}
+GI_HD double mx_pow(double x, double p) {
+    if (p >= 0.0 && p <= 64.0 && p == (double)(int)p) return mx_powi(x, (int)p);
+    if (p != p || x != x) return __builtin_nan("");
+    if (x == 0.0) return p > 0.0 ? 0.0 : __builtin_inf();
+    if (x < 0.0) return __builtin_nan("");
+    if (x == __builtin_inf()) return p > 0.0 ? x : 0.0;
+    return mx_exp(p * mx_ln(x));
+}
 
 // Texture (material.h:65-106): 32x32 int checker, colour truncated to int (A.7); a negative
 // index (out-of-bounds UB in the reference, A.9) wraps into [0,32).

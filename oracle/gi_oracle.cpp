@@ -6,6 +6,7 @@
 // Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load this library.
 #include "gi_oracle.h"
 
+#include <algorithm>
 #include <cfloat>
 #include <climits>
 #include <cmath>
@@ -634,7 +635,7 @@ struct Scene {
     Octree tree;
 };
 
-bool parse(const char* text, Scene& s) {
+bool parse(const char* text, Scene& s, bool build_tree = true) {
     std::istringstream in(text);
     std::string line;
     while (std::getline(in, line)) {
@@ -670,7 +671,8 @@ bool parse(const char* text, Scene& s) {
     }
     s.tree.ents = &s.ents;
     s.tree.init(s.omin, s.omax);
-    for (int i = 0; i < (int)s.ents.size(); ++i) s.tree.push_back(i);
+    if (build_tree)   // Mode X does not use the reference octree
+        for (int i = 0; i < (int)s.ents.size(); ++i) s.tree.push_back(i);
     return true;
 }
 
@@ -753,6 +755,60 @@ double mx_powi(double x, int p) {
         p >>= 1;
     }
     return r;
+}
+
+// Any specular power (material.h:29 is a double): integer p in [0, 64] by square-and-multiply,
+// otherwise exp(p * ln x) -- ln from the atanh series of the mantissa in [sqrt(1/2), sqrt(2)],
+// exp by a degree-17 Taylor polynomial after n = round(y / ln 2), 2^n through the exponent bits.
+// Only +, -, *, / and exact bit operations: the same doubles on any IEEE machine.
+double mx_ln(double x) {
+    int e = 0;
+    if (x < 0x1.0p-1022) { x = x * 0x1.0p+54; e = -54; }
+    uint64_t b;
+    memcpy(&b, &x, 8);
+    e += (int)((b >> 52) & 0x7FF) - 1023;
+    const uint64_t mb = (b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull;
+    double m;
+    memcpy(&m, &mb, 8);
+    if (m > 1.4142135623730951) { m = m * 0.5; e += 1; }
+    const double s = (m - 1.0) / (m + 1.0), z = s * s;
+    static const double inv_odd[13] = {1.0 / 25.0, 1.0 / 23.0, 1.0 / 21.0, 1.0 / 19.0, 1.0 / 17.0, 1.0 / 15.0, 1.0 / 13.0,
+                                       1.0 / 11.0, 1.0 / 9.0, 1.0 / 7.0, 1.0 / 5.0, 1.0 / 3.0, 1.0};
+    double q = inv_odd[0];
+    for (int k = 1; k < 13; ++k) q = q * z + inv_odd[k];
+    const double de = (double)e;
+    return de * 0x1.62e42fee00000p-1 + (de * 0x1.a39ef35793c76p-33 + 2.0 * s * q);
+}
+double mx_exp(double y) {
+    if (!(y > -746.0)) return std::isnan(y) ? y : 0.0;
+    if (y > 710.0) return INFINITY;
+    const int n = (int)(y * 0x1.71547652b82fep+0 + (y >= 0.0 ? 0.5 : -0.5));
+    const double dn = (double)n;
+    const double r = (y - dn * 0x1.62e42fee00000p-1) - dn * 0x1.a39ef35793c76p-33;
+    static const double inv_fact[18] = {1.0 / 355687428096000.0, 1.0 / 20922789888000.0, 1.0 / 1307674368000.0,
+                                        1.0 / 87178291200.0, 1.0 / 6227020800.0, 1.0 / 479001600.0, 1.0 / 39916800.0,
+                                        1.0 / 3628800.0, 1.0 / 362880.0, 1.0 / 40320.0, 1.0 / 5040.0, 1.0 / 720.0,
+                                        1.0 / 120.0, 1.0 / 24.0, 1.0 / 6.0, 0.5, 1.0, 1.0};
+    double q = inv_fact[0];
+    for (int k = 1; k < 18; ++k) q = q * r + inv_fact[k];
+    uint64_t sb;
+    double sc;
+    if (n >= -1022) {
+        sb = (uint64_t)(n + 1023) << 52;
+        memcpy(&sc, &sb, 8);
+        return q * sc;
+    }
+    sb = (uint64_t)(n + 1023 + 54) << 52;
+    memcpy(&sc, &sb, 8);
+    return (q * sc) * 0x1.0p-54;
+}
+double mx_pow(double x, double p) {
+    if (p >= 0.0 && p <= 64.0 && p == (double)(int)p) return mx_powi(x, (int)p);
+    if (std::isnan(p) || std::isnan(x)) return NAN;
+    if (x == 0.0) return p > 0.0 ? 0.0 : INFINITY;
+    if (x < 0.0) return NAN;
+    if (std::isinf(x)) return p > 0.0 ? x : 0.0;
+    return mx_exp(p * mx_ln(x));
 }
 
 inline uint64_t mix64(uint64_t z) {
@@ -865,19 +921,158 @@ inline double mx_prim_t(const Prim& p, V3 o, V3 d, double tmin) {
     return p.kind == 0 ? mx_tri_t(p, o, d, tmin) : mx_sph_t(p, o, d, tmin);
 }
 
-int mx_closest(const std::vector<Prim>& prims, V3 o, V3 d, double& tbest) {
+// Closest hit over ALL primitives: min t > MX_TMIN, ties to the lower primitive index; shadow
+// query: any t in (MX_TMIN, tmax).  Two equivalent evaluations (same answer for every ray):
+//  * brute force over the primitive list (structure independent; small scenes, cross-checks);
+//  * this oracle's own binary BVH (median split, fp64 boxes padded far above rounding), used for
+//    large scenes so the C4/C5 workloads can be checked in seconds.  It only skips primitives
+//    whose padded box the ray cannot reach before the current best t, so it returns exactly what
+//    the brute force returns (CPU test: tests/test_oracle_golden.py, bvh vs brute force).
+struct OAccel {
+    struct Node { double lo[3], hi[3]; int left, right, first, count; };   // leaf: left < 0
+    std::vector<Node> nodes;
+    std::vector<int> idx;
+    bool brute = true;
+};
+
+int g_accel_mode = -1;   // -1: BVH above 256 primitives; 0: always brute force; 1: always BVH
+
+void prim_bounds(const Prim& p, double lo[3], double hi[3]) {
+    if (p.kind == 0) {
+        const V3 a = p.v0, b = p.v0 + p.e1, c = p.v0 + p.e2;
+        const double va[3] = {a.x, a.y, a.z}, vb[3] = {b.x, b.y, b.z}, vc[3] = {c.x, c.y, c.z};
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = std::fmin(va[k], std::fmin(vb[k], vc[k]));
+            hi[k] = std::fmax(va[k], std::fmax(vb[k], vc[k]));
+        }
+    } else {
+        const double cc[3] = {p.c.x, p.c.y, p.c.z};
+        for (int k = 0; k < 3; ++k) { lo[k] = cc[k] - p.r; hi[k] = cc[k] + p.r; }
+    }
+    for (int k = 0; k < 3; ++k) {   // padding: 1e-7 of the coordinates' magnitude plus the extent
+        const double pad = 1e-7 * (std::fabs(lo[k]) + std::fabs(hi[k]) + (hi[k] - lo[k])) + 1e-12;
+        lo[k] -= pad;
+        hi[k] += pad;
+    }
+}
+
+int build_node(OAccel& A, std::vector<double>& blo, std::vector<double>& bhi, std::vector<double>& cen, int first,
+               int count) {
+    OAccel::Node nd;
+    for (int k = 0; k < 3; ++k) { nd.lo[k] = INFINITY; nd.hi[k] = -INFINITY; }
+    double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int i = first; i < first + count; ++i) {
+        const int q = A.idx[i];
+        for (int k = 0; k < 3; ++k) {
+            nd.lo[k] = std::fmin(nd.lo[k], blo[3 * q + k]);
+            nd.hi[k] = std::fmax(nd.hi[k], bhi[3 * q + k]);
+            clo[k] = std::fmin(clo[k], cen[3 * q + k]);
+            chi[k] = std::fmax(chi[k], cen[3 * q + k]);
+        }
+    }
+    nd.left = nd.right = -1;
+    nd.first = first;
+    nd.count = count;
+    const int me = (int)A.nodes.size();
+    A.nodes.push_back(nd);
+    if (count <= 4) return me;
+    int ax = 0;
+    for (int k = 1; k < 3; ++k)
+        if (chi[k] - clo[k] > chi[ax] - clo[ax]) ax = k;
+    const int mid = first + count / 2;
+    std::nth_element(A.idx.begin() + first, A.idx.begin() + mid, A.idx.begin() + first + count, [&](int a, int b) {
+        const double ca = cen[3 * a + ax], cb = cen[3 * b + ax];
+        return ca < cb || (ca == cb && a < b);
+    });
+    const int l = build_node(A, blo, bhi, cen, first, mid - first);
+    const int r = build_node(A, blo, bhi, cen, mid, first + count - mid);
+    A.nodes[me].left = l;
+    A.nodes[me].right = r;
+    return me;
+}
+
+void build_accel(const std::vector<Prim>& prims, OAccel& A) {
+    A.brute = g_accel_mode == 0 || (g_accel_mode < 0 && prims.size() <= 256);
+    A.nodes.clear();
+    A.idx.clear();
+    if (A.brute || prims.empty()) { A.brute = true; return; }
+    const int n = (int)prims.size();
+    std::vector<double> blo(3 * (size_t)n), bhi(3 * (size_t)n), cen(3 * (size_t)n);
+    for (int i = 0; i < n; ++i) {
+        prim_bounds(prims[i], &blo[3 * (size_t)i], &bhi[3 * (size_t)i]);
+        for (int k = 0; k < 3; ++k) cen[3 * (size_t)i + k] = 0.5 * (blo[3 * (size_t)i + k] + bhi[3 * (size_t)i + k]);
+    }
+    A.idx.resize((size_t)n);
+    for (int i = 0; i < n; ++i) A.idx[(size_t)i] = i;
+    A.nodes.reserve(2 * (size_t)n / 2 + 8);
+    build_node(A, blo, bhi, cen, 0, n);
+}
+
+// fp64 slab test of a padded box against the ray segment t in [0, tlim]
+bool node_reach(const OAccel::Node& nd, V3 o, V3 d, double tlim) {
+    const double oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z};
+    double tn = 0.0, tf = tlim;
+    for (int k = 0; k < 3; ++k) {
+        if (dd[k] == 0.0) {
+            if (oo[k] < nd.lo[k] || oo[k] > nd.hi[k]) return false;
+            continue;
+        }
+        double t0 = (nd.lo[k] - oo[k]) / dd[k], t1 = (nd.hi[k] - oo[k]) / dd[k];
+        if (t0 > t1) std::swap(t0, t1);
+        tn = std::fmax(tn, t0);
+        tf = std::fmin(tf, t1);
+    }
+    return tn <= tf;
+}
+inline double t_slack(double t) { return std::isinf(t) ? t : t * (1.0 + 1e-9) + 1e-9; }
+
+int mx_closest(const std::vector<Prim>& prims, const OAccel& A, V3 o, V3 d, double& tbest) {
     int best = -1;
     tbest = INFINITY;
-    for (int i = 0; i < (int)prims.size(); ++i) {
-        const double t = mx_prim_t(prims[i], o, d, MX_TMIN);
-        if (t < tbest) { tbest = t; best = i; }   // strict: ties keep the lower index
+    if (A.brute) {
+        for (int i = 0; i < (int)prims.size(); ++i) {
+            const double t = mx_prim_t(prims[i], o, d, MX_TMIN);
+            if (t < tbest) { tbest = t; best = i; }   // strict: ties keep the lower index
+        }
+        return best;
+    }
+    int stack[128], sp = 0;
+    stack[sp++] = 0;
+    while (sp) {
+        const OAccel::Node& nd = A.nodes[stack[--sp]];
+        if (!node_reach(nd, o, d, t_slack(tbest))) continue;
+        if (nd.left < 0) {
+            for (int j = nd.first; j < nd.first + nd.count; ++j) {
+                const int i = A.idx[j];
+                const double t = mx_prim_t(prims[i], o, d, MX_TMIN);
+                if (t < tbest || (t == tbest && i < best)) { tbest = t; best = i; }
+            }
+        } else {
+            stack[sp++] = nd.right;
+            stack[sp++] = nd.left;
+        }
     }
     return best;
 }
-bool mx_occluded(const std::vector<Prim>& prims, V3 o, V3 d, double tmax) {
-    for (const Prim& p : prims) {
-        const double t = mx_prim_t(p, o, d, MX_TMIN);
-        if (t < tmax) return true;
+bool mx_occluded(const std::vector<Prim>& prims, const OAccel& A, V3 o, V3 d, double tmax) {
+    if (A.brute) {
+        for (const Prim& p : prims)
+            if (mx_prim_t(p, o, d, MX_TMIN) < tmax) return true;
+        return false;
+    }
+    int stack[128], sp = 0;
+    stack[sp++] = 0;
+    const double tl = t_slack(tmax);
+    while (sp) {
+        const OAccel::Node& nd = A.nodes[stack[--sp]];
+        if (!node_reach(nd, o, d, tl)) continue;
+        if (nd.left < 0) {
+            for (int j = nd.first; j < nd.first + nd.count; ++j)
+                if (mx_prim_t(prims[A.idx[j]], o, d, MX_TMIN) < tmax) return true;
+        } else {
+            stack[sp++] = nd.right;
+            stack[sp++] = nd.left;
+        }
     }
     return false;
 }
@@ -951,71 +1146,83 @@ void mx_texcoord(const Ent& e, V3 ip, int32_t& x, int32_t& y) {
     } else x = y = 0;   // ExpBox
 }
 
-void pixel_mode_x(const Scene& s, const std::vector<Prim>& prims, const Cam& c, int w, int x, int y,
-                  int spp, int depth, uint64_t seed, double* rgb, int32_t& hit0, int32_t& u0, int32_t& v0,
-                  int32_t& nrays) {
+// One sample of pixel (x, y): its radiance L (before the pixel mean) and the rays it traced.
+void sample_mode_x(const Scene& s, const std::vector<Prim>& prims, const OAccel& A, const Cam& c, int w, int x, int y,
+                   int smp, int spp, int depth, uint64_t seed, V3& Lout, int32_t& hit0, int32_t& u0, int32_t& v0,
+                   long& rays) {
     const uint64_t pix = (uint64_t)y * (uint64_t)w + (uint64_t)x;
+    double jx = 0.0, jy = 0.0;
+    if (spp > 1) { jx = mx_u01(seed, pix, smp, 0xFFFF, 0); jy = mx_u01(seed, pix, smp, 0xFFFF, 1); }
+    const V3 dir0 = (c.top_left - (c.left * ((double)x + jx)) * c.rx) - (c.up * ((double)y + jy)) * c.ry;
+    V3 o = c.pos, d = normalize(dir0);
+    V3 L{0, 0, 0}, T{1, 1, 1};
+    for (int b = 0; b < depth; ++b) {
+        double t;
+        const int pi = mx_closest(prims, A, o, d, t);
+        ++rays;
+        if (pi < 0) break;
+        const Prim& p = prims[pi];
+        const Ent& e = s.ents[p.ent];
+        const V3 P = o + t * d;
+        V3 N = p.kind == 0 ? p.n : normalize(P - p.c);
+        if (!(dot(d, N) < 0)) N = -N;
+        int32_t tu, tv;
+        mx_texcoord(e, P, tu, tv);
+        if (smp == 0 && b == 0) { hit0 = p.ent; u0 = tu; v0 = tv; }
+        const V3 tc = texel(e.mat.color, tu, tv);
+        // local Blinn-Phong with a shadow ray toward the point light
+        const V3 lv = s.light - P;
+        const double ldist = std::sqrt(dot(lv, lv));
+        const V3 Ld = normalize(lv);
+        const bool vis = !mx_occluded(prims, A, P, Ld, ldist);
+        ++rays;
+        const V3 la = tc * e.mat.shader.x;
+        V3 loc = la;
+        if (vis) {
+            const V3 ld = (smax(0.0, dot(N, Ld)) * (tc * 0.5)) * e.mat.shader.y;
+            const V3 bis = normalize(normalize(-d) + Ld);
+            const double sp = mx_pow(smax(0.0, dot(N, bis)), e.mat.spec_pow);
+            const V3 ls = V3{sp, sp, sp} * e.mat.shader.z;
+            loc = (la + ld) + ls;
+        }
+        loc = {smin(loc.x, 1.0), smin(loc.y, 1.0), smin(loc.z, 1.0)};
+        L = L + mul(T, loc);
+        if (b == depth - 1) break;
+        // mirror bounce with probability refl (uniform dim 4): T unchanged, d reflected about N
+        if (e.mat.refl > 0.0 && mx_u01(seed, pix, smp, b, 4) < e.mat.refl) {
+            d = normalize(d - N * (2.0 * dot(d, N)));
+            o = P;
+            continue;
+        }
+        T = mul(T, tc * 0.5);
+        if (T.x == 0.0 && T.y == 0.0 && T.z == 0.0) break;
+        // cosine-weighted direction: concentric disk point + Malley's projection
+        double sx, sy, r2;
+        mx_disk(mx_u01(seed, pix, smp, b, 2), mx_u01(seed, pix, smp, b, 3), sx, sy, r2);
+        const double sz = std::sqrt(1.0 - r2);
+        const double sg = N.z >= 0.0 ? 1.0 : -1.0;   // Duff et al. 2017 orthonormal basis
+        const double aa = -1.0 / (sg + N.z);
+        const double bb = N.x * N.y * aa;
+        const V3 t1{1.0 + sg * N.x * N.x * aa, sg * bb, -sg * N.x};
+        const V3 t2{bb, sg + N.y * N.y * aa, -N.y};
+        d = normalize((t1 * sx + t2 * sy) + N * sz);
+        o = P;
+    }
+    Lout = L;
+}
+
+// pixel = min(sum_s L_s / spp, 1), samples added in order s = 0..spp-1 from +0.  Ls (optional):
+// the samples' radiance, already computed (parallel over samples for small windows).
+void pixel_mode_x(const Scene& s, const std::vector<Prim>& prims, const OAccel& A, const Cam& c, int w, int x, int y,
+                  int spp, int depth, uint64_t seed, double* rgb, int32_t& hit0, int32_t& u0, int32_t& v0,
+                  int32_t& nrays, const V3* Ls = nullptr, long pre_rays = 0) {
     double sum[3] = {0, 0, 0};
     hit0 = -1; u0 = v0 = 0;
-    long rays = 0;
+    long rays = pre_rays;
     for (int smp = 0; smp < spp; ++smp) {
-        double jx = 0.0, jy = 0.0;
-        if (spp > 1) { jx = mx_u01(seed, pix, smp, 0xFFFF, 0); jy = mx_u01(seed, pix, smp, 0xFFFF, 1); }
-        const V3 dir0 = (c.top_left - (c.left * ((double)x + jx)) * c.rx) - (c.up * ((double)y + jy)) * c.ry;
-        V3 o = c.pos, d = normalize(dir0);
-        V3 L{0, 0, 0}, T{1, 1, 1};
-        for (int b = 0; b < depth; ++b) {
-            double t;
-            const int pi = mx_closest(prims, o, d, t);
-            ++rays;
-            if (pi < 0) break;
-            const Prim& p = prims[pi];
-            const Ent& e = s.ents[p.ent];
-            const V3 P = o + t * d;
-            V3 N = p.kind == 0 ? p.n : normalize(P - p.c);
-            if (!(dot(d, N) < 0)) N = -N;
-            int32_t tu, tv;
-            mx_texcoord(e, P, tu, tv);
-            if (smp == 0 && b == 0) { hit0 = p.ent; u0 = tu; v0 = tv; }
-            const V3 tc = texel(e.mat.color, tu, tv);
-            // local Blinn-Phong with a shadow ray toward the point light
-            const V3 lv = s.light - P;
-            const double ldist = std::sqrt(dot(lv, lv));
-            const V3 Ld = normalize(lv);
-            const bool vis = !mx_occluded(prims, P, Ld, ldist);
-            ++rays;
-            const V3 la = tc * e.mat.shader.x;
-            V3 loc = la;
-            if (vis) {
-                const V3 ld = (smax(0.0, dot(N, Ld)) * (tc * 0.5)) * e.mat.shader.y;
-                const V3 bis = normalize(normalize(-d) + Ld);
-                const double sp = mx_powi(smax(0.0, dot(N, bis)), (int)e.mat.spec_pow);
-                const V3 ls = V3{sp, sp, sp} * e.mat.shader.z;
-                loc = (la + ld) + ls;
-            }
-            loc = {smin(loc.x, 1.0), smin(loc.y, 1.0), smin(loc.z, 1.0)};
-            L = L + mul(T, loc);
-            if (b == depth - 1) break;
-            // mirror bounce with probability refl (uniform dim 4): T unchanged, d reflected about N
-            if (e.mat.refl > 0.0 && mx_u01(seed, pix, smp, b, 4) < e.mat.refl) {
-                d = normalize(d - N * (2.0 * dot(d, N)));
-                o = P;
-                continue;
-            }
-            T = mul(T, tc * 0.5);
-            if (T.x == 0.0 && T.y == 0.0 && T.z == 0.0) break;
-            // cosine-weighted direction: concentric disk point + Malley's projection
-            double sx, sy, r2;
-            mx_disk(mx_u01(seed, pix, smp, b, 2), mx_u01(seed, pix, smp, b, 3), sx, sy, r2);
-            const double sz = std::sqrt(1.0 - r2);
-            const double sg = N.z >= 0.0 ? 1.0 : -1.0;   // Duff et al. 2017 orthonormal basis
-            const double aa = -1.0 / (sg + N.z);
-            const double bb = N.x * N.y * aa;
-            const V3 t1{1.0 + sg * N.x * N.x * aa, sg * bb, -sg * N.x};
-            const V3 t2{bb, sg + N.y * N.y * aa, -N.y};
-            d = normalize((t1 * sx + t2 * sy) + N * sz);
-            o = P;
-        }
+        V3 L;
+        if (Ls) L = Ls[smp];
+        else sample_mode_x(s, prims, A, c, w, x, y, smp, spp, depth, seed, L, hit0, u0, v0, rays);
         sum[0] = sum[0] + L.x; sum[1] = sum[1] + L.y; sum[2] = sum[2] + L.z;
     }
     for (int k = 0; k < 3; ++k) rgb[k] = smin(sum[k] / (double)spp, 1.0);
@@ -1028,36 +1235,64 @@ extern "C" {
 
 const char* gio_last_error(void) { return g_err.c_str(); }
 
+void gio_set_accel(int mode) { g_accel_mode = mode < 0 ? -1 : (mode ? 1 : 0); }
+
 int gio_render(const char* scn, int w, int h, int mode, int spp, int depth, uint64_t seed, int x0, int y0,
                int x1, int y1, int threads, double* rgb, int32_t* hit, int32_t* uv, int32_t* ncand,
                int32_t* nnode, uint8_t* q) {
     Scene s;
-    if (!parse(scn, s)) return -1;
+    if (!parse(scn, s, mode != 1)) return -1;
     if (w <= 0 || h <= 0 || x0 < 0 || y0 < 0 || x1 > w || y1 > h || x0 > x1 || y0 > y1) { g_err = "bad window"; return -2; }
     if (mode == 1) {
         if (spp < 1 || depth < 1) { g_err = "mode X needs spp >= 1 and depth >= 1"; return -3; }
         for (const Ent& e : s.ents)
-            if (!(e.mat.spec_pow >= 0 && e.mat.spec_pow <= 64 && e.mat.spec_pow == (double)(int)e.mat.spec_pow)) {
-                g_err = "mode X needs integer specular_power in [0,64]"; return -3;
-            }
-        for (const Ent& e : s.ents)
             if (!(e.mat.refl >= 0.0 && e.mat.refl <= 1.0)) { g_err = "reflectivity must lie in [0, 1]"; return -3; }
     }
     std::vector<Prim> prims;
-    if (mode == 1) build_prims(s, prims);
+    OAccel A;
+    if (mode == 1) { build_prims(s, prims); build_accel(prims, A); }
     const Cam c = make_cam(s, w);
     const int ww = x1 - x0;
     const long npx = (long)ww * (y1 - y0);
 #ifdef _OPENMP
     if (threads > 0) omp_set_num_threads(threads);
 #endif
-#pragma omp parallel for schedule(dynamic, 16)
+    // few pixels with many samples: the samples of each pixel in parallel, summed in order after
+    if (mode == 1 && spp > 1 && npx < 64) {
+        std::vector<V3> Ls((size_t)spp);
+        std::vector<long> nr((size_t)spp);
+        std::vector<int32_t> h0((size_t)spp), uu((size_t)spp), vv((size_t)spp);
+        for (long i = 0; i < npx; ++i) {
+            const int x = x0 + (int)(i % ww), y = y0 + (int)(i / ww);
+#pragma omp parallel for schedule(dynamic, 1)
+            for (int smp = 0; smp < spp; ++smp) {
+                nr[(size_t)smp] = 0;
+                h0[(size_t)smp] = -1; uu[(size_t)smp] = vv[(size_t)smp] = 0;
+                sample_mode_x(s, prims, A, c, w, x, y, smp, spp, depth, seed, Ls[(size_t)smp], h0[(size_t)smp],
+                              uu[(size_t)smp], vv[(size_t)smp], nr[(size_t)smp]);
+            }
+            long rays = 0;
+            for (int smp = 0; smp < spp; ++smp) rays += nr[(size_t)smp];
+            double col[3];
+            int32_t hh, u, v, nc;
+            pixel_mode_x(s, prims, A, c, w, x, y, spp, depth, seed, col, hh, u, v, nc, Ls.data(), rays);
+            hh = h0[0]; u = uu[0]; v = vv[0];
+            if (rgb) { rgb[3 * i] = col[0]; rgb[3 * i + 1] = col[1]; rgb[3 * i + 2] = col[2]; }
+            if (hit) hit[i] = hh;
+            if (uv) { uv[2 * i] = u; uv[2 * i + 1] = v; }
+            if (ncand) ncand[i] = nc;
+            if (nnode) nnode[i] = 0;
+            if (q) quantize(col, q + 3 * i);
+        }
+        return 0;
+    }
+#pragma omp parallel for schedule(dynamic, 1)
     for (long i = 0; i < npx; ++i) {
         const int x = x0 + (int)(i % ww), y = y0 + (int)(i / ww);
         double col[3];
         int32_t hh, u, v, nc = 0, nn = 0;
         if (mode == 0) pixel_mode_r(s, c, x, y, col, hh, u, v, nc, nn);
-        else { pixel_mode_x(s, prims, c, w, x, y, spp, depth, seed, col, hh, u, v, nc); nn = 0; }
+        else { pixel_mode_x(s, prims, A, c, w, x, y, spp, depth, seed, col, hh, u, v, nc); nn = 0; }
         if (rgb) { rgb[3 * i] = col[0]; rgb[3 * i + 1] = col[1]; rgb[3 * i + 2] = col[2]; }
         if (hit) hit[i] = hh;
         if (uv) { uv[2 * i] = u; uv[2 * i + 1] = v; }

@@ -7,7 +7,7 @@
 // Mode R (mode=0): the reference's semantics bit for bit, pinned against
 //   golden vectors produced by the compiled reference (oracle/_ref/ref_harness).
 // Mode X (mode=1): the build-defined depth/spp integrator specified in DESIGN.md §"Mode X";
-//   brute-force nearest hit over all primitives (structure independent).
+//   nearest hit over all primitives (brute force, or an equivalent padded fp64 BVH for large scenes).
 #pragma once
 #include <stddef.h>
 #include <stdint.h>
@@ -39,6 +39,10 @@ int gio_rays(const char* scn, int n, const double* rays, int32_t* out_hit, doubl
 
 // ExpBox node test over n x (min[3], max[3], origin[3], dir[3]) records.
 int gio_boxes(int n, const double* recs, int32_t* out);
+
+// Mode X closest-hit / shadow queries: -1 (default) = this oracle's BVH above 256 primitives,
+// brute force below; 0 = brute force always; 1 = BVH always.  Same results either way (tested).
+void gio_set_accel(int mode);
 
 const char* gio_last_error(void);
 

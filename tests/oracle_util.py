@@ -49,6 +49,7 @@ def oracle():
         lib.gio_rays.argtypes = [ctypes.c_char_p, ctypes.c_int, f64p, i32p, f64p, i32p]
         lib.gio_boxes.argtypes = [ctypes.c_int, f64p, i32p]
         lib.gio_last_error.restype = ctypes.c_char_p
+        lib.gio_set_accel.argtypes = [ctypes.c_int]
         _oracle = lib
     return _oracle
 
@@ -71,6 +72,11 @@ def oracle_render(scn: str, w: int, h: int, mode: int = 0, spp: int = 1, depth: 
     if rc != 0:
         raise RuntimeError(f"gio_render failed ({rc}): {lib.gio_last_error().decode()}")
     return out
+
+
+def oracle_accel(mode: int) -> None:
+    """Mode X queries: -1 default (BVH above 256 primitives), 0 brute force, 1 BVH."""
+    oracle().gio_set_accel(mode)
 
 
 def oracle_tree(scn: str) -> str:

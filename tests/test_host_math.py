@@ -90,3 +90,15 @@ def test_host_code_under_sanitizers(tmp_path):
             assert "mismatches 0" in out.stdout
         else:
             assert out.stdout.count(" rc 0") == 2 * len(scns)
+
+
+def test_mode_x_pow_any_specular_power(tmp_path):
+    """gi_math.h mx_pow -- Mode X's x^p for any Material::specular_power (material.h:29 is a double):
+    integer p in [0, 64] by square-and-multiply (unchanged), otherwise the exp/ln series; within a
+    few ulps of libm pow (relative error grows with |p ln x|, the exponent's own amplification)."""
+    exe = str(tmp_path / "mxpow")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I" + os.path.join(U.ROOT, "2019global_amd", "csrc"),
+                    "-o", exe, os.path.join(U.ROOT, "tests", "cpp", "mxpow_check.cpp")], check=True)
+    out = subprocess.run([exe], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout
+    assert "bad 0" in out.stdout

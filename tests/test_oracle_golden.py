@@ -47,6 +47,11 @@ def texel_ub_mask(hit, uv):
     return (hit >= 0) & ((f < 0) | (f >= 1024))
 
 
+# pixels excluded as texel UB, exactly, per fixture (only the single-ExpSphere frame has any: its
+# latitude coordinate goes negative below the equator, entities.h:549-571)
+TEXEL_UB_PIXELS = {"only_expsphere_96x96": 154}
+
+
 def test_frames_present():
     assert len(FRAMES) >= 6, FRAMES
 
@@ -60,7 +65,7 @@ def test_mode_r_bit_exact_vs_reference_golden(name):
         pytest.skip("large")
     o = render_pixels(sc.to_scn(), meta["w"], meta["h"], z["x"], z["y"])
     ok = ~texel_ub_mask(z["hit"], z["uv"])
-    assert ok.mean() > 0.9
+    assert int((~ok).sum()) == TEXEL_UB_PIXELS.get(name, 0), "texel-UB pixel count drifted"
     assert U.bits_equal(o["rgb"], z["rgb"])[ok].all(), "fp64 radiance differs from the reference"
     assert (o["hit"] == z["hit"]).all()
     assert (o["uv"] == z["uv"]).all()
@@ -155,3 +160,36 @@ def test_live_reference_random_scene():
     assert U.bits_equal(r["rgb"], o["rgb"])[ok].all()
     assert (r["hit"] == o["hit"]).all() and (r["nnode"] == o["nnode"]).all()
     assert U.ref_tree(scn) == U.oracle_tree(scn)
+
+
+@pytest.mark.parametrize("scene,w,h,spp,depth,win", [
+    ("soup1000", 64, 48, 2, 8, None), ("zoo", 48, 48, 2, 4, None), ("cornell", 48, 40, 3, 5, None),
+    ("cornell_mirror", 40, 40, 2, 6, None), ("main", 40, 40, 2, 3, None),
+    ("soup100000", 1920, 1080, 1, 8, (956, 956, 964, 964))])
+def test_oracle_mode_x_bvh_equals_brute_force(scene, w, h, spp, depth, win):
+    """The oracle's Mode X closest / shadow queries by its own BVH (used for the 100k-soup C4/C5
+    checks) return exactly the brute-force answer over all primitives: same frames bit for bit and
+    the same ray counts."""
+    scn = S.named_scene(scene).to_scn()
+    out = []
+    try:
+        for m in (0, 1):
+            U.oracle_accel(m)
+            out.append(U.oracle_render(scn, w, h, mode=1, spp=spp, depth=depth, seed=7, window=win))
+    finally:
+        U.oracle_accel(-1)
+    assert U.bits_equal(out[0]["rgb"], out[1]["rgb"]).all()
+    assert (out[0]["ncand"] == out[1]["ncand"]).all()
+    assert (out[0]["hit"] == out[1]["hit"]).all()
+
+
+def test_oracle_mode_x_sample_parallel_window_equals_pixel_loop():
+    """Small windows with many samples run the samples of a pixel in parallel (summed in order
+    afterwards): the same pixels as the pixel-parallel loop over a larger window."""
+    scn = S.cornell_scene().to_scn()
+    a = U.oracle_render(scn, 64, 48, mode=1, spp=33, depth=4, seed=5, window=(20, 20, 28, 28))    # 64 px: pixel loop
+    b = U.oracle_render(scn, 64, 48, mode=1, spp=33, depth=4, seed=5, window=(22, 22, 25, 25))    # 9 px: sample loop
+    aa = a["rgb"].reshape(8, 8, 3)[2:5, 2:5].reshape(-1, 3)
+    assert U.bits_equal(aa, b["rgb"]).all()
+    assert (a["ncand"].reshape(8, 8)[2:5, 2:5].reshape(-1) == b["ncand"]).all()
+    assert (a["hit"].reshape(8, 8)[2:5, 2:5].reshape(-1) == b["hit"]).all()
