@@ -5,7 +5,7 @@ Host-side mirror of the reference's render API over the C-ABI in ``include/gi.h`
   reference (C++ header-only)                         here
   ---------------------------------------------------  ------------------------------------------
   Camera(pos, lookAt, focal)        camera.h:8-10      Camera(pos, look_at, focal)
-  Octree(min, max) / push_back(e)   octree.h:115,121   Octree(min, max) / push_back(e)
+  Octree(min, max) / push_back(e)   octree.h:14,20   Octree(min, max) / push_back(e)
   ImpSphere / ImpTriangle / ExpQuad entities.h:45,138,581  same names and constructor arguments
   Material(color[, shader]), .specular_power           Material(color, shader, specular_power)
   RayTracer(camera, light)          raytracer.h:18     RayTracer(camera, light)
@@ -17,7 +17,9 @@ Host-side mirror of the reference's render API over the C-ABI in ``include/gi.h`
 render raises ``GIError``.
 
 Lower-level handles for benchmarks and multi-GPU: ``DeviceScene`` (a scene resident in HBM) with
-``render_device`` into caller-owned device buffers on a HIP stream.
+``render_device`` into caller-owned device buffers on a HIP stream; ``MultiScene`` (several GPUs of
+one process, RCCL gather; ``RayTracer`` uses it when ``GI_DEVICES`` lists more than one device);
+``Octree.intersect`` (the reference's public candidate query, on the host).
 """
 from __future__ import annotations
 
@@ -34,7 +36,7 @@ __all__ = [
     "GIError", "lib", "Camera", "Material", "Octree", "ImpSphere", "ImpTriangle", "ExpQuad",
     "ExpSphere", "ExpCube", "ExpCone", "ExpRectangle", "ExpBox",
     "RayTracer", "DeviceScene", "MODE_R", "MODE_X", "STAT_RAYS", "STAT_NODES", "STAT_PRIMS",
-    "STAT_PIXELS", "TILE",
+    "STAT_PIXELS", "TILE", "MultiScene", "devices_from_env",
 ]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -49,7 +51,7 @@ STAT_X_ITERS, STAT_X_TRAV, STAT_X_HANDLE, STAT_X_HLANES, STAT_X_HCLOSE, STAT_X_H
 STAT_X_CYC_TRAV, STAT_X_CYC_HIT, STAT_X_CYC_NEXT, STAT_X_CYC_ALL = 11, 12, 13, 14
 STATS_N = 16
 TILE = 8
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class GIError(RuntimeError):
@@ -96,7 +98,8 @@ TILE_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ct
 
 EXPORTS = ["gi_abi_version", "gi_last_error", "gi_camera_init", "gi_scene_create", "gi_scene_destroy",
            "gi_scene_get_info", "gi_render", "gi_render_device", "gi_shard_tiles", "gi_unshard_device",
-           "gi_trace_ray", "gi_kat_expbox", "gi_scene_kernel_ms"]
+           "gi_trace_ray", "gi_kat_expbox", "gi_scene_kernel_ms", "gi_octree_create", "gi_octree_destroy",
+           "gi_octree_intersect", "gi_multi_create", "gi_multi_destroy", "gi_multi_info", "gi_multi_render", "gi_device_count"]
 
 _lib = None
 _lock = threading.Lock()
@@ -133,6 +136,18 @@ def lib():
         L.gi_trace_ray.argtypes = [vp, dp, dp, dp, ctypes.POINTER(Hit), dp]
         L.gi_kat_expbox.argtypes = [i32, dp, ctypes.POINTER(ctypes.c_int32)]
         L.gi_scene_kernel_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int64)]
+        L.gi_octree_create.argtypes = [ctypes.POINTER(SceneDesc), ctypes.POINTER(vp)]
+        L.gi_octree_destroy.argtypes = [vp]
+        L.gi_octree_destroy.restype = None
+        L.gi_octree_intersect.argtypes = [vp, dp, dp, ctypes.POINTER(ctypes.c_int32), ctypes.c_int64,
+                                          ctypes.POINTER(ctypes.c_int64)]
+        L.gi_multi_create.argtypes = [ctypes.POINTER(SceneDesc), i32, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(vp)]
+        L.gi_multi_destroy.argtypes = [vp]
+        L.gi_multi_destroy.restype = None
+        L.gi_multi_info.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                    ctypes.POINTER(ctypes.c_int)]
+        L.gi_multi_render.argtypes = [vp, ctypes.POINTER(CameraDesc), dp, i32, i32, ctypes.POINTER(Opts), dp,
+                                      ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_int), TILE_CB, vp]
         if L.gi_abi_version() != ABI_VERSION:
             raise GIError(f"libgi ABI {L.gi_abi_version()} != {ABI_VERSION}")
         _lib = L
@@ -256,16 +271,53 @@ class ExpBox(_Entity):
 
 
 class Octree:
-    """Octree(min, max) + push_back (octree.h:115-144).  The tree itself is built by libgi from the
+    """Octree(min, max) + push_back (octree.h:14-43).  The tree itself is built by libgi from the
     push order (gi_scene_create), exactly as the reference builds it."""
 
     def __init__(self, min=(-20, -20, -20), max=(20, 20, 20)):
         self.min = tuple(float(v) for v in min)
         self.max = tuple(float(v) for v in max)
         self.entities = []
+        self.generation = 0       # bumped by push_back: a RayTracer re-uploads a changed scene
+        self._host = None         # gi_octree for intersect(), rebuilt when the generation changes
+        self._host_gen = -1
 
     def push_back(self, e: _Entity) -> None:
         self.entities.append(e)
+        self.generation += 1
+
+    def intersect(self, origin, direction) -> list:
+        """Octree::intersect(Ray(origin, dir)) (octree.h:46-68 -> Node::intersect :132-155): the
+        candidate list -- entities in DFS order over children 0..7, duplicates kept -- from libgi's
+        host copy of the reference octree (gi_octree_intersect; no device needed).  `direction` is
+        normalised first, as the reference's Ray constructor does (ray.h:6)."""
+        L = lib()
+        if self._host is None or self._host_gen != self.generation:
+            self._close_host()
+            d, keep = self._scene_desc()
+            h = ctypes.c_void_p()
+            _check(L.gi_octree_create(ctypes.byref(d), ctypes.byref(h)), "gi_octree_create")
+            del keep
+            self._host, self._host_gen = h, self.generation
+        dv = np.asarray(direction, np.float64)
+        dv = dv * (1.0 / np.sqrt((dv[0] * dv[0] + dv[1] * dv[1]) + dv[2] * dv[2]))   # glm::normalize
+        n = ctypes.c_int64()
+        _check(L.gi_octree_intersect(self._host, _d3(origin), _d3(dv), None, 0, ctypes.byref(n)), "gi_octree_intersect")
+        out = (ctypes.c_int32 * max(1, n.value))()
+        _check(L.gi_octree_intersect(self._host, _d3(origin), _d3(dv), out, n.value, ctypes.byref(n)),
+               "gi_octree_intersect")
+        return [self.entities[i] for i in out[:n.value]]
+
+    def _close_host(self):
+        if self._host is not None and self._host.value:
+            lib().gi_octree_destroy(self._host)
+        self._host = None
+
+    def __del__(self):
+        try:
+            self._close_host()
+        except Exception:
+            pass
 
     @classmethod
     def from_scene(cls, s: "_scenes.Scene") -> "Octree":
@@ -399,6 +451,63 @@ class DeviceScene:
         return hit, tuple(rgb)
 
 
+def devices_from_env(default=None):
+    """GI_DEVICES="0,1,2,3" (device per shard; repeats allowed) or "all"; None when unset."""
+    v = os.environ.get("GI_DEVICES")
+    if not v:
+        return default
+    if v.strip() == "all":
+        import torch
+        return list(range(torch.cuda.device_count()))
+    return [int(t) for t in v.split(",") if t.strip()]
+
+
+class MultiScene:
+    """RayTracer::run over several GPUs of this process (gi_multi_*): a scene replica per device,
+    8x8 tiles dealt round-robin over the shards, packed tiles gathered to devices[0] by RCCL
+    send/recv over xGMI, bit-identical to a one-device render."""
+
+    def __init__(self, octree: Octree, devices: Sequence[int]):
+        L = lib()
+        d, keep = octree._scene_desc()
+        devs = (ctypes.c_int * len(devices))(*[int(x) for x in devices])
+        h = ctypes.c_void_p()
+        _check(L.gi_multi_create(ctypes.byref(d), len(devices), devs, ctypes.byref(h)), "gi_multi_create")
+        self._h = h
+        del keep
+
+    @classmethod
+    def from_scene(cls, s: "_scenes.Scene", devices: Sequence[int]) -> "MultiScene":
+        return cls(Octree.from_scene(s), devices)
+
+    def info(self) -> dict:
+        a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _check(lib().gi_multi_info(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), "gi_multi_info")
+        return {"shards": a.value, "devices": b.value, "rccl": bool(c.value)}
+
+    def render(self, cam: Camera, light, w: int, h: int, mode=MODE_R, spp=1, depth=1, seed=0, band_rows=0,
+               cancel: Optional[ctypes.c_int] = None, callback=None):
+        rgb, rgb8 = np.zeros((h, w, 3), np.float64), np.zeros((h, w, 3), np.uint8)
+        cb = TILE_CB(callback) if callback is not None else TILE_CB()
+        o = DeviceScene.opts(mode, spp, depth, seed, band_rows=band_rows)
+        _check(lib().gi_multi_render(self._h, ctypes.byref(cam._c), _d3(light), w, h, ctypes.byref(o),
+                                     rgb.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                     rgb8.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                                     ctypes.byref(cancel) if cancel is not None else None, cb, None), "gi_multi_render")
+        return rgb, rgb8
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) and self._h.value:
+            lib().gi_multi_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def kat_expbox(recs: np.ndarray) -> np.ndarray:
     """Device ExpBox node test over (min, max, origin, dir) records (gi_kat_expbox)."""
     recs = np.ascontiguousarray(recs, np.float64)
@@ -450,6 +559,7 @@ class RayTracer:
     def setScene(self, scene: Octree) -> None:
         self._scene = scene
         self._dev = None   # rebuilt lazily on the next run()
+        self._dev_gen = -1
 
     def running(self) -> bool:
         return self._cancel.value == 0
@@ -467,8 +577,11 @@ class RayTracer:
         self._image = Image(np.zeros((h, w, 3), np.uint8), np.zeros((h, w, 3)))   # raytracer.h:25
         if self._scene is None:
             raise GIError("setScene() was not called")
-        if self._dev is None:
-            self._dev = DeviceScene(self._scene)
+        # the reference reads the live octree on every run (raytracer.h:45): re-upload after push_back
+        if self._dev is None or getattr(self, "_dev_gen", -1) != self._scene.generation:
+            devs = devices_from_env()
+            self._dev = MultiScene(self._scene, devs) if devs and len(devs) > 1 else DeviceScene(self._scene)
+            self._dev_gen = self._scene.generation
         img = self._image
 
         def on_band(_user, y0, rows, p8, pf):
@@ -480,7 +593,8 @@ class RayTracer:
         rgb8 = np.zeros((h, w, 3), np.uint8)
         o = DeviceScene.opts(MODE_R, band_rows=self.band_rows)
         cb = TILE_CB(on_band)
-        rc = lib().gi_render(self._dev._h, ctypes.byref(self._camera._c), _d3(self._light), w, h, ctypes.byref(o),
+        fn = lib().gi_multi_render if isinstance(self._dev, MultiScene) else lib().gi_render
+        rc = fn(self._dev._h, ctypes.byref(self._camera._c), _d3(self._light), w, h, ctypes.byref(o),
                              rgb.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
                              rgb8.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), ctypes.byref(self._cancel), cb, None)
         if rc not in (0, -4):   # -4: stopped, partial frame like the reference's loop exit

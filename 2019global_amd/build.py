@@ -20,9 +20,9 @@ OUT = os.path.join(HERE, "libgi.so")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = "gfx950"
 
-HOST_SRCS = ["gi_build.cpp", "gi_bvh.cpp", "gi_capi.cpp"]
+HOST_SRCS = ["gi_build.cpp", "gi_bvh.cpp", "gi_capi.cpp", "gi_multi.cpp"]
 DEV_SRCS = ["gi_kernels.hip"]
-HEADERS = ["gi_math.h", "gi_scene.h"]
+HEADERS = ["gi_math.h", "gi_scene.h", "gi_internal.h"]
 
 COMMON = ["-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", f"-I{INCLUDE}", f"-I{CSRC}"]
 
@@ -65,7 +65,7 @@ def build(verbose: bool = False, force: bool = False, variant: str = "", hip_def
                   "-munsafe-fp-atomics", "-c", src, "-o", obj], verbose)
         objs.append(obj)
     if force or _stale(out, objs):
-        _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-o", out, *objs, f"-L{ROCM}/lib", "-lamdhip64"], verbose)
+        _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-o", out, *objs, f"-L{ROCM}/lib", "-lamdhip64", "-ldl"], verbose)
         for leftover in glob.glob(out + ".0.*"):   # hipcc's unbundling temporaries
             os.remove(leftover)
     return out

@@ -10,7 +10,7 @@
 //   ExpCone     entities.h:823-899 (fixed axis (-1,0,-10), fp32 glm::mat3 rotations, 50 sectors)
 //   ExpRectangle entities.h:310-340 (t1 = (p1,p2,p3), t2 = (p1,p2,-p3): p4 = -p3, A.4)
 //   ExpBox      entities.h:381-446 (6 faces x (t1, t2 with the third corner negated))
-// then pushed into the reference octree with Octree::push_back semantics (octree.h:121-230,
+// then pushed into the reference octree with Octree::push_back semantics (octree.h:20-129,
 // bbox.h:25-39), including the silent drop (A.14) and entities kept only at the split node (A.6).
 #include <algorithm>
 #include <cmath>
@@ -292,7 +292,7 @@ struct RBuild {
     std::vector<N> nodes;
     const std::vector<BEnt>* ents;
 
-    void partition(int ni) {   // octree.h:176-211
+    void partition(int ni) {   // octree.h:75-110
         if (nodes[ni].child0 >= 0) return;
         const V3 mn = nodes[ni].mn, mx = nodes[ni].mx;
         const V3 mid = (mn + mx) * 0.5;
@@ -318,7 +318,7 @@ struct RBuild {
         }
         nodes[ni].child0 = c0;
     }
-    void push_obj(int ni, int32_t e) {   // octree.h:216-230
+    void push_obj(int ni, int32_t e) {   // octree.h:115-129
         nodes[ni].ents.push_back(e);
         partition(ni);
         if (nodes[ni].child0 < 0) return;
@@ -495,7 +495,7 @@ bool build_host_scene(const gi_scene_desc& desc, HostScene& hs, std::string& err
     rb.nodes.push_back(root);
     hs.n_dropped = 0;
     for (int32_t i = 0; i < desc.n_entities; ++i) {
-        if (!bb_overlap(rb.nodes[0].mn, rb.nodes[0].mx, ents[i].bmin, ents[i].bmax)) { ++hs.n_dropped; continue; }   // octree.h:123-125
+        if (!bb_overlap(rb.nodes[0].mn, rb.nodes[0].mx, ents[i].bmin, ents[i].bmax)) { ++hs.n_dropped; continue; }   // octree.h:22-24
         rb.push_obj(0, i);
     }
     const size_t nn = rb.nodes.size();

@@ -1,26 +1,30 @@
 // gi_capi.cpp — the extern "C" boundary (include/gi.h).  Host-side only: validates arguments,
 // builds the scene (gi_build.cpp), owns its HBM copy, and launches the gfx950 kernels
-// (gi_kernels.hip).  There is no CPU rendering path: without a gfx950 device every call fails.
+// (gi_kernels.hip).  There is no CPU rendering path: without a gfx950 device every render fails.
+// No exception crosses the boundary: every entry point that can allocate runs inside guard(),
+// which maps std::bad_alloc to GI_ERR_NOMEM and anything else to GI_ERR_INTERNAL.
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <memory>
+#include <mutex>
+#include <new>
 #include <string>
 #include <vector>
 
 #include "gi.h"
+#include "gi_internal.h"
 #include "gi_scene.h"
 
 namespace gi {
-struct CamDev {
-    V3 pos, up, left, top_left;
-    double rx, ry;
-};
 bool build_host_scene(const gi_scene_desc& desc, HostScene& hs, std::string& err);
 long long shard_tiles(int w, int h, int shard_count);
-hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w, int h, int y0, const gi_opts& o,
-                         double* rgb, uint8_t* rgb8, const XScratch& xs, KTimer* kt, hipStream_t stream);
+hipError_t x_launch_config(const DevScene& sc, int device, XLaunchCfg& cfg);
+hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev& cam, V3 light, int w, int h, int y0,
+                         const gi_opts& o, double* rgb, uint8_t* rgb8, const XScratch& xs, KTimer* kt,
+                         hipStream_t stream);
 hipError_t launch_unshard(int w, int h, int shard_count, const double* packed, const uint8_t* packed8, double* rgb,
                           uint8_t* rgb8, hipStream_t stream);
 hipError_t launch_trace_ray(const DevScene& sc, V3 o, V3 d, V3 light, int32_t* out_i, double* out_d, hipStream_t stream);
@@ -48,23 +52,42 @@ struct HostPath {
 struct gi_scene {
     HostScene host;
     DevScene dev;
+    XLaunchCfg xcfg;   // Mode X launch configuration on this scene's device
     std::vector<void*> allocs;
-    XScratch xs;   // Mode X work list + per-sample radiance, grown on demand (one render in flight per scene)
-    KTimer kt;     // GI_FLAG_TIME events
-    HostPath hp;   // gi_render's band pipeline (streams, device band slots, pinned staging)
+    XScratch xs;       // Mode X work list + per-sample radiance, grown on demand
+    KTimer kt;         // GI_FLAG_TIME events
+    HostPath hp;       // gi_render's band pipeline (streams, device band slots, pinned staging)
+    // every render launch of this scene waits on the device for the previous one (they share xs
+    // and the work counters), whatever stream each is issued on
+    hipEvent_t last = nullptr;
+    bool launched = false;
+    std::mutex mu;     // host-side calls on one scene are serialised
     int device = -1;
     int64_t bytes = 0;
+};
+
+struct gi_octree {
+    HostScene host;
 };
 
 namespace {
 thread_local std::string g_err;
 
-int fail(int code, const std::string& msg) {
-    g_err = msg;
+int fail(int code, const char* msg) noexcept {
+    try {
+        g_err = msg;
+    } catch (...) {
+        // the message is best effort; the status code is what the caller acts on
+    }
     return code;
 }
-int hip_fail(hipError_t e, const char* what) {
-    return fail(GI_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+int fail(int code, const std::string& msg) noexcept { return fail(code, msg.c_str()); }
+int hip_fail(hipError_t e, const char* what) noexcept {
+    try {
+        return fail(GI_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+    } catch (...) {
+        return GI_ERR_DEVICE;
+    }
 }
 
 template <typename T>
@@ -82,31 +105,6 @@ hipError_t upload(gi_scene* s, const std::vector<T>& v, const T** out) {
     }
     *out = static_cast<const T*>(p);
     return hipSuccess;
-}
-
-// raytracer.h:26-30: camera basis and the frame's top-left (vertical offset uses w, SURVEY A.12)
-CamDev make_cam(const gi_camera& c, int w) {
-    CamDev d;
-    d.pos = v3(c.pos[0], c.pos[1], c.pos[2]);
-    d.up = v3(c.up[0], c.up[1], c.up[2]);
-    const V3 fwd = v3(c.forward[0], c.forward[1], c.forward[2]);
-    d.rx = 0.0002;
-    d.ry = 0.0002;
-    d.left = normalize(cross(d.up, fwd));
-    d.top_left = (((d.pos + c.focal * fwd) + ((d.left * (double)w) * 0.5) * d.rx) + ((d.up * (double)w) * 0.5) * d.ry) - d.pos;
-    return d;
-}
-
-int check_opts(const gi_scene* s, int w, int h, const gi_opts* o) {
-    if (!s || !o) return fail(GI_ERR_ARG, "null scene or opts");
-    if (w <= 0 || h <= 0 || (int64_t)w * h > (int64_t)1 << 34) return fail(GI_ERR_ARG, "bad frame size");
-    if (o->mode != GI_MODE_R && o->mode != GI_MODE_X) return fail(GI_ERR_ARG, "bad mode");
-    if (o->shard_count < 1 || o->shard_index < 0 || o->shard_index >= o->shard_count) return fail(GI_ERR_ARG, "bad shard");
-    if (o->mode == GI_MODE_X) {
-        if (o->spp < 1 || o->depth < 1 || o->depth > 0xFFFF) return fail(GI_ERR_ARG, "mode X needs spp >= 1, 1 <= depth <= 65535");
-    }
-    if ((o->flags & GI_FLAG_STATS) && !o->stats) return fail(GI_ERR_ARG, "GI_FLAG_STATS without stats buffer");
-    return GI_OK;
 }
 
 // Mode X work buffers for a frame of w x h pixels cut into this call's shard (k_x_classify's list,
@@ -169,6 +167,20 @@ int ensure_timer(gi_scene* s, const gi_opts* o) {
     return GI_OK;
 }
 
+// One render launch of scene s on `stream`, ordered behind the scene's previous launch.
+int issue_render(gi_scene* s, const CamDev& cd, V3 light, int w, int h, int y0, const gi_opts& o, double* d_rgb,
+                 uint8_t* d_rgb8, hipStream_t stream, bool timer) {
+    hipError_t e = hipSuccess;
+    if (!s->last && (e = hipEventCreateWithFlags(&s->last, hipEventDisableTiming)) != hipSuccess)
+        return hip_fail(e, "hipEventCreate");
+    if (s->launched && (e = hipStreamWaitEvent(stream, s->last, 0)) != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
+    e = launch_render(s->dev, s->xcfg, cd, light, w, h, y0, o, d_rgb, d_rgb8, s->xs, timer ? &s->kt : nullptr, stream);
+    if (e != hipSuccess) return hip_fail(e, "render launch");
+    if ((e = hipEventRecord(s->last, stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+    s->launched = true;
+    return GI_OK;
+}
+
 void free_hostpath_buffers(HostPath& hp) {
     for (int i = 0; i < HostPath::kSlots; i++) {
         (void)hipFree(hp.d_rgb[i]);
@@ -216,22 +228,201 @@ int ensure_hostpath(gi_scene* s, size_t px, int slots) {
     return GI_OK;
 }
 
-int bind_device(const gi_scene* s) {
+void destroy_scene(gi_scene* s) noexcept {
+    if (!s) return;
+    if (s->device >= 0) (void)hipSetDevice(s->device);
+    HostPath& hp = s->hp;
+    if (hp.render) (void)hipStreamSynchronize(hp.render);
+    if (hp.copy) (void)hipStreamSynchronize(hp.copy);
+    if (s->last) (void)hipEventSynchronize(s->last);
+    for (void* p : s->allocs) (void)hipFree(p);
+    (void)hipFree(s->xs.list);
+    (void)hipFree(s->xs.part);
+    for (int i = 0; i < KTimer::kRing; i++) {
+        if (s->kt.ev0[i]) (void)hipEventDestroy(static_cast<hipEvent_t>(s->kt.ev0[i]));
+        if (s->kt.ev1[i]) (void)hipEventDestroy(static_cast<hipEvent_t>(s->kt.ev1[i]));
+    }
+    free_hostpath_buffers(hp);
+    for (int i = 0; i < HostPath::kSlots; i++) {
+        if (hp.rendered[i]) (void)hipEventDestroy(hp.rendered[i]);
+        if (hp.copied[i]) (void)hipEventDestroy(hp.copied[i]);
+    }
+    if (hp.render) (void)hipStreamDestroy(hp.render);
+    if (hp.copy) (void)hipStreamDestroy(hp.copy);
+    if (s->last) (void)hipEventDestroy(s->last);
+    delete s;
+}
+
+// host-side reference octree query: Octree::intersect -> Node::intersect (octree.h:46-68, 132-155)
+void octree_query(const HostScene& h, int ni, V3 o, V3 d, std::vector<int32_t>& out) {
+    const RNode& nd = h.rnodes[(size_t)ni];
+    if (nd.child0 < 0) {   // leaf: a copy of its list (octree.h:133-135)
+        out.insert(out.end(), h.leaf_ents.begin() + nd.ent_off, h.leaf_ents.begin() + nd.ent_off + nd.ent_cnt);
+        return;
+    }
+    for (int c = 0; c < 8; ++c) {   // children 0..7 (octree.h:139-152)
+        const RNode& ch = h.rnodes[(size_t)nd.child0 + c];
+        if (ch.ent_cnt == 0) continue;   // octree.h:140
+        if (box_hit(ld3(ch.mn), ld3(ch.mx), o, d)) octree_query(h, nd.child0 + c, o, d, out);
+    }
+}
+
+}  // namespace
+
+// ---- internal entry points shared with gi_multi.cpp (gi_internal.h) -------------------------
+namespace gi {
+
+int error(int code, const std::string& msg) noexcept { return fail(code, msg); }
+int hip_error(hipError_t e, const char* what) noexcept { return hip_fail(e, what); }
+
+int bind_device(int device) {
     int cur = -1;
     hipError_t e = hipGetDevice(&cur);
     if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
-    if (cur != s->device) {
-        e = hipSetDevice(s->device);
+    if (cur != device) {
+        e = hipSetDevice(device);
         if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
     }
     return GI_OK;
 }
-}  // namespace
+
+int check_device(int dev) {
+    hipDeviceProp_t prop;
+    const hipError_t e = hipGetDeviceProperties(&prop, dev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(GI_ERR_DEVICE, std::string("device ") + std::to_string(dev) + " is " + prop.gcnArchName +
+                                       ", libgi is built for gfx950 only");
+    return GI_OK;
+}
+
+// raytracer.h:26-30: camera basis and the frame's top-left (vertical offset uses w, SURVEY A.12)
+CamDev make_cam(const gi_camera& c, int w) {
+    CamDev d;
+    d.pos = v3(c.pos[0], c.pos[1], c.pos[2]);
+    d.up = v3(c.up[0], c.up[1], c.up[2]);
+    const V3 fwd = v3(c.forward[0], c.forward[1], c.forward[2]);
+    d.rx = 0.0002;
+    d.ry = 0.0002;
+    d.left = normalize(cross(d.up, fwd));
+    d.top_left = (((d.pos + c.focal * fwd) + ((d.left * (double)w) * 0.5) * d.rx) + ((d.up * (double)w) * 0.5) * d.ry) - d.pos;
+    return d;
+}
+
+int check_opts(int w, int h, const gi_opts* o) {
+    if (!o) return fail(GI_ERR_ARG, "null opts");
+    if (w <= 0 || h <= 0 || (int64_t)w * h > (int64_t)1 << 34) return fail(GI_ERR_ARG, "bad frame size");
+    if (o->mode != GI_MODE_R && o->mode != GI_MODE_X) return fail(GI_ERR_ARG, "bad mode");
+    if (o->shard_count < 1 || o->shard_index < 0 || o->shard_index >= o->shard_count) return fail(GI_ERR_ARG, "bad shard");
+    if (o->mode == GI_MODE_X && (o->spp < 1 || o->depth < 1 || o->depth > 0xFFFF))
+        return fail(GI_ERR_ARG, "mode X needs spp >= 1, 1 <= depth <= 65535");
+    if ((o->flags & GI_FLAG_STATS) && !o->stats) return fail(GI_ERR_ARG, "GI_FLAG_STATS without stats buffer");
+    return GI_OK;
+}
+
+int band_rows_of(const gi_opts* o, int h) {
+    int band = o->band_rows > 0 ? o->band_rows : h;
+    band = ((band + GI_TILE - 1) / GI_TILE) * GI_TILE;
+    return std::min(band, ((h + GI_TILE - 1) / GI_TILE) * GI_TILE);
+}
+
+// Builds the scene on the host and uploads it to `device` (made current).
+int scene_create_on(const gi_scene_desc* desc, int device, gi_scene** out) {
+    *out = nullptr;
+    int rc = bind_device(device);
+    if (rc || (rc = check_device(device))) return rc;
+    std::unique_ptr<gi_scene, void (*)(gi_scene*)> s(new gi_scene(), [](gi_scene* p) { destroy_scene(p); });
+    s->device = device;
+    std::string err;
+    if (!build_host_scene(*desc, s->host, err)) return fail(GI_ERR_SCENE, err);
+    DevScene& d = s->dev;
+    memset(&d, 0, sizeof d);
+    const HostScene& h = s->host;
+    hipError_t e;
+    gi_scene* sp = s.get();
+    if ((e = upload(sp, h.rnodes, &d.rnodes)) != hipSuccess || (e = upload(sp, h.leaf_ents, &d.leaf_ents)) != hipSuccess ||
+        (e = upload(sp, h.ents, &d.ents)) != hipSuccess || (e = upload(sp, h.tris, &d.tris)) != hipSuccess ||
+        (e = upload(sp, h.xwnodes, &d.xwnodes)) != hipSuccess || (e = upload(sp, h.xhot, &d.xhot)) != hipSuccess ||
+        (e = upload(sp, h.xbox, &d.xbox)) != hipSuccess ||
+        (e = upload(sp, h.xprims, &d.xprims)) != hipSuccess ||
+        (e = upload(sp, std::vector<unsigned>(16, 0u), const_cast<const unsigned**>(&d.work))) != hipSuccess ||
+        (e = upload(sp, h.app_off, &d.app_off)) != hipSuccess || (e = upload(sp, h.app_leaf, &d.app_leaf)) != hipSuccess ||
+        (e = upload(sp, h.app_rank, &d.app_rank)) != hipSuccess || (e = upload(sp, h.rpath_off, &d.rpath_off)) != hipSuccess ||
+        (e = upload(sp, h.rpath, &d.rpath)) != hipSuccess || (e = upload(sp, h.rc_nodes, &d.rc_nodes)) != hipSuccess ||
+        (e = upload(sp, h.rc_ent, &d.rc_ent)) != hipSuccess || (e = upload(sp, h.r_always, &d.r_always)) != hipSuccess)
+        return hip_fail(e, "scene upload");
+    d.n_rnodes = (int32_t)h.rnodes.size();
+    d.n_ents = (int32_t)h.ents.size();
+    d.n_xwnodes = (int32_t)h.xwnodes.size();
+    d.n_xprims = (int32_t)h.xprims.size();
+    d.x_max_depth = h.x_max_depth;
+    d.x_handle8 = h.x_handle8;
+    d.x_flags = h.x_flags;
+    d.n_xhot = (int32_t)h.xhot.size();
+    d.n_r_always = (int32_t)h.r_always.size();
+    d.rc_ext = (float)h.rc_ext;
+    {   // LDS-resident traversal + shading records for small scenes (<= 40 KB per workgroup: three
+        // 256-thread workgroups per CU stay resident within the CU's 160 KB of LDS)
+        const size_t bytes = h.xwnodes.size() * sizeof(XWNode) + h.xhot.size() * sizeof(XHot) +
+                             h.xprims.size() * sizeof(XPrim) + h.ents.size() * sizeof(REnt);
+        d.x_lds_bytes = bytes <= 40 * 1024 ? (int32_t)bytes : 0;
+        // light shading (no acos texture mapping, no sphere primitives): 4 waves per SIMD pay off,
+        // provided four workgroups fit a CU's 160 KB: each holds the scene, the per-lane path slots
+        // (256 lanes x 80 B) and the per-wave unit blocks (4 x 68 x 4 B)
+        const size_t per_wg = bytes + 256 * 10 * sizeof(double) + 4 * 68 * sizeof(unsigned);
+        d.x_waves4 = (d.x_lds_bytes > 0 && 4 * per_wg <= 160 * 1024) ? 1 : 0;
+        for (const REnt& r : h.ents)
+            if (r.kind == K_IMP_SPHERE || r.kind == K_EXP_SPHERE || r.kind == K_EXP_CONE || r.kind == K_EXP_RECTANGLE)
+                d.x_waves4 = 0;
+    }
+    for (int k = 0; k < 3; ++k) { d.root_lo[k] = INFINITY; d.root_hi[k] = -INFINITY; }
+    if (!h.xwnodes.empty())
+        for (int c = 0; c < 8; ++c)
+            if (h.xwnodes[0].child[c] != XEMPTY)
+                for (int k = 0; k < 3; ++k) {
+                    d.root_lo[k] = std::min(d.root_lo[k], h.xwnodes[0].lo[k][c]);
+                    d.root_hi[k] = std::max(d.root_hi[k], h.xwnodes[0].hi[k][c]);
+                }
+    if ((e = x_launch_config(d, device, s->xcfg)) != hipSuccess) return hip_fail(e, "occupancy query");
+    *out = s.release();
+    return GI_OK;
+}
+
+void scene_destroy(gi_scene* s) noexcept { destroy_scene(s); }
+int scene_device(const gi_scene* s) { return s->device; }
+std::mutex& scene_mutex(gi_scene* s) { return s->mu; }
+
+// Asynchronous render of a band (rows [y0, y0 + h) of a frame w pixels wide; the whole frame for
+// y0 = 0, h = its height) or of one shard of it, into device buffers on `stream`.
+int scene_render_band(gi_scene* s, const CamDev& cd, const double light[3], int w, int h, int y0, const gi_opts& o,
+                      double* d_rgb, uint8_t* d_rgb8, hipStream_t stream, bool timer) {
+    int rc = bind_device(s->device);
+    if (rc || (rc = ensure_xscratch(s, w, h, &o)) || (timer && (rc = ensure_timer(s, &o)))) return rc;
+    return issue_render(s, cd, v3(light[0], light[1], light[2]), w, h, y0, o, d_rgb, d_rgb8, stream, timer);
+}
+
+int unshard(int w, int h, int n, const double* packed, const uint8_t* packed8, double* rgb, uint8_t* rgb8,
+            hipStream_t stream) {
+    const hipError_t e = launch_unshard(w, h, n, packed, packed8, rgb, rgb8, stream);
+    return e == hipSuccess ? GI_OK : hip_fail(e, "unshard launch");
+}
+
+}  // namespace gi
 
 extern "C" {
 
 int gi_abi_version(void) { return GI_ABI_VERSION; }
 const char* gi_last_error(void) { return g_err.c_str(); }
+
+int gi_device_count(void) {
+    int ndev = 0, n = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess) return 0;
+    for (int d = 0; d < ndev; ++d) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, d) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) == 0) ++n;
+    }
+    return n;
+}
 
 int gi_camera_init(const double pos[3], const double look_at[3], double focal, gi_camera* out) {
     if (!pos || !look_at || !out) return fail(GI_ERR_ARG, "null argument");
@@ -246,96 +437,20 @@ int gi_camera_init(const double pos[3], const double look_at[3], double focal, g
 }
 
 int gi_scene_create(const gi_scene_desc* desc, gi_scene** out) {
-    if (!desc || !out || desc->n_entities < 0 || (desc->n_entities > 0 && !desc->entities))
-        return fail(GI_ERR_ARG, "bad scene descriptor");
-    *out = nullptr;
-    int ndev = 0;
-    hipError_t e = hipGetDeviceCount(&ndev);
-    if (e != hipSuccess || ndev <= 0) return fail(GI_ERR_DEVICE, "no HIP device (libgi renders only on gfx950)");
-    int dev = 0;
-    if ((e = hipGetDevice(&dev)) != hipSuccess) return hip_fail(e, "hipGetDevice");
-    hipDeviceProp_t prop;
-    if ((e = hipGetDeviceProperties(&prop, dev)) != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
-    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
-        return fail(GI_ERR_DEVICE, std::string("device is ") + prop.gcnArchName + ", libgi is built for gfx950 only");
-
-    gi_scene* s = new gi_scene();
-    s->device = dev;
-    std::string err;
-    if (!build_host_scene(*desc, s->host, err)) {
-        delete s;
-        return fail(GI_ERR_SCENE, err);
-    }
-    DevScene& d = s->dev;
-    memset(&d, 0, sizeof d);
-    const HostScene& h = s->host;
-    if ((e = upload(s, h.rnodes, &d.rnodes)) != hipSuccess || (e = upload(s, h.leaf_ents, &d.leaf_ents)) != hipSuccess ||
-        (e = upload(s, h.ents, &d.ents)) != hipSuccess || (e = upload(s, h.tris, &d.tris)) != hipSuccess ||
-        (e = upload(s, h.xwnodes, &d.xwnodes)) != hipSuccess || (e = upload(s, h.xhot, &d.xhot)) != hipSuccess ||
-        (e = upload(s, h.xbox, &d.xbox)) != hipSuccess ||
-        (e = upload(s, h.xprims, &d.xprims)) != hipSuccess ||
-        (e = upload(s, std::vector<unsigned>(16, 0u), const_cast<const unsigned**>(&d.work))) != hipSuccess ||
-        (e = upload(s, h.app_off, &d.app_off)) != hipSuccess || (e = upload(s, h.app_leaf, &d.app_leaf)) != hipSuccess ||
-        (e = upload(s, h.app_rank, &d.app_rank)) != hipSuccess || (e = upload(s, h.rpath_off, &d.rpath_off)) != hipSuccess ||
-        (e = upload(s, h.rpath, &d.rpath)) != hipSuccess || (e = upload(s, h.rc_nodes, &d.rc_nodes)) != hipSuccess ||
-        (e = upload(s, h.rc_ent, &d.rc_ent)) != hipSuccess || (e = upload(s, h.r_always, &d.r_always)) != hipSuccess) {
-        gi_scene_destroy(s);
-        return hip_fail(e, "scene upload");
-    }
-    d.n_rnodes = (int32_t)h.rnodes.size();
-    d.n_ents = (int32_t)h.ents.size();
-    d.n_xwnodes = (int32_t)h.xwnodes.size();
-    d.n_xprims = (int32_t)h.xprims.size();
-    d.x_max_depth = h.x_max_depth;
-    d.x_handle8 = h.x_handle8;
-    d.x_flags = h.x_flags;
-    d.n_xhot = (int32_t)h.xhot.size();
-    d.n_r_always = (int32_t)h.r_always.size();
-    d.rc_ext = (float)h.rc_ext;
-    {   // LDS-resident traversal + shading records for small scenes (<= 40 KB per workgroup:
-        // three 256-thread workgroups per CU stay resident within the CU's 160 KB of LDS)
-        const size_t bytes = h.xwnodes.size() * sizeof(XWNode) + h.xhot.size() * sizeof(XHot) +
-                             h.xprims.size() * sizeof(XPrim) + h.ents.size() * sizeof(REnt);
-        d.x_lds_bytes = bytes <= 40 * 1024 ? (int32_t)bytes : 0;
-        // light shading (no acos texture mapping, no sphere primitives): 4 waves per SIMD pay off
-        d.x_waves4 = 1;
-        for (const REnt& r : h.ents)
-            if (r.kind == K_IMP_SPHERE || r.kind == K_EXP_SPHERE || r.kind == K_EXP_CONE || r.kind == K_EXP_RECTANGLE)
-                d.x_waves4 = 0;
-    }
-    for (int k = 0; k < 3; ++k) { d.root_lo[k] = INFINITY; d.root_hi[k] = -INFINITY; }
-    if (!h.xwnodes.empty())
-        for (int c = 0; c < 8; ++c)
-            if (h.xwnodes[0].child[c] != XEMPTY)
-                for (int k = 0; k < 3; ++k) {
-                    d.root_lo[k] = std::min(d.root_lo[k], h.xwnodes[0].lo[k][c]);
-                    d.root_hi[k] = std::max(d.root_hi[k], h.xwnodes[0].hi[k][c]);
-                }
-    *out = s;
-    return GI_OK;
+    return guard([&]() -> int {
+        if (!desc || !out || desc->n_entities < 0 || (desc->n_entities > 0 && !desc->entities))
+            return fail(GI_ERR_ARG, "bad scene descriptor");
+        *out = nullptr;
+        int ndev = 0;
+        hipError_t e = hipGetDeviceCount(&ndev);
+        if (e != hipSuccess || ndev <= 0) return fail(GI_ERR_DEVICE, "no HIP device (libgi renders only on gfx950)");
+        int dev = 0;
+        if ((e = hipGetDevice(&dev)) != hipSuccess) return hip_fail(e, "hipGetDevice");
+        return scene_create_on(desc, dev, out);
+    });
 }
 
-void gi_scene_destroy(gi_scene* s) {
-    if (!s) return;
-    for (void* p : s->allocs) (void)hipFree(p);
-    (void)hipFree(s->xs.list);
-    (void)hipFree(s->xs.part);
-    for (int i = 0; i < KTimer::kRing; i++) {
-        if (s->kt.ev0[i]) (void)hipEventDestroy(static_cast<hipEvent_t>(s->kt.ev0[i]));
-        if (s->kt.ev1[i]) (void)hipEventDestroy(static_cast<hipEvent_t>(s->kt.ev1[i]));
-    }
-    HostPath& hp = s->hp;
-    if (hp.render) (void)hipStreamSynchronize(hp.render);
-    if (hp.copy) (void)hipStreamSynchronize(hp.copy);
-    free_hostpath_buffers(hp);
-    for (int i = 0; i < HostPath::kSlots; i++) {
-        if (hp.rendered[i]) (void)hipEventDestroy(hp.rendered[i]);
-        if (hp.copied[i]) (void)hipEventDestroy(hp.copied[i]);
-    }
-    if (hp.render) (void)hipStreamDestroy(hp.render);
-    if (hp.copy) (void)hipStreamDestroy(hp.copy);
-    delete s;
-}
+void gi_scene_destroy(gi_scene* s) { destroy_scene(s); }
 
 int gi_scene_get_info(const gi_scene* s, gi_scene_info* info) {
     if (!s || !info) return fail(GI_ERR_ARG, "null argument");
@@ -358,153 +473,192 @@ int64_t gi_shard_tiles(int w, int h, int shard_count) {
 
 int gi_render_device(gi_scene* s, const gi_camera* cam, const double light[3], int w, int h, const gi_opts* o,
                      double* d_rgb, uint8_t* d_rgb8, void* stream) {
-    int rc = check_opts(s, w, h, o);
-    if (rc) return rc;
-    if (!cam || !light) return fail(GI_ERR_ARG, "null camera or light");
-    if ((rc = bind_device(s)) || (rc = ensure_xscratch(s, w, h, o)) || (rc = ensure_timer(s, o))) return rc;
-    const hipError_t e = launch_render(s->dev, make_cam(*cam, w), v3(light[0], light[1], light[2]), w, h, 0, *o, d_rgb,
-                                       d_rgb8, s->xs, &s->kt, static_cast<hipStream_t>(stream));
-    if (e != hipSuccess) return hip_fail(e, "render launch");
-    return GI_OK;
+    return guard([&]() -> int {
+        if (!s) return fail(GI_ERR_ARG, "null scene");
+        int rc = check_opts(w, h, o);
+        if (rc) return rc;
+        if (!cam || !light) return fail(GI_ERR_ARG, "null camera or light");
+        std::lock_guard<std::mutex> lk(s->mu);
+        return scene_render_band(s, make_cam(*cam, w), light, w, h, 0, *o, d_rgb, d_rgb8, static_cast<hipStream_t>(stream),
+                                 true);
+    });
 }
 
 int gi_render(gi_scene* s, const gi_camera* cam, const double light[3], int w, int h, const gi_opts* o, double* rgb,
               uint8_t* rgb8, const volatile int* cancel, gi_tile_cb cb, void* user) {
-    int rc = check_opts(s, w, h, o);
-    if (rc) return rc;
-    if (!cam || !light) return fail(GI_ERR_ARG, "null camera or light");
-    if (o->shard_count != 1) return fail(GI_ERR_ARG, "gi_render renders whole frames; use gi_render_device to shard");
-    if ((rc = bind_device(s))) return rc;
-    // progressive bands of whole tile rows (the reference fills rows in order, raytracer.h:32-33,
-    // and the Viewer repaints what is done, viewer.h:18-21); cancel is polled between bands.
-    int band = o->band_rows > 0 ? o->band_rows : h;
-    band = ((band + GI_TILE - 1) / GI_TILE) * GI_TILE;
-    band = std::min(band, ((h + GI_TILE - 1) / GI_TILE) * GI_TILE);
-    const size_t band_px = (size_t)w * (size_t)band;
-    const int n_bands = (h + band - 1) / band;
-    if ((rc = ensure_xscratch(s, w, band, o)) || (rc = ensure_hostpath(s, band_px, std::min(n_bands, HostPath::kSlots))))
-        return rc;
-    HostPath& hp = s->hp;
-    const CamDev cd = make_cam(*cam, w);
-    const V3 L = v3(light[0], light[1], light[2]);
-    const bool want_rgb = rgb || cb, want_rgb8 = rgb8 || cb;
-    // a whole-frame call copies straight into the caller's buffers (no staging, nothing to overlap)
-    const bool direct = n_bands == 1;
-    double* const dst_rgb = direct && rgb ? rgb : hp.h_rgb[0];
-    uint8_t* const dst_rgb8 = direct && rgb8 ? rgb8 : hp.h_rgb8[0];
-    // band i: render into slot i % 2 (after that slot's previous copy), then copy to its staging
-    auto issue = [&](int i) -> hipError_t {
-        const int k = i % HostPath::kSlots, y0 = i * band, rows = std::min(band, h - y0);
-        const size_t n = (size_t)w * rows * 3;
+    return guard([&]() -> int {
+        if (!s) return fail(GI_ERR_ARG, "null scene");
+        int rc = check_opts(w, h, o);
+        if (rc) return rc;
+        if (!cam || !light) return fail(GI_ERR_ARG, "null camera or light");
+        if (o->shard_count != 1) return fail(GI_ERR_ARG, "gi_render renders whole frames; use gi_render_device or gi_multi to shard");
+        std::lock_guard<std::mutex> lk(s->mu);
+        if ((rc = bind_device(s->device))) return rc;
+        // progressive bands of whole tile rows (the reference fills rows in order, raytracer.h:32-33,
+        // and the Viewer repaints what is done, viewer.h:18-21); cancel is polled between bands.
+        const int band = band_rows_of(o, h);
+        const size_t band_px = (size_t)w * (size_t)band;
+        const int n_bands = (h + band - 1) / band;
+        if ((rc = ensure_hostpath(s, band_px, std::min(n_bands, HostPath::kSlots)))) return rc;
+        HostPath& hp = s->hp;
+        const CamDev cd = make_cam(*cam, w);
+        const bool want_rgb = rgb || cb, want_rgb8 = rgb8 || cb;
+        // a whole-frame call copies straight into the caller's buffers (no staging, nothing to overlap)
+        const bool direct = n_bands == 1;
+        double* const dst_rgb = direct && rgb ? rgb : hp.h_rgb[0];
+        uint8_t* const dst_rgb8 = direct && rgb8 ? rgb8 : hp.h_rgb8[0];
+        // band i: render into slot i % 2 (after that slot's previous copy), then copy to its staging
+        auto issue = [&](int i) -> int {
+            const int k = i % HostPath::kSlots, y0 = i * band, rows = std::min(band, h - y0);
+            const size_t n = (size_t)w * rows * 3;
+            hipError_t e = hipSuccess;
+            if (i >= HostPath::kSlots && (e = hipStreamWaitEvent(hp.render, hp.copied[k], 0)) != hipSuccess)
+                return hip_fail(e, "render");
+            const int r = scene_render_band(s, cd, light, w, rows, y0, *o, hp.d_rgb[k], hp.d_rgb8[k], hp.render, false);
+            if (r) return r;
+            e = hipEventRecord(hp.rendered[k], hp.render);
+            if (e == hipSuccess) e = hipStreamWaitEvent(hp.copy, hp.rendered[k], 0);
+            double* const to = i == 0 ? dst_rgb : hp.h_rgb[k];
+            uint8_t* const to8 = i == 0 ? dst_rgb8 : hp.h_rgb8[k];
+            if (e == hipSuccess && want_rgb) e = hipMemcpyAsync(to, hp.d_rgb[k], n * sizeof(double), hipMemcpyDeviceToHost, hp.copy);
+            if (e == hipSuccess && want_rgb8) e = hipMemcpyAsync(to8, hp.d_rgb8[k], n, hipMemcpyDeviceToHost, hp.copy);
+            if (e == hipSuccess) e = hipEventRecord(hp.copied[k], hp.copy);
+            return e == hipSuccess ? GI_OK : hip_fail(e, "render");
+        };
         hipError_t e = hipSuccess;
-        if (i >= HostPath::kSlots) e = hipStreamWaitEvent(hp.render, hp.copied[k], 0);
-        if (e == hipSuccess) e = launch_render(s->dev, cd, L, w, rows, y0, *o, hp.d_rgb[k], hp.d_rgb8[k], s->xs, nullptr, hp.render);
-        if (e == hipSuccess) e = hipEventRecord(hp.rendered[k], hp.render);
-        if (e == hipSuccess) e = hipStreamWaitEvent(hp.copy, hp.rendered[k], 0);
-        double* const to = i == 0 ? dst_rgb : hp.h_rgb[k];
-        uint8_t* const to8 = i == 0 ? dst_rgb8 : hp.h_rgb8[k];
-        if (e == hipSuccess && want_rgb) e = hipMemcpyAsync(to, hp.d_rgb[k], n * sizeof(double), hipMemcpyDeviceToHost, hp.copy);
-        if (e == hipSuccess && want_rgb8) e = hipMemcpyAsync(to8, hp.d_rgb8[k], n, hipMemcpyDeviceToHost, hp.copy);
-        if (e == hipSuccess) e = hipEventRecord(hp.copied[k], hp.copy);
-        return e;
-    };
-    rc = GI_OK;
-    hipError_t e = hipSuccess;
-    if (cancel && *cancel) rc = fail(GI_ERR_CANCELLED, "cancelled");
-    else if ((e = issue(0)) != hipSuccess) rc = hip_fail(e, "render");
-    for (int i = 0; rc == GI_OK && i < n_bands; i++) {
-        // the next band goes to the GPU before this one is delivered; cancel is polled between bands
-        if (i + 1 < n_bands) {
-            if (cancel && *cancel) { rc = fail(GI_ERR_CANCELLED, "cancelled"); break; }
-            if ((e = issue(i + 1)) != hipSuccess) { rc = hip_fail(e, "render"); break; }
+        if (cancel && *cancel) rc = fail(GI_ERR_CANCELLED, "cancelled");
+        else rc = issue(0);
+        for (int i = 0; rc == GI_OK && i < n_bands; i++) {
+            // the next band goes to the GPU before this one is delivered; cancel is polled between bands
+            if (i + 1 < n_bands) {
+                if (cancel && *cancel) { rc = fail(GI_ERR_CANCELLED, "cancelled"); break; }
+                if ((rc = issue(i + 1)) != GI_OK) break;
+            }
+            const int k = i % HostPath::kSlots, y0 = i * band, rows = std::min(band, h - y0);
+            const size_t n = (size_t)w * rows * 3;
+            if ((e = hipEventSynchronize(hp.copied[k])) != hipSuccess) { rc = hip_fail(e, "render"); break; }
+            const double* hr = i == 0 ? dst_rgb : hp.h_rgb[k];
+            const uint8_t* hr8 = i == 0 ? dst_rgb8 : hp.h_rgb8[k];
+            if (rgb && hr != rgb) { std::memcpy(rgb + (size_t)y0 * w * 3, hr, n * sizeof(double)); hr = rgb + (size_t)y0 * w * 3; }
+            if (rgb8 && hr8 != rgb8) { std::memcpy(rgb8 + (size_t)y0 * w * 3, hr8, n); hr8 = rgb8 + (size_t)y0 * w * 3; }
+            if (cb) cb(user, y0, rows, hr8, hr);
         }
-        const int k = i % HostPath::kSlots, y0 = i * band, rows = std::min(band, h - y0);
-        const size_t n = (size_t)w * rows * 3;
-        if ((e = hipEventSynchronize(hp.copied[k])) != hipSuccess) { rc = hip_fail(e, "render"); break; }
-        const double* hr = i == 0 ? dst_rgb : hp.h_rgb[k];
-        const uint8_t* hr8 = i == 0 ? dst_rgb8 : hp.h_rgb8[k];
-        if (rgb && hr != rgb) { std::memcpy(rgb + (size_t)y0 * w * 3, hr, n * sizeof(double)); hr = rgb + (size_t)y0 * w * 3; }
-        if (rgb8 && hr8 != rgb8) { std::memcpy(rgb8 + (size_t)y0 * w * 3, hr8, n); hr8 = rgb8 + (size_t)y0 * w * 3; }
-        if (cb) cb(user, y0, rows, hr8, hr);
-    }
-    // nothing of this call stays in flight (a cancelled or failed call drains its bands)
-    const hipError_t e1 = hipStreamSynchronize(hp.render), e2 = hipStreamSynchronize(hp.copy);
-    if (rc == GI_OK && (e1 != hipSuccess || e2 != hipSuccess)) rc = hip_fail(e1 != hipSuccess ? e1 : e2, "render");
-    return rc;
+        // nothing of this call stays in flight (a cancelled or failed call drains its bands)
+        const hipError_t e1 = hipStreamSynchronize(hp.render), e2 = hipStreamSynchronize(hp.copy);
+        if (rc == GI_OK && (e1 != hipSuccess || e2 != hipSuccess)) rc = hip_fail(e1 != hipSuccess ? e1 : e2, "render");
+        return rc;
+    });
 }
 
 int gi_scene_kernel_ms(gi_scene* s, float* avg_ms, int64_t* n) {
-    if (!s || !avg_ms) return fail(GI_ERR_ARG, "null argument");
-    KTimer& kt = s->kt;
-    if (kt.recorded == 0) return fail(GI_ERR_ARG, "no render issued with GI_FLAG_TIME since the last read");
-    int rc = bind_device(s);
-    if (rc) return rc;
-    // the unfolded pairs are the last min(recorded, kRing) slots
-    const long long first = kt.recorded > KTimer::kRing ? kt.recorded - KTimer::kRing : 0;
-    for (long long r = std::max(first, kt.folded); r < kt.recorded; r++) {
-        const hipError_t e = fold_timer(kt, (int)(r % KTimer::kRing));
-        if (e != hipSuccess) return hip_fail(e, "gi_scene_kernel_ms");
-    }
-    *avg_ms = (float)(kt.sum_ms / (double)kt.folded);
-    if (n) *n = kt.folded;
-    kt.recorded = 0;
-    kt.folded = 0;
-    kt.sum_ms = 0.0;
-    return GI_OK;
+    return guard([&]() -> int {
+        if (!s || !avg_ms) return fail(GI_ERR_ARG, "null argument");
+        std::lock_guard<std::mutex> lk(s->mu);
+        KTimer& kt = s->kt;
+        if (kt.recorded == 0) return fail(GI_ERR_ARG, "no render issued with GI_FLAG_TIME since the last read");
+        int rc = bind_device(s->device);
+        if (rc) return rc;
+        // the unfolded pairs are the last min(recorded, kRing) slots
+        const long long first = kt.recorded > KTimer::kRing ? kt.recorded - KTimer::kRing : 0;
+        for (long long r = std::max(first, kt.folded); r < kt.recorded; r++) {
+            const hipError_t e = fold_timer(kt, (int)(r % KTimer::kRing));
+            if (e != hipSuccess) return hip_fail(e, "gi_scene_kernel_ms");
+        }
+        *avg_ms = (float)(kt.sum_ms / (double)kt.folded);
+        if (n) *n = kt.folded;
+        kt.recorded = 0;
+        kt.folded = 0;
+        kt.sum_ms = 0.0;
+        return GI_OK;
+    });
 }
 
 int gi_unshard_device(int w, int h, int shard_count, const double* d_packed, const uint8_t* d_packed8, double* d_rgb,
                       uint8_t* d_rgb8, void* stream) {
-    if (w <= 0 || h <= 0 || shard_count < 1) return fail(GI_ERR_ARG, "bad unshard arguments");
-    if ((d_rgb && !d_packed) || (d_rgb8 && !d_packed8)) return fail(GI_ERR_ARG, "missing packed input");
-    const hipError_t e = launch_unshard(w, h, shard_count, d_packed, d_packed8, d_rgb, d_rgb8, static_cast<hipStream_t>(stream));
-    if (e != hipSuccess) return hip_fail(e, "unshard launch");
-    return GI_OK;
+    return guard([&]() -> int {
+        if (w <= 0 || h <= 0 || shard_count < 1) return fail(GI_ERR_ARG, "bad unshard arguments");
+        if ((d_rgb && !d_packed) || (d_rgb8 && !d_packed8)) return fail(GI_ERR_ARG, "missing packed input");
+        return unshard(w, h, shard_count, d_packed, d_packed8, d_rgb, d_rgb8, static_cast<hipStream_t>(stream));
+    });
 }
 
 int gi_trace_ray(gi_scene* s, const double origin[3], const double dir[3], const double light[3], gi_hit* hit,
                  double rgb[3]) {
-    if (!s || !origin || !dir || !light || !hit || !rgb) return fail(GI_ERR_ARG, "null argument");
-    int rc = bind_device(s);
-    if (rc) return rc;
-    int32_t* d_i = nullptr;
-    double* d_d = nullptr;
-    hipError_t e;
-    if ((e = hipMalloc((void**)&d_i, 4 * sizeof(int32_t))) != hipSuccess) return hip_fail(e, "hipMalloc");
-    if ((e = hipMalloc((void**)&d_d, 9 * sizeof(double))) != hipSuccess) { (void)hipFree(d_i); return hip_fail(e, "hipMalloc"); }
-    const V3 o = v3(origin[0], origin[1], origin[2]);
-    const V3 d = normalize(v3(dir[0], dir[1], dir[2]));   // Ray ctor (ray.h:6)
-    e = launch_trace_ray(s->dev, o, d, v3(light[0], light[1], light[2]), d_i, d_d, nullptr);
-    int32_t hi[3] = {-1, 0, 0};
-    double hd[9] = {0};
-    if (e == hipSuccess) e = hipMemcpy(hi, d_i, 3 * sizeof(int32_t), hipMemcpyDeviceToHost);
-    if (e == hipSuccess) e = hipMemcpy(hd, d_d, 9 * sizeof(double), hipMemcpyDeviceToHost);
-    (void)hipFree(d_i);
-    (void)hipFree(d_d);
-    if (e != hipSuccess) return hip_fail(e, "trace_ray");
-    hit->entity = hi[0];
-    hit->u = hi[1];
-    hit->v = hi[2];
-    for (int k = 0; k < 3; ++k) { hit->point[k] = hd[k]; hit->normal[k] = hd[3 + k]; rgb[k] = hd[6 + k]; }
-    return GI_OK;
+    return guard([&]() -> int {
+        if (!s || !origin || !dir || !light || !hit || !rgb) return fail(GI_ERR_ARG, "null argument");
+        std::lock_guard<std::mutex> lk(s->mu);
+        int rc = bind_device(s->device);
+        if (rc) return rc;
+        int32_t* d_i = nullptr;
+        double* d_d = nullptr;
+        hipError_t e;
+        if ((e = hipMalloc((void**)&d_i, 4 * sizeof(int32_t))) != hipSuccess) return hip_fail(e, "hipMalloc");
+        if ((e = hipMalloc((void**)&d_d, 9 * sizeof(double))) != hipSuccess) { (void)hipFree(d_i); return hip_fail(e, "hipMalloc"); }
+        const V3 o = v3(origin[0], origin[1], origin[2]);
+        const V3 d = normalize(v3(dir[0], dir[1], dir[2]));   // Ray ctor (ray.h:6)
+        e = launch_trace_ray(s->dev, o, d, v3(light[0], light[1], light[2]), d_i, d_d, nullptr);
+        int32_t hi[3] = {-1, 0, 0};
+        double hd[9] = {0};
+        if (e == hipSuccess) e = hipMemcpy(hi, d_i, 3 * sizeof(int32_t), hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = hipMemcpy(hd, d_d, 9 * sizeof(double), hipMemcpyDeviceToHost);
+        (void)hipFree(d_i);
+        (void)hipFree(d_d);
+        if (e != hipSuccess) return hip_fail(e, "trace_ray");
+        hit->entity = hi[0];
+        hit->u = hi[1];
+        hit->v = hi[2];
+        for (int k = 0; k < 3; ++k) { hit->point[k] = hd[k]; hit->normal[k] = hd[3 + k]; rgb[k] = hd[6 + k]; }
+        return GI_OK;
+    });
 }
 
 int gi_kat_expbox(int n, const double* recs, int32_t* out) {
-    if (n < 0 || (n > 0 && (!recs || !out))) return fail(GI_ERR_ARG, "bad arguments");
-    if (n == 0) return GI_OK;
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(GI_ERR_DEVICE, "no HIP device");
-    double* d_r = nullptr;
-    int32_t* d_o = nullptr;
-    hipError_t e;
-    if ((e = hipMalloc((void**)&d_r, (size_t)n * 12 * sizeof(double))) != hipSuccess) return hip_fail(e, "hipMalloc");
-    if ((e = hipMalloc((void**)&d_o, (size_t)n * sizeof(int32_t))) != hipSuccess) { (void)hipFree(d_r); return hip_fail(e, "hipMalloc"); }
-    e = hipMemcpy(d_r, recs, (size_t)n * 12 * sizeof(double), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = launch_box_kat(n, d_r, d_o, nullptr);
-    if (e == hipSuccess) e = hipMemcpy(out, d_o, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost);
-    (void)hipFree(d_r);
-    (void)hipFree(d_o);
-    return e == hipSuccess ? GI_OK : hip_fail(e, "gi_kat_expbox");
+    return guard([&]() -> int {
+        if (n < 0 || (n > 0 && (!recs || !out))) return fail(GI_ERR_ARG, "bad arguments");
+        if (n == 0) return GI_OK;
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(GI_ERR_DEVICE, "no HIP device");
+        double* d_r = nullptr;
+        int32_t* d_o = nullptr;
+        hipError_t e;
+        if ((e = hipMalloc((void**)&d_r, (size_t)n * 12 * sizeof(double))) != hipSuccess) return hip_fail(e, "hipMalloc");
+        if ((e = hipMalloc((void**)&d_o, (size_t)n * sizeof(int32_t))) != hipSuccess) { (void)hipFree(d_r); return hip_fail(e, "hipMalloc"); }
+        e = hipMemcpy(d_r, recs, (size_t)n * 12 * sizeof(double), hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = launch_box_kat(n, d_r, d_o, nullptr);
+        if (e == hipSuccess) e = hipMemcpy(out, d_o, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost);
+        (void)hipFree(d_r);
+        (void)hipFree(d_o);
+        return e == hipSuccess ? GI_OK : hip_fail(e, "gi_kat_expbox");
+    });
+}
+
+int gi_octree_create(const gi_scene_desc* desc, gi_octree** out) {
+    return guard([&]() -> int {
+        if (!desc || !out || desc->n_entities < 0 || (desc->n_entities > 0 && !desc->entities))
+            return fail(GI_ERR_ARG, "bad scene descriptor");
+        *out = nullptr;
+        std::unique_ptr<gi_octree> t(new gi_octree());
+        std::string err;
+        if (!build_host_scene(*desc, t->host, err)) return fail(GI_ERR_SCENE, err);
+        *out = t.release();
+        return GI_OK;
+    });
+}
+
+void gi_octree_destroy(gi_octree* t) { delete t; }
+
+int gi_octree_intersect(const gi_octree* t, const double origin[3], const double dir[3], int32_t* out, int64_t cap,
+                        int64_t* n) {
+    return guard([&]() -> int {
+        if (!t || !origin || !dir || !n || cap < 0 || (cap > 0 && !out)) return fail(GI_ERR_ARG, "bad arguments");
+        std::vector<int32_t> list;
+        if (!t->host.rnodes.empty())
+            octree_query(t->host, 0, v3(origin[0], origin[1], origin[2]), v3(dir[0], dir[1], dir[2]), list);
+        *n = (int64_t)list.size();
+        const int64_t k = std::min<int64_t>(cap, (int64_t)list.size());
+        if (k > 0) std::memcpy(out, list.data(), (size_t)k * sizeof(int32_t));
+        return GI_OK;
+    });
 }
 
 }  // extern "C"

@@ -6,7 +6,7 @@
 // taking (pixel, run of samples) units from a device work list.
 //
 // Mode R (reference semantics):
-//   The reference builds the full candidate list of Octree::intersect (octree.h:233-256, DFS over
+//   The reference builds the full candidate list of Octree::intersect (octree.h:132-155, DFS over
 //   children 0..7, ExpBox node test) and keeps the LAST candidate whose intersect() succeeds
 //   (raytracer.h:53-74, A.1).  The kernel reconstructs that answer from the entities the ray's line
 //   passes near (a line BVH), their exact tests and the reachability of their leaves (the same
@@ -26,6 +26,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdlib>
+#include <mutex>
 
 #include "gi.h"
 #include "gi_scene.h"
@@ -226,7 +227,7 @@ __device__ void trace_mode_r(const DevScene& sc, V3 o, V3 d, RResult& r, uint32_
         }
         const int c = parent_child0 + slot;
         const RNode nd = nodes[c];
-        if (nd.ent_cnt == 0) { --slot; continue; }   // octree.h:241
+        if (nd.ent_cnt == 0) { --slot; continue; }   // octree.h:140
         ++nnode;
         if (!box_hit(ld3(nd.mn), ld3(nd.mx), o, d)) { --slot; continue; }
         if (nd.child0 < 0) {
@@ -1390,8 +1391,49 @@ TileMap make_map(int w, int h, int shard_count, int shard_index, int y0 = 0) {
 
 long long shard_tiles(int w, int h, int shard_count) { return make_map(w, h, shard_count, 0).n_local; }
 
-hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w, int h, int y0, const gi_opts& o,
-                         double* rgb, uint8_t* rgb8, const XScratch& xs, KTimer* kt, hipStream_t stream) {
+// Tuning knobs read once per process from the environment (thread-safe; several host threads may
+// each drive their own device and scene): GI_X_LDS=0 disables LDS-resident scenes, GI_X_HANDLE8
+// overrides the shading-handler threshold, GI_X_FLAGS the schedule flags, GI_X_MAX_RUN the largest
+// work-unit run length (scenes of cheap background samples such as the main.cpp scene prefer 8).
+struct XEnv {
+    int lds = 1, h8 = 0, xf = -1, run_log2 = 0;
+};
+const XEnv& x_env() {
+    static XEnv env;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        if (const char* v = std::getenv("GI_X_LDS")) env.lds = std::atoi(v);
+        if (const char* v = std::getenv("GI_X_HANDLE8")) env.h8 = std::max(1, std::min(8, std::atoi(v)));
+        if (const char* v = std::getenv("GI_X_FLAGS")) env.xf = std::atoi(v);
+        const char* v = std::getenv("GI_X_MAX_RUN");
+        const int r = v ? std::max(1, std::min(128, std::atoi(v))) : GI_X_MAX_RUN;
+        int lg = 0;
+        while ((2 << lg) <= r) ++lg;
+        env.run_log2 = lg;
+    });
+    return env;
+}
+
+hipError_t x_launch_config(const DevScene& sc, int device, XLaunchCfg& cfg) {
+    const bool lds = x_env().lds != 0 && sc.x_lds_bytes > 0;
+    cfg.lds_bytes = lds ? (size_t)sc.x_lds_bytes + ((sc.x_waves4 && GI_X_PSL) ? 256 * 10 * sizeof(double) : 0) : 0;
+    cfg.kv = 2 * (int)lds + ((lds && sc.x_waves4) ? 1 : 0);
+    int cus = 0, per_cu = 0;
+    hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    if (e != hipSuccess) return e;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, cfg.kv == 3 ? reinterpret_cast<const void*>(k_mode_x<false, true, true>)
+                 : cfg.kv == 2 ? reinterpret_cast<const void*>(k_mode_x<false, true, false>)
+                               : reinterpret_cast<const void*>(k_mode_x<false, false, false>),
+        64 * kWavesPerBlock, cfg.lds_bytes);
+    if (e != hipSuccess) return e;
+    cfg.resident = std::max(1, cus) * std::max(1, per_cu);
+    return hipSuccess;
+}
+
+hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev& cam, V3 light, int w, int h, int y0,
+                         const gi_opts& o, double* rgb, uint8_t* rgb8, const XScratch& xs, KTimer* kt,
+                         hipStream_t stream) {
     // GI_FLAG_TIME: events on the launch stream around the dominant kernel only (slot chosen by
     // the caller, gi_capi.cpp, which folds a reused pair before this call)
     const bool timed = (o.flags & GI_FLAG_TIME) && kt && kt->ev0[0];
@@ -1416,35 +1458,15 @@ hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w,
         else hipLaunchKernelGGL(k_mode_r<false>, grid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, dfs);
         mark(ev_end);
     } else {
-        // persistent grid: as many 4-wave blocks as can be resident, each wave pulls tiles
-        static int env_lds = -1;   // GI_X_LDS=0 disables the LDS-resident scene (tuning)
-        if (env_lds == -1) {
-            const char* v = std::getenv("GI_X_LDS");
-            env_lds = v ? std::atoi(v) : 1;
-        }
-        const bool lds = env_lds != 0 && sc.x_lds_bytes > 0;
-        const size_t lds_bytes = lds ? (size_t)sc.x_lds_bytes + ((sc.x_waves4 && GI_X_PSL) ? 256 * 10 * sizeof(double) : 0) : 0;
-        const int w4 = (lds && sc.x_waves4) ? 1 : 0;
-        const int kv = 2 * (int)lds + w4;   // kernel variant
-        static int resident_blocks[4] = {0, 0, 0, 0};
-        static size_t resident_lds[4] = {0, 0, 0, 0};
-        if (resident_blocks[kv] == 0 || resident_lds[kv] != lds_bytes) {
-            int dev = 0, cus = 0, per_cu = 0;
-            (void)hipGetDevice(&dev);
-            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &per_cu, kv == 3 ? reinterpret_cast<const void*>(k_mode_x<false, true, true>)
-                         : kv == 2 ? reinterpret_cast<const void*>(k_mode_x<false, true, false>)
-                                   : reinterpret_cast<const void*>(k_mode_x<false, false, false>),
-                64 * kWavesPerBlock, lds_bytes);
-            resident_blocks[kv] = std::max(1, cus) * std::max(1, per_cu);
-            resident_lds[kv] = lds_bytes;
-        }
-        const int resident = resident_blocks[kv];
+        // persistent grid: as many 4-wave blocks as can be resident (xc, per scene), each wave pulls
+        // blocks of work units
+        const XEnv& env = x_env();
+        const int kv = xc.kv;
+        const size_t lds_bytes = xc.lds_bytes;
         const long long n_slots = m.n_local * (kTile * kTile);
         // up to one lane per (pixel slot, sample): single-sample units can occupy that many lanes
         const long long want = (n_slots * (long long)o.spp / 64 + kWavesPerBlock - 1) / kWavesPerBlock;
-        const dim3 pgrid((unsigned)std::max<long long>(1, std::min<long long>(want, resident)));
+        const dim3 pgrid((unsigned)std::max<long long>(1, std::min<long long>(want, xc.resident)));
         if (!xs.list || (unsigned long long)xs.cap < (unsigned long long)n_slots || (o.spp > 1 && (!xs.part || xs.spp < o.spp)))
             return hipErrorInvalidValue;
         hipError_t e = hipMemsetAsync(sc.work, 0, 16 * sizeof(unsigned), stream);
@@ -1458,29 +1480,10 @@ hipError_t launch_render(const DevScene& sc, const CamDev& cam, V3 light, int w,
         if (stats) hipLaunchKernelGGL(k_x_classify<true>, sgrid, dim3(256), 0, stream, sc, cam, m, o.spp, rgb, rgb8, xs.list, sc.work + 1, st);
         else hipLaunchKernelGGL(k_x_classify<false>, sgrid, dim3(256), 0, stream, sc, cam, m, o.spp, rgb, rgb8, xs.list, sc.work + 1, st);
         // shading-handler threshold (eighths of the live lanes that must wait): the builder's
-        // estimate for the scene (DevScene::x_handle8), overridable for tuning with GI_X_HANDLE8
-        static int env_h8 = -1;
-        if (env_h8 == -1) {
-            const char* v = std::getenv("GI_X_HANDLE8");
-            env_h8 = v ? std::max(1, std::min(8, std::atoi(v))) : 0;
-        }
-        const int h8 = env_h8 > 0 ? env_h8 : sc.x_handle8;
-        static int env_xf = -2;   // GI_X_FLAGS overrides the builder's choice (bit 0: inline shadow)
-        if (env_xf == -2) {
-            const char* v = std::getenv("GI_X_FLAGS");
-            env_xf = v ? std::atoi(v) : -1;
-        }
-        // maximum run length (samples per work unit), log2 in bits 8-10; GI_X_MAX_RUN=<power of two>
-        // in the environment overrides the build's default (scenes of cheap background samples
-        // such as the main.cpp scene prefer 8)
-        static int env_run = -1;
-        if (env_run == -1) {
-            const char* v = std::getenv("GI_X_MAX_RUN");
-            int r = v ? std::max(1, std::min(128, std::atoi(v))) : GI_X_MAX_RUN, lg = 0;
-            while ((2 << lg) <= r) ++lg;
-            env_run = lg;
-        }
-        const int xf = (env_xf >= 0 ? env_xf : sc.x_flags) | (env_run << 8);
+        // estimate for the scene (DevScene::x_handle8) unless GI_X_HANDLE8 overrides it
+        const int h8 = env.h8 > 0 ? env.h8 : sc.x_handle8;
+        // schedule flags (bit 0: inline shadow) and the maximum run length (log2, bits 8-10)
+        const int xf = (env.xf >= 0 ? env.xf : sc.x_flags) | (env.run_log2 << 8);
 #define GI_LAUNCH_X(S, L, W) hipLaunchKernelGGL((k_mode_x<S, L, W>), pgrid, block, lds_bytes, stream, sc, cam, light, m, o.spp, \
                                            o.depth, o.seed, rgb, rgb8, st, wk, h8, xf)
         mark(ev_begin);

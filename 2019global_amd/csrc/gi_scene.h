@@ -2,7 +2,7 @@
 //
 // Mode R keeps the reference octree exactly (octree.h:12-163, including SURVEY A.4-A.6, A.14):
 //   RNode[]   64 B/node: AABB (fp64) + child0 / parent / leaf list range.  Children of a node are
-//             8 consecutive records in octant order 0..7 (octree.h:195-209).
+//             8 consecutive records in octant order 0..7 (octree.h:94-108).
 //   leaf_ents int32 entity indices, each leaf's list in push order.
 //   REnt[]    entity records (kind, material, sphere/quad parameters) + TriRec[] triangles.
 // Mode X uses its own tight octree over primitives (XWNode[] traversal nodes, XHot[] leaf records,
@@ -23,7 +23,7 @@ struct RNode {             // 64 bytes
     int32_t child0;        // -1: leaf
     int32_t parent;        // -1: root
     int32_t ent_off;       // leaves: offset into leaf_ents
-    int32_t ent_cnt;       // size of the node's _entities (interior: only emptiness is used, octree.h:241)
+    int32_t ent_cnt;       // size of the node's _entities (interior: only emptiness is used, octree.h:140)
 };
 static_assert(sizeof(RNode) == 64, "RNode layout");
 
@@ -192,6 +192,14 @@ struct XScratch {
     double* part = nullptr;     // cap * spp * 3 doubles
     long long cap = 0;          // pixel slots the buffers hold
     int spp = 0;                // samples per pixel the part buffer was sized for
+};
+
+// Mode X launch configuration, computed once per scene when it is created (gi_capi.cpp, on the
+// scene's device): kernel variant, dynamic LDS bytes and the resident persistent grid.
+struct XLaunchCfg {
+    int kv = 0;              // kernel variant: 2 * (LDS-resident scene) + (4 waves per SIMD)
+    size_t lds_bytes = 0;    // dynamic LDS per workgroup
+    int resident = 1;        // resident 256-thread workgroups on the device (occupancy x CUs)
 };
 
 }  // namespace gi

@@ -1,8 +1,8 @@
 """Scene descriptions for the gi path (host side, no GPU).
 
 A scene is exactly what the reference's app code builds by hand in ``main.cpp:24-48``: an
-``Octree(min, max)`` (octree.h:115), a ``Camera(pos, lookAt, focal)`` (camera.h:8-10), a point
-light, and a sequence of ``Octree::push_back(new Entity(...))`` calls (octree.h:121-144) whose
+``Octree(min, max)`` (octree.h:14), a ``Camera(pos, lookAt, focal)`` (camera.h:8-10), a point
+light, and a sequence of ``Octree::push_back(new Entity(...))`` calls (octree.h:20-43) whose
 order defines the reference's candidate order.  Entity parameters are the reference
 constructor arguments (entities.h:45, 138, 461, 581, 652, 823), optionally followed by a
 ``material`` override (``entity->material = Material(color[, shader])``, material.h:12-29).

@@ -3,12 +3,12 @@
  * This is the drop-in boundary for the reference's render driver.  The reference has no ABI: its
  * path is the header-only class RayTracer (include/raytracer.h:15-101) whose run(w, h)
  * (raytracer.h:23-87) loops over pixels and, per pixel, queries Octree::intersect
- * (octree.h:147-169), calls Entity::intersect / getTextureCoord (entities.h:26, 32) and
+ * (octree.h:46-68), calls Entity::intersect / getTextureCoord (entities.h:26, 32) and
  * Material::blinn_phong_texture (material.h:48-62), and stores through Image::setPixel
  * (image.h:14-16).  The entry points below replace, one for one:
  *
- *   gi_scene_create      Octree(min,max) (octree.h:115) + Octree::push_back per entity
- *                        (octree.h:121-144) + the entity constructors (entities.h:45, 138, 581, ...)
+ *   gi_scene_create      Octree(min,max) (octree.h:14) + Octree::push_back per entity
+ *                        (octree.h:20-43) + the entity constructors (entities.h:45, 138, 581, ...)
  *   gi_camera_init       Camera(pos, lookAt, focal) (camera.h:8-10)
  *   gi_render            RayTracer::run(w, h) (raytracer.h:23-87), host buffers, progressive tiles,
  *                        cancel flag = RayTracer::stop() (raytracer.h:90)
@@ -17,6 +17,13 @@
  *   gi_trace_ray         one iteration of raytracer.h:41-84 for an arbitrary ray
  *   gi_unshard_device    reassembles a frame from per-rank packed tiles after the RCCL gather
  *   gi_scene_kernel_ms   HIP-event duration of the last timed render's dominant kernel (bench)
+ *   gi_octree_*          Octree(min,max) + push_back (octree.h:14-43) and the public query
+ *                        Octree::intersect(const Ray&) (octree.h:46-68 -> Node::intersect :132-155)
+ *                        on the host, for reference-side callers of the candidate list
+ *   gi_multi_*           RayTracer::run over several GPUs of one process: a scene replica per
+ *                        device, 8x8 tiles dealt round-robin, RCCL send/recv gather over xGMI to
+ *                        the first device (the drop-in RayTracer uses it when GI_DEVICES lists
+ *                        more than one device or the node has several)
  *
  * Conventions: all pointers are plain C pointers; buffers are caller-owned; sizes are in elements;
  * every function returns 0 on success and a negative gi_status on error, with a thread-local
@@ -33,14 +40,16 @@
 extern "C" {
 #endif
 
-#define GI_ABI_VERSION 4
+#define GI_ABI_VERSION 5
 
 typedef enum gi_status {
     GI_OK = 0,
     GI_ERR_ARG = -1,      /* invalid argument */
     GI_ERR_DEVICE = -2,   /* HIP error / no device */
     GI_ERR_SCENE = -3,    /* unsupported entity or material */
-    GI_ERR_CANCELLED = -4 /* *cancel became non-zero; frame partially rendered */
+    GI_ERR_CANCELLED = -4,/* *cancel became non-zero; frame partially rendered */
+    GI_ERR_NOMEM = -5,    /* host memory exhausted (std::bad_alloc inside the library) */
+    GI_ERR_INTERNAL = -6  /* any other exception caught at the boundary */
 } gi_status;
 
 /* Entity kinds.  args[] holds the reference constructor's arguments in constructor order. */
@@ -153,6 +162,8 @@ typedef void (*gi_tile_cb)(void* user, int y0, int rows, const uint8_t* rgb8_row
 
 int gi_abi_version(void);
 const char* gi_last_error(void);
+/* gfx950 devices visible to this process (0 when there is none). */
+int gi_device_count(void);
 
 int gi_camera_init(const double pos[3], const double look_at[3], double focal, gi_camera* out);
 
@@ -163,7 +174,10 @@ void gi_scene_destroy(gi_scene* scene);
 int gi_scene_get_info(const gi_scene* scene, gi_scene_info* info);
 
 /* Renders a w x h frame into host buffers (rgb: w*h*3 fp64, rgb8: w*h*3 RGB888; either may be
- * NULL).  Polls *cancel (if non-NULL) between bands; calls cb (if non-NULL) after each band. */
+ * NULL).  Polls *cancel (if non-NULL) between bands; calls cb (if non-NULL) after each band.
+ * Threading: a scene may be used from any host thread; calls on one scene are serialised by the
+ * library (a mutex for the host side, and every render of a scene is ordered on the device behind
+ * the scene's previous one, whatever stream each was issued on: they share the Mode X work list). */
 int gi_render(gi_scene* scene, const gi_camera* cam, const double light[3], int w, int h,
               const gi_opts* opts, double* rgb, uint8_t* rgb8, const volatile int* cancel,
               gi_tile_cb cb, void* user);
@@ -191,7 +205,39 @@ int gi_trace_ray(gi_scene* scene, const double origin[3], const double dir[3], c
  * GI_ERR_ARG if there was none. */
 int gi_scene_kernel_ms(gi_scene* scene, float* avg_ms, int64_t* n);
 
-/* Known-answer hook: the device's ExpBox node test (entities.h:379-440 as octree.h:242-247 uses
+/* ---- host-side reference octree (no device needed) --------------------------------------------
+ * gi_octree_create builds the reference octree from the same descriptors as gi_scene_create (push
+ * order, node boxes, lost entities A.6, silent drop A.14 -- bit for bit the reference's tree).
+ * gi_octree_intersect returns Octree::intersect(Ray(origin, dir))'s candidate list: DFS over the
+ * children 0..7, a child skipped when its list is empty (octree.h:140), else tested by the ExpBox
+ * node test (A.4) and descended; leaves contribute their lists; duplicates kept.  `dir` is used as
+ * given (the reference's Ray ctor has already normalised it, ray.h:6).  Entity indices are push
+ * order; min(*n, cap) of them are written to out, *n = the full length. */
+typedef struct gi_octree gi_octree;
+int gi_octree_create(const gi_scene_desc* desc, gi_octree** out);
+void gi_octree_destroy(gi_octree* octree);
+int gi_octree_intersect(const gi_octree* octree, const double origin[3], const double dir[3], int32_t* out,
+                        int64_t cap, int64_t* n);
+
+/* ---- several GPUs of one process ------------------------------------------------------------
+ * gi_multi_create: n_shards >= 1 shards, shard i rendered on HIP device devices[i] (duplicates
+ * allowed: several shards on one device render one after the other).  devices[0] is the root that
+ * assembles the frame.  The frame's 8x8 tiles are dealt round-robin over the shards (tile t ->
+ * shard t % n_shards, as gi_render_device's shard_count/shard_index); each shard renders its tiles
+ * into a packed buffer on its device, and one RCCL group of ncclSend/ncclRecv (rccl.h:700-725;
+ * librccl is loaded when a second device is used) brings them to the root over xGMI, where
+ * gi_unshard_device's kernel reassembles the frame.  Shards on the root device need no copy.
+ * gi_multi_render: as gi_render (bands, cancel, callback, host buffers); opts->shard_count and
+ * shard_index must be 1 and 0 (the multi handle does the sharding).  Results are bit-identical to
+ * gi_render on one device. */
+typedef struct gi_multi gi_multi;
+int gi_multi_create(const gi_scene_desc* desc, int n_shards, const int* devices, gi_multi** out);
+void gi_multi_destroy(gi_multi* multi);
+int gi_multi_info(const gi_multi* multi, int* n_shards, int* n_devices, int* uses_rccl);
+int gi_multi_render(gi_multi* multi, const gi_camera* cam, const double light[3], int w, int h, const gi_opts* opts,
+                    double* rgb, uint8_t* rgb8, const volatile int* cancel, gi_tile_cb cb, void* user);
+
+/* Known-answer hook: the device's ExpBox node test (entities.h:379-440 as octree.h:141-146 uses
  * it) over n host records (min[3], max[3], origin[3], dir[3]); out[i] = 0/1. */
 int gi_kat_expbox(int n, const double* recs, int32_t* out);
 

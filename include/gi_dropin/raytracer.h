@@ -15,6 +15,8 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <memory>
 #include <vector>
 
@@ -25,6 +27,7 @@
 #include "image.h"
 #include "octree.h"   // gi_dropin/octree.h (same directory, searched first)
 #include "gi.h"
+#include "gi_describe.h"
 
 class RayTracer {
   public:
@@ -40,8 +43,15 @@ class RayTracer {
     void run(int w, int h) {
         _image = std::make_shared<Image>(w, h);   // raytracer.h:25
         if (!_scene || w <= 0 || h <= 0) return;
-        if (!_gpu || _gpu_generation != _scene->generation()) {
-            if (!upload()) return;
+        // the reference reads the live octree on every run (raytracer.h:45): the entities are
+        // described again and the scene re-uploaded when anything changed (push_back, a material)
+        std::vector<gi_entity_desc> ents;
+        if (!gi_dropin::describe_all(_scene->entities(), ents)) return;
+        const double mn[3] = {_scene->min.x, _scene->min.y, _scene->min.z};
+        const double mx[3] = {_scene->max.x, _scene->max.y, _scene->max.z};
+        const uint64_t hash = gi_dropin::scene_hash(ents, mn, mx);
+        if (!_gpu || _gpu->hash != hash) {
+            if (!upload(ents, mn, mx, hash)) return;
         }
         gi_camera cam;
         for (int k = 0; k < 3; ++k) {
@@ -58,7 +68,10 @@ class RayTracer {
         o.shard_count = 1;
         o.band_rows = 32;
         Band band{_image.get(), w};
-        const int rc = gi_render(_gpu.get(), &cam, light, w, h, &o, nullptr, nullptr, &_cancel, &RayTracer::on_band, &band);
+        const int rc = _gpu->multi ? gi_multi_render(_gpu->multi, &cam, light, w, h, &o, nullptr, nullptr, &_cancel,
+                                                     &RayTracer::on_band, &band)
+                                   : gi_render(_gpu->scene, &cam, light, w, h, &o, nullptr, nullptr, &_cancel,
+                                               &RayTracer::on_band, &band);
         if (rc != GI_OK && rc != GI_ERR_CANCELLED) std::fprintf(stderr, "gi_render: %s\n", gi_last_error());
     }
 
@@ -74,6 +87,18 @@ class RayTracer {
         int w;
     };
 
+    // the uploaded scene: one device (gi_scene) or several (gi_multi: GI_DEVICES="0,1,..." or
+    // "all"; by default every gfx950 of the node when there is more than one)
+    struct Gpu {
+        gi_scene* scene = nullptr;
+        gi_multi* multi = nullptr;
+        uint64_t hash = 0;
+        ~Gpu() {
+            if (scene) gi_scene_destroy(scene);
+            if (multi) gi_multi_destroy(multi);
+        }
+    };
+
     static void on_band(void* user, int y0, int rows, const uint8_t*, const double* rgb) {
         Band* b = static_cast<Band*>(user);
         for (int j = 0; j < rows; ++j)
@@ -83,91 +108,50 @@ class RayTracer {
             }
     }
 
-    static void set_material(gi_entity_desc& d, const Material& m) {
-        d.has_material = 1;
-        for (int k = 0; k < 3; ++k) {
-            d.mat_color[k] = m.color[k];
-            d.mat_shader[k] = m.shader_parameters[k];
+    static std::vector<int> devices() {
+        std::vector<int> d;
+        const char* env = std::getenv("GI_DEVICES");
+        if (env && *env && std::strcmp(env, "all") != 0) {
+            for (const char* p = env; *p;) {
+                char* end = nullptr;
+                const long v = std::strtol(p, &end, 10);
+                if (end == p) break;
+                d.push_back((int)v);
+                p = *end == ',' ? end + 1 : end;
+            }
+            return d;
         }
-        d.mat_specular_power = m.specular_power;
+        const int n = gi_device_count();
+        if (env || n > 1)
+            for (int i = 0; i < n; ++i) d.push_back(i);
+        return d;
     }
 
-    // The entity's constructor arguments are recovered from its public members (entities.h) and
-    // its current material is passed explicitly (covers `entity->material = ...` after construction).
-    static bool describe(const Entity* e, gi_entity_desc& d) {
-        d = gi_entity_desc();
-        if (auto* s = dynamic_cast<const ImpSphere*>(e)) {
-            d.kind = GI_IMP_SPHERE;
-            const double a[7] = {s->pos.x, s->pos.y, s->pos.z, (double)s->radius,
-                                 s->material.color.x, s->material.color.y, s->material.color.z};
-            std::copy(a, a + 7, d.args);
-        } else if (auto* t = dynamic_cast<const ImpTriangle*>(e)) {
-            d.kind = GI_IMP_TRIANGLE;
-            const double a[9] = {t->p1.x, t->p1.y, t->p1.z, t->p2.x, t->p2.y, t->p2.z, t->p3.x, t->p3.y, t->p3.z};
-            std::copy(a, a + 9, d.args);
-        } else if (auto* q = dynamic_cast<const ExpQuad*>(e)) {
-            d.kind = GI_EXP_QUAD;
-            const double a[9] = {q->pos.x, q->pos.y, q->pos.z, (double)q->width, (double)q->length, (double)q->alpha,
-                                 q->material.color.x, q->material.color.y, q->material.color.z};
-            std::copy(a, a + 9, d.args);
-        } else if (auto* es = dynamic_cast<const ExpSphere*>(e)) {
-            d.kind = GI_EXP_SPHERE;
-            const double a[7] = {es->pos.x, es->pos.y, es->pos.z, (double)es->radius,
-                                 es->material.color.x, es->material.color.y, es->material.color.z};
-            std::copy(a, a + 7, d.args);
-        } else if (auto* c = dynamic_cast<const ExpCube*>(e)) {
-            d.kind = GI_EXP_CUBE;
-            const double a[9] = {c->pos.x, c->pos.y, c->pos.z, (double)c->width, (double)c->length, (double)c->height,
-                                 c->material.color.x, c->material.color.y, c->material.color.z};
-            std::copy(a, a + 9, d.args);
-        } else if (auto* k = dynamic_cast<const ExpCone*>(e)) {
-            d.kind = GI_EXP_CONE;   // the member dir holds the constructor argument (entities.h:823)
-            const double a[11] = {k->pos.x, k->pos.y, k->pos.z, k->dir.x, k->dir.y, k->dir.z, (double)k->height,
-                                  (double)k->radius, k->material.color.x, k->material.color.y, k->material.color.z};
-            std::copy(a, a + 11, d.args);
-        } else if (auto* r = dynamic_cast<const ExpRectangle*>(e)) {
-            d.kind = GI_EXP_RECTANGLE;
-            const double a[9] = {r->p1.x, r->p1.y, r->p1.z, r->p2.x, r->p2.y, r->p2.z, r->p3.x, r->p3.y, r->p3.z};
-            std::copy(a, a + 9, d.args);
-        } else if (auto* b = dynamic_cast<const ExpBox*>(e)) {
-            d.kind = GI_EXP_BOX;
-            const double a[6] = {b->min.x, b->min.y, b->min.z, b->max.x, b->max.y, b->max.z};
-            std::copy(a, a + 6, d.args);
-        } else {
-            return false;
-        }
-        set_material(d, e->material);
-        return true;
-    }
-
-    bool upload() {
+    bool upload(const std::vector<gi_entity_desc>& ents, const double mn[3], const double mx[3], uint64_t hash) {
         if (gi_abi_version() != GI_ABI_VERSION) {   // gi.h's structs must match the loaded libgi
             std::fprintf(stderr, "gi: libgi ABI %d, built against %d\n", gi_abi_version(), GI_ABI_VERSION);
             return false;
         }
-        std::vector<gi_entity_desc> ents;
-        for (const Entity* e : _scene->entities()) {
-            gi_entity_desc d;
-            if (!describe(e, d)) {
-                std::fprintf(stderr, "gi: unknown entity type (not one of entities.h's eight)\n");
-                return false;
-            }
-            ents.push_back(d);
-        }
         gi_scene_desc sd = {};
         for (int k = 0; k < 3; ++k) {
-            sd.octree_min[k] = _scene->min[k];
-            sd.octree_max[k] = _scene->max[k];
+            sd.octree_min[k] = mn[k];
+            sd.octree_max[k] = mx[k];
         }
         sd.n_entities = (int32_t)ents.size();
         sd.entities = ents.data();
-        gi_scene* s = nullptr;
-        if (gi_scene_create(&sd, &s) != GI_OK) {
+        auto g = std::make_shared<Gpu>();
+        const std::vector<int> devs = devices();
+        if (devs.size() > 1) {
+            if (gi_multi_create(&sd, (int)devs.size(), devs.data(), &g->multi) != GI_OK) {
+                std::fprintf(stderr, "gi_multi_create: %s\n", gi_last_error());
+                return false;
+            }
+        } else if (gi_scene_create(&sd, &g->scene) != GI_OK) {
             std::fprintf(stderr, "gi_scene_create: %s\n", gi_last_error());
             return false;
         }
-        _gpu = std::shared_ptr<gi_scene>(s, gi_scene_destroy);
-        _gpu_generation = _scene->generation();
+        g->hash = hash;
+        _gpu = g;
         return true;
     }
 
@@ -176,6 +160,5 @@ class RayTracer {
     Camera _camera;
     glm::dvec3 _light;
     std::shared_ptr<Image> _image;
-    std::shared_ptr<gi_scene> _gpu;   // shared by copies (Gui/Viewer copy the RayTracer by value)
-    std::size_t _gpu_generation = 0;
+    std::shared_ptr<Gpu> _gpu;   // shared by copies (Gui/Viewer copy the RayTracer by value)
 };

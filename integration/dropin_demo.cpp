@@ -6,7 +6,10 @@
 // (gui.h:19,35).  Writes the RGB888 frame the Viewer would paint.
 // With "zoo" it builds the every-entity scene of scenes.zoo_scene() instead (entities.h's eight
 // entity classes, constructed by the reference's own constructors).
-//   dropin_demo <w> <h> <out.rgb> [zoo]
+// With a 5th argument "cands" it writes, instead of a frame, the length of the drop-in
+// Octree::intersect(const Ray&) candidate list (octree.h:46-68) for every pixel's primary ray
+// (raytracer.h:26-30, 41-43), as int32 -- compared with the compiled reference's lists.
+//   dropin_demo <w> <h> <out> [zoo|main] [cands]
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -40,6 +43,23 @@ int main(int argc, char** argv) {
         scene.push_back(q);
         scene.push_back(s2);
         scene.push_back(s3);
+    }
+    if (argc > 5 && std::string(argv[5]) == "cands") {
+        // raytracer.h:26-30 (vertical offset from w, A.12) and :41-43
+        const glm::dvec3 left = glm::normalize(glm::cross(camera.up, camera.forward));
+        const glm::dvec2 res{0.0002, 0.0002};
+        const glm::dvec3 top_left = ((camera.pos + camera.focalDist * camera.forward) + left * (double)w * 0.5 * res.x +
+                                     camera.up * (double)w * 0.5 * res.y) - camera.pos;
+        FILE* f = std::fopen(argv[3], "wb");
+        if (!f) return 1;
+        for (int y = 0; y < h; ++y)
+            for (int x = 0; x < w; ++x) {
+                const glm::dvec3 dir = top_left - left * (double)x * res.x - camera.up * (double)y * res.y;
+                const int32_t n = (int32_t)scene.intersect(Ray(camera.pos, dir)).size();
+                std::fwrite(&n, 4, 1, f);
+            }
+        std::fclose(f);
+        return 0;
     }
     raytracer.setScene(&scene);
     RayTracer viewer_copy = raytracer;

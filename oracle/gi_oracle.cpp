@@ -550,7 +550,7 @@ struct Octree {
 
     void init(V3 mn, V3 mx) { nodes.clear(); nodes.push_back(Node{mn, mx, {}, -1}); }
 
-    void partition(int ni) {   // octree.h:176-211
+    void partition(int ni) {   // octree.h:75-110
         if (nodes[ni].child0 >= 0) return;
         const V3 mn = nodes[ni].mn, mx = nodes[ni].mx;
         const V3 mid = (mn + mx) * 0.5;
@@ -575,7 +575,7 @@ struct Octree {
         nodes[ni].child0 = c0;
     }
 
-    void push_obj(int ni, int e) {   // octree.h:216-230
+    void push_obj(int ni, int e) {   // octree.h:115-129
         nodes[ni].ents.push_back(e);
         partition(ni);
         if (nodes[ni].child0 < 0) return;
@@ -587,7 +587,7 @@ struct Octree {
         }
     }
 
-    void push_back(int e) {   // octree.h:121-144
+    void push_back(int e) {   // octree.h:20-43
         const Ent& E = (*ents)[e];
         if (!bb_intersect(nodes[0].mn, nodes[0].mx, E.bmin, E.bmax)) return;   // A.14
         push_obj(0, e);
@@ -614,7 +614,7 @@ bool box_hit(V3 mn, V3 mx, V3 o, V3 d) {
     return hit;
 }
 
-void query(const Octree& t, int ni, V3 o, V3 d, std::vector<int>& out, int& ntests) {   // octree.h:233-256
+void query(const Octree& t, int ni, V3 o, V3 d, std::vector<int>& out, int& ntests) {   // octree.h:132-155
     const Node& n = t.nodes[ni];
     if (n.child0 < 0) { out.insert(out.end(), n.ents.begin(), n.ents.end()); return; }
     for (int c = 0; c < 8; ++c) {

@@ -7,7 +7,7 @@
 //
 //   render  <scene.scn> <w> <h> <out.bin> [x0 y0 x1 y1 [stride]]
 //       Per-pixel restatement of RayTracer::run's body (raytracer.h:41-84): Octree::intersect
-//       (octree.h:147-169), Entity::intersect (entities.h:26), last-hit-wins selection
+//       (octree.h:46-68), Entity::intersect (entities.h:26), last-hit-wins selection
 //       (raytracer.h:53-74), getTextureCoord (entities.h:32), Material::blinn_phong_texture
 //       (material.h:48-62) and Image::setPixel's (int)(255*c) quantisation (image.h:14-16).
 //       Records fp64 radiance, hit entity, (u,v), candidate count and node-test count.
@@ -33,7 +33,7 @@
 #include "material.h"
 #include "bbox.h"
 #include "entities.h"
-#define private public   // node-level statistics need Octree::Node (octree.h:171-261)
+#define private public   // node-level statistics need Octree::Node (octree.h:71-160)
 #include "octree.h"
 #undef private
 
@@ -92,7 +92,7 @@ static bool load_scene(const char* path, Scene& s) {
     return true;
 }
 
-// Node-test counter: same DFS as Octree::Node::intersect (octree.h:233-256), counting ExpBox tests.
+// Node-test counter: same DFS as Octree::Node::intersect (octree.h:132-155), counting ExpBox tests.
 static long g_node_tests = 0;
 static std::vector<Entity*> counted_intersect(const Octree::Node& n, const Ray& ray) {
     if (n.is_leaf()) return n._entities;

@@ -103,3 +103,71 @@ def test_soup_vertex_generator():
     assert v.shape == (1000, 3, 3)
     assert (np.abs(v - c[:, None, :]) <= 0.3 + 1e-12).all()   # vertices within 0.15 of the drawn centre
     assert -0.15 <= c[:, 0].min() and c[:, 0].max() <= 10.15
+
+
+def _primary_dirs(sc, w, xs, ys):
+    """raytracer.h:26-30, 41-43 in fp64 with glm's operation order (same as the kernels' make_cam /
+    primary_dir): the un-normalised primary directions of pixels (xs, ys)."""
+    pos = np.array(sc.cam_pos, np.float64)
+    look = np.array(sc.cam_look, np.float64)
+    f = look - pos
+    f = f * (1.0 / np.sqrt((f[0] * f[0] + f[1] * f[1]) + f[2] * f[2]))
+    up = np.array([0.0, 0.0, 1.0])
+    left = np.array([up[1] * f[2] - f[1] * up[2], up[2] * f[0] - f[2] * up[0], up[0] * f[1] - f[0] * up[1]])
+    left = left * (1.0 / np.sqrt((left[0] * left[0] + left[1] * left[1]) + left[2] * left[2]))
+    rx = ry = 0.0002
+    tl = (((pos + sc.focal * f) + ((left * float(w)) * 0.5) * rx) + ((up * float(w)) * 0.5) * ry) - pos
+    out = []
+    for x, y in zip(xs, ys):
+        out.append((tl - (left * float(x)) * rx) - (up * float(y)) * ry)
+    return pos, out
+
+
+@pytest.mark.parametrize("name", ["cornell_128x128", "zoo_160x160", "soup1000_160x160", "main_200x200"])
+def test_octree_intersect_candidate_lists_match_reference(name):
+    """Octree::intersect(const Ray&) (octree.h:46-68) through the C-ABI's host octree
+    (gi_octree_intersect, no device): for every golden pixel, the candidate list has the length the
+    compiled reference's list had (ncand) and contains the entity the reference chose (hit)."""
+    import json
+    z = np.load(os.path.join(U.GOLDEN, name + ".npz"))
+    meta = json.loads(str(z["meta"]))
+    sc = S.named_scene(meta["scene"])
+    tree = gi.Octree.from_scene(sc)
+    idx = np.arange(len(z["x"]))[::7]
+    pos, dirs = _primary_dirs(sc, meta["w"], z["x"][idx], z["y"][idx])
+    for i, d in zip(idx, dirs):
+        cand = tree.intersect(pos, d)
+        assert len(cand) == int(z["ncand"][i]), (int(z["x"][i]), int(z["y"][i]))
+        if z["hit"][i] >= 0:
+            assert tree.entities[int(z["hit"][i])] in cand
+
+
+def test_error_paths_without_device():
+    """gi_multi_create with no GPU fails with GI_ERR_DEVICE (no CPU fallback); argument errors are
+    GI_ERR_ARG; gi_device_count is 0."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    L = gi.lib()
+    assert L.gi_device_count() == 0
+    with pytest.raises(gi.GIError, match=r"\(-2\)"):
+        gi.MultiScene.from_scene(S.sphere_scene(), [0, 0])
+    h = ctypes.c_void_p()
+    assert L.gi_multi_create(None, 1, None, ctypes.byref(h)) == -1
+    assert L.gi_octree_create(None, ctypes.byref(h)) == -1
+
+
+@pytest.mark.parametrize("scene,w,h", [("main", 200, 200), ("zoo", 160, 160)])
+def test_cpp_dropin_octree_intersect_matches_reference(tmp_path, scene, w, h):
+    """include/gi_dropin/octree.h's Octree::intersect(const Ray&) (octree.h:46-68), called from the
+    reference app's own classes (integration/dropin_demo.cpp, built where the reference tree
+    exists): candidate-list lengths equal the compiled reference's on every pixel's primary ray."""
+    exe = os.path.join(U.ROOT, "integration", "_build", "dropin_demo")
+    if not os.path.exists(exe):
+        pytest.skip("integration/_build/dropin_demo not built (needs the reference tree)")
+    out = tmp_path / "c.bin"
+    subprocess.run([exe, str(w), str(h), str(out), scene, "cands"], check=True, timeout=120)
+    c = np.fromfile(out, np.int32)
+    z = np.load(os.path.join(U.GOLDEN, f"{scene}_{w}x{h}.npz"))
+    assert c.size == w * h
+    assert (c[z["y"] * w + z["x"]] == z["ncand"]).all()

@@ -717,3 +717,104 @@ def test_mode_x_non_integer_specular_power(torch_cuda, spec_pow):
     rgb, rgb8 = d.render(cam_of(s), s.light, w, h, mode=gi.MODE_X, spp=2, depth=4, seed=3)
     assert U.bits_equal(rgb.reshape(-1, 3), o["rgb"]).all()
     assert (rgb8.reshape(-1, 3) == o["q"]).all()
+
+
+# ---- several GPUs through the C-ABI (gi_multi_*) -------------------------------------------------
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+def test_multi_render_equals_single_device(torch_cuda, devices):
+    """gi_multi_render (tile shards over the listed devices, gathered to devices[0]) against
+    gi_render on one device, bit for bit: Mode R with progressive bands, Mode X with spp > 1.  On a
+    one-GPU box the shards share device 0 (the RCCL route is tested separately, below)."""
+    sc = S.cornell_scene()
+    single = dev_scene("cornell")
+    m = gi.MultiScene.from_scene(sc, devices)
+    assert m.info() == {"shards": len(devices), "devices": 1, "rccl": False}
+    w, h = 203, 117
+    for kw in (dict(mode=gi.MODE_R, band_rows=24), dict(mode=gi.MODE_X, spp=3, depth=4, seed=9)):
+        a, a8 = single.render(cam_of(sc), sc.light, w, h, **kw)
+        b, b8 = m.render(cam_of(sc), sc.light, w, h, **kw)
+        assert U.bits_equal(a, b).all(), kw
+        assert (a8 == b8).all(), kw
+    m.close()
+
+
+def test_multi_render_through_rccl(torch_cuda, tmp_path):
+    """The RCCL gather itself (ncclCommInitAll + a group of ncclSend/ncclRecv, rccl.h:236, 700-725):
+    GI_MULTI_RCCL=1 routes every shard through RCCL even on one device (rank 0 sends to itself), in
+    a child process with its own time limit.  The frame equals the one-device frame bit for bit."""
+    import subprocess
+    import sys
+    sc = S.cornell_scene()
+    w, h = 160, 96
+    out = tmp_path / "m.npy"
+    code = ("import sys, numpy as np; sys.path.insert(0, %r); sys.path.insert(0, %r); import oracle_util as U; "
+            "gi = U.pkg(); S = U.scenes(); sc = S.cornell_scene(); "
+            "m = gi.MultiScene.from_scene(sc, [0, 0]); info = m.info(); assert info['rccl'], info; "
+            "rgb, rgb8 = m.render(gi.Camera(sc.cam_pos, sc.cam_look, sc.focal), sc.light, %d, %d, mode=gi.MODE_X, "
+            "spp=2, depth=3, seed=4, band_rows=48); np.save(%r, rgb); m.close(); print('rccl ok', info)"
+            ) % (U.ROOT, os.path.join(U.ROOT, "tests"), w, h, str(out))
+    r = subprocess.run([sys.executable, "-c", code], timeout=180, capture_output=True, text=True,
+                       env=dict(os.environ, GI_MULTI_RCCL="1", NCCL_DEBUG="WARN"))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    got = np.load(out)
+    ref, _ = dev_scene("cornell").render(cam_of(sc), sc.light, w, h, mode=gi.MODE_X, spp=2, depth=3, seed=4)
+    assert U.bits_equal(got, ref).all()
+
+
+def test_cpp_dropin_multi_device_matches_reference_run(torch_cuda, tmp_path):
+    """The drop-in RayTracer with GI_DEVICES=0,0 (two tile shards through gi_multi) still gives
+    RayTracer::run's frame of the main.cpp scene."""
+    import subprocess
+    exe = os.path.join(U.ROOT, "integration", "_build", "dropin_demo")
+    if not os.path.exists(exe):
+        pytest.skip("integration/_build/dropin_demo not built (needs the reference tree)")
+    out = tmp_path / "f.rgb"
+    env = dict(os.environ, QT_QPA_PLATFORM="offscreen", GI_DEVICES="0,0")
+    subprocess.run([exe, "200", "200", str(out)], check=True, env=env, timeout=120)
+    got = np.frombuffer(out.read_bytes(), np.uint8).reshape(200, 200, 3)
+    z = np.load(os.path.join(GOLD, "main_200x200.npz"))
+    assert (got == z["run_q"]).all()
+
+
+def test_renders_on_two_streams_are_ordered(torch_cuda):
+    """One scene, a Mode X gi_render_device on a side stream immediately followed by gi_render on
+    the scene's own stream (they share the scene's work list): the library orders them, both frames
+    are right (per-scene launches ordered by an event)."""
+    torch = torch_cuda
+    sc = S.cornell_scene()
+    d = gi.DeviceScene.from_scene(sc)
+    w, h, kw = 160, 120, dict(mode=gi.MODE_X, spp=4, depth=4, seed=21)
+    ref, _ = d.render(cam_of(sc), sc.light, w, h, **kw)
+    side = torch.cuda.Stream()
+    buf = torch.zeros(w * h * 3, dtype=torch.float64, device="cuda")
+    for _ in range(3):
+        d.render_device(cam_of(sc), sc.light, w, h, buf.data_ptr(), stream=side.cuda_stream, **kw)
+        host, _ = d.render(cam_of(sc), sc.light, w, h, mode=gi.MODE_X, spp=2, depth=3, seed=5)
+    side.synchronize()
+    assert U.bits_equal(buf.cpu().numpy().reshape(h, w, 3), ref).all()
+    o = U.oracle_render(sc.to_scn(), w, h, mode=1, spp=2, depth=3, seed=5)
+    assert U.bits_equal(host.reshape(-1, 3), o["rgb"]).all()
+
+
+def test_python_raytracer_sees_push_back_after_first_run(torch_cuda):
+    """RayTracer.run reads the live octree (raytracer.h:45): an entity pushed after the first run
+    appears in the next frame (the scene is re-uploaded when Octree.generation changes)."""
+    sc = S.main_scene()
+    rt = gi.RayTracer(gi.Camera(sc.cam_pos, sc.cam_look, sc.focal), sc.light)
+    tree = gi.Octree(sc.octree_min, sc.octree_max)
+    tree.push_back(gi.ImpSphere((5.0, 0.0, 0.0), 1, (1, 0, 0)))
+    rt.setScene(tree)
+    rt.start()
+    rt.run(64, 64)
+    a = rt.getImage().rgb8.copy()
+    assert a.any()
+    tree.push_back(gi.ImpSphere((2.0, 0.3, 0.3), 0.3, (0, 0, 1)))
+    rt.start()
+    rt.run(64, 64)
+    b = rt.getImage().rgb8
+    assert (a != b).any()
+    s2 = S.Scene(entities=[])
+    s2.imp_sphere((5.0, 0.0, 0.0), 1, (1, 0, 0))
+    s2.imp_sphere((2.0, 0.3, 0.3), 0.3, (0, 0, 1))
+    o = U.oracle_render(s2.to_scn(), 64, 64)
+    assert (b.reshape(-1, 3) == o["q"]).all()
