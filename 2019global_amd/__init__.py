@@ -49,6 +49,7 @@ FLAG_TIME = 4    # HIP events around the dominant kernel; read with DeviceScene.
 STAT_RAYS, STAT_NODES, STAT_PRIMS, STAT_PIXELS, STAT_PBOX = 0, 1, 2, 3, 4
 STAT_X_ITERS, STAT_X_TRAV, STAT_X_HANDLE, STAT_X_HLANES, STAT_X_HCLOSE, STAT_X_HSHADOW = 5, 6, 7, 8, 9, 10
 STAT_X_CYC_TRAV, STAT_X_CYC_HIT, STAT_X_CYC_NEXT, STAT_X_CYC_ALL = 11, 12, 13, 14
+STAT_X_RESOLVED = 15
 STATS_N = 16
 TILE = 8
 ABI_VERSION = 5

@@ -533,7 +533,7 @@ __device__ __forceinline__ void r_consider(const DevScene& sc, int e, V3 o, V3 d
     }
 }
 
-__device__ void trace_mode_r_cand(const DevScene& sc, V3 o, V3 d, float tau, RResult& r, uint32_t& nnode,
+__device__ __forceinline__ void trace_mode_r_cand(const DevScene& sc, V3 o, V3 d, float tau, RResult& r, uint32_t& nnode,
                                   uint32_t& nprim) {
     r.ent = -1;
     long long best = -1;
@@ -737,7 +737,7 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 #endif
 
 struct XCounters {
-    uint64_t rays = 0, nodes = 0, prims = 0, px = 0, box = 0;
+    uint64_t rays = 0, nodes = 0, prims = 0, px = 0, res = 0;   // res: samples resolved without traversal
     uint64_t iters = 0, trav = 0, handle = 0, hlanes = 0, hclose = 0, hshadow = 0;   // wave-level (lane 0)
     uint64_t cyc_trav = 0, cyc_hit = 0, cyc_next = 0, cyc_all = 0;                    // wave clock cycles
 };
@@ -800,7 +800,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     if (lane == 0) blk_meta[0] = 64u;
     __builtin_amdgcn_wave_barrier();
     const bool inline_shadow = (xflags & 1) != 0;
-    uint32_t nnode = 0, nprim = 0, nrays = 0, nbox = 0, npx = 0, nsteps = 0;
+    uint32_t nnode = 0, nprim = 0, nrays = 0, nres = 0, npx = 0, nsteps = 0;
     long long idx = -1;
     int x = 0, y = 0;
     uint64_t key = 0;
@@ -1139,6 +1139,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                                           __builtin_amdgcn_rcpf((float)d0.z));
                         if (!root_hit(sc, f3((float)cam.pos.x, (float)cam.pos.y, (float)cam.pos.z), iv0)) {
                             ++nrays;   // background sample: L = 0
+                            ++nres;
                             if (spp > 1) {
                                 double* q = wk.part + 3 * ((size_t)idx * (size_t)spp + (size_t)smp);
                                 q[0] = 0.0; q[1] = 0.0; q[2] = 0.0;
@@ -1195,7 +1196,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     cnt.nodes += nnode;
     cnt.prims += nprim;
     cnt.px += npx;
-    cnt.box += nbox;
+    cnt.res += nres;
 }
 
 // Persistent waves: the grid is sized to the resident capacity; every lane pulls pixel slots
@@ -1259,9 +1260,9 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
             atomicAdd(stats + GI_STAT_X_CYC_ALL, (unsigned long long)c.cyc_all);
         }
         wave_add_stats(stats, c.rays, c.nodes, c.prims, c.px);
-        uint64_t cb = c.box;
-        for (int off = 32; off > 0; off >>= 1) cb += __shfl_xor(cb, off);
-        if ((threadIdx.x & 63) == 0) atomicAdd(stats + GI_STAT_PBOX, (unsigned long long)cb);
+        uint64_t cr = c.res;
+        for (int off = 32; off > 0; off >>= 1) cr += __shfl_xor(cr, off);
+        if ((threadIdx.x & 63) == 0) atomicAdd(stats + GI_STAT_X_RESOLVED, (unsigned long long)cr);
     }
 }
 
@@ -1300,8 +1301,12 @@ __global__ __launch_bounds__(256) void k_x_classify(DevScene sc, CamDev cam, Til
         base = __shfl(base, leader);
         if (scene) list[base + (unsigned)__popcll(ms & ((1ull << lane) - 1))] = (unsigned)s;
     }
-    if (STATS && (s & ~63ll) < m.n_local * 64)
+    if (STATS && (s & ~63ll) < m.n_local * 64) {
         wave_add_stats(stats, bg ? (uint64_t)spp : 0, 0, 0, bg ? 1 : 0);
+        uint64_t r = bg ? (uint64_t)spp : 0;   // samples resolved here, without traversal
+        for (int off = 32; off > 0; off >>= 1) r += __shfl_xor(r, off);
+        if (lane == 0 && r) atomicAdd(stats + GI_STAT_X_RESOLVED, (unsigned long long)r);
+    }
 }
 
 // Mode X pass 3 (spp > 1): a listed pixel's per-sample radiance added in sample order from +0, then
@@ -1352,7 +1357,7 @@ __global__ __launch_bounds__(256) void k_box_kat(int n, const double* recs, int3
                      normalize(v3(q[9], q[10], q[11]))) ? 1 : 0;
 }
 
-__global__ void k_trace_ray(DevScene sc, V3 o, V3 d, V3 light, int32_t* out_i, double* out_d) {
+__global__ __launch_bounds__(64) void k_trace_ray(DevScene sc, V3 o, V3 d, V3 light, int32_t* out_i, double* out_d) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     RResult r;
     uint32_t nn = 0, np = 0;

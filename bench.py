@@ -45,7 +45,6 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 NODE_BYTES = {0: 64, 1: 256}   # RNode / XWNode (8 child boxes) records
 PRIM_BYTES = {0: 144, 1: 80}   # Mode R: TriRec (sphere/quad records are <= 160 B) / Mode X: XHot fp64 record
-PBOX_BYTES = 32                # Mode X: XBox fp32 prefilter record
 
 WORKLOADS = {
     # name: (scene, w, h, mode, spp, depth, description)
@@ -68,17 +67,91 @@ def make_scene(name):
     return import_module("2019global_amd.scenes").named_scene(name)
 
 
-def pmc_traffic(workload: str):
-    """HBM bytes per launch of the dominant kernel from the committed PMC summary, if any."""
+FP64_VALU_PEAK_TFS = 78.6     # MI355X FP64 vector peak (AMD spec; half the guide's 157.3 TF FP32 vector rate)
+N_SIMDS = 1024                 # 256 CUs x 4 SIMDs
+
+
+def pmc_summary(workload: str):
+    """The latest committed rocprofv3 PMC summary of this workload's dominant kernel
+    (profiles/rNN_<workload>_pmc.json, written by profiles/summarize.py), or None."""
     best = None
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json"))):
         try:
             d = json.load(open(p))
         except Exception:
             continue
-        if d.get("workload") == workload and d.get("hbm_bytes_per_launch"):
-            best = d["hbm_bytes_per_launch"]
+        if d.get("workload") == workload and d.get("counters_per_launch"):
+            best = (os.path.relpath(p, ROOT), d)
     return best
+
+
+def counter_ceilings(workload: str, kern_ms: float):
+    """What the dominant kernel meets, from the committed PMC summary of the same workload:
+      * HBM: counter bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction) / live kernel
+        time / 8 TB/s -- the bytes that actually reach HBM;
+      * VALU: issue share = SQ_INSTS_VALU x 4 cycles / (1,024 SIMDs x kernel cycles, GRBM_GUI_ACTIVE / 8)
+        and lane utilisation = SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU); their product is
+        the fraction of the chip's VALU lane-slots doing work;
+      * FP64 (Mode R): f64 VALU instructions / all VALU instructions, and the f64 FLOP
+        rate they imply (FMA = 2, every lane counted) against the 78.6 TF/s FP64 vector peak.
+    `binding` names the tightest: valu_issue when the SIMDs issue in >= 75% of their slots,
+    else hbm when counter traffic is >= 60% of peak, else latency (waiting on memory)."""
+    got = pmc_summary(workload)
+    if got is None:
+        return None
+    src, d = got
+    c = d["counters_per_launch"]
+    out = {"pmc_source": src, "pmc_kernel_ms": round(d.get("avg_launch_ns", 0) / 1e6, 4)}
+    hbm = d.get("hbm_bytes_per_launch")
+    if hbm:
+        out["hbm_counter_bytes"] = int(hbm)
+        out["hbm_counter_frac"] = round(hbm / (kern_ms * 1e-3) / (HBM_PEAK_GBS * 1e9), 5)
+    if c.get("GRBM_GUI_ACTIVE") and c.get("SQ_INSTS_VALU"):
+        cycles = c["GRBM_GUI_ACTIVE"] / 8.0
+        out["valu_issue_frac"] = round(c["SQ_INSTS_VALU"] * 4.0 / (N_SIMDS * cycles), 4)
+    if c.get("SQ_ACTIVE_INST_VALU") and c.get("SQ_THREAD_CYCLES_VALU"):
+        out["valu_lane_util"] = round(c["SQ_THREAD_CYCLES_VALU"] / (64.0 * c["SQ_ACTIVE_INST_VALU"]), 4)
+    if "valu_issue_frac" in out and "valu_lane_util" in out:
+        out["valu_frac"] = round(out["valu_issue_frac"] * out["valu_lane_util"], 4)
+    if c.get("SQ_WAVE_CYCLES") and c.get("SQ_WAIT_ANY"):
+        out["wait_share"] = round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 4)
+    f64 = [c.get(k) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                              "SQ_INSTS_VALU_TRANS_F64")]
+    if all(v is not None for v in f64) and c.get("SQ_INSTS_VALU"):
+        add, mul, fma, trans = f64
+        out["f64_inst_share"] = round((add + mul + fma + trans) / c["SQ_INSTS_VALU"], 4)
+        flops = 64.0 * (add + mul + 2.0 * fma + trans)
+        out["f64_tflops_upper"] = round(flops / (kern_ms * 1e-3) / 1e12, 3)
+        out["f64_valu_frac"] = round(out["f64_tflops_upper"] / FP64_VALU_PEAK_TFS, 4)
+    if c.get("SQ_INSTS_VALU_FLOPS_FP64") is not None:   # the counter's own f64 FLOP count
+        out["f64_tflops_counter"] = round(c["SQ_INSTS_VALU_FLOPS_FP64"] / (kern_ms * 1e-3) / 1e12, 3)
+        out["f64_valu_frac_counter"] = round(out["f64_tflops_counter"] / FP64_VALU_PEAK_TFS, 4)
+    if out.get("valu_issue_frac", 0) >= 0.75:
+        out["binding"] = "valu_issue"
+    elif out.get("hbm_counter_frac", 0) >= 0.6:
+        out["binding"] = "hbm"
+    else:
+        out["binding"] = "latency"
+    return out
+
+
+def cpu_info():
+    model = "?"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return model, os.cpu_count() or 1
+
+
+def cpu_threads():
+    """Threads for the CPU port: OMP_NUM_THREADS when set (the GPU box sets it to this job's CPU share,
+    16; os.cpu_count() there reports the whole machine), else every core."""
+    v = os.environ.get("OMP_NUM_THREADS")
+    return max(1, int(v)) if v and v.isdigit() else (os.cpu_count() or 1)
 
 
 def cpu_baseline(scn_text, w, h, mode, spp, depth, seed, target_s=20.0):
@@ -86,7 +159,7 @@ def cpu_baseline(scn_text, w, h, mode, spp, depth, seed, target_s=20.0):
     a 256x96 probe sets the rate, then a window sized for about `target_s` seconds is timed."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_util as U
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads = cpu_threads()
 
     def window(ww, wh):
         cx, cy = w // 2, (int(h * 0.8) if mode == 1 else h // 2)
@@ -107,9 +180,13 @@ def cpu_baseline(scn_text, w, h, mode, spp, depth, seed, target_s=20.0):
         f = min(scale ** 0.5, max(w / (win[2] - win[0]), h / (win[3] - win[1])))
         win = window(min(w, int((win[2] - win[0]) * f)), min(h, int((win[3] - win[1]) * f)))
         rays, dt = run(win)
+    model, host_cores = cpu_info()
     return {"value": round(rays / dt / 1e6, 4), "unit": "Mray/s", "cores": threads, "kind": "port",
+            "cpu_model": model, "host_cores": host_cores,
             "sample": f"window x[{win[0]},{win[2]}) y[{win[1]},{win[3]}) of the same frame, {rays} rays, "
-                      f"{dt:.2f} s wall, OpenMP"}
+                      f"{dt:.2f} s wall, OpenMP over {threads} threads (OMP_NUM_THREADS; the host has "
+                      f"{host_cores} logical CPUs); closest-hit queries by the oracle's own BVH for scenes "
+                      f"above 256 primitives, brute force below"}
 
 
 def reference_cpu(scn_text, w, h):
@@ -129,7 +206,9 @@ def reference_cpu(scn_text, w, h):
         except Exception as e:   # never fail the bench on the optional reference leg
             return {"error": str(e)[:200]}
     r = json.loads(out)
+    model, host_cores = cpu_info()
     return {"value": round(r["mray_s"], 6), "unit": "Mray/s", "cores": 1, "kind": "reference",
+            "cpu_model": model, "host_cores": host_cores,
             "sample": f"depth 1 (the reference's only depth), every {stride}th pixel, {r['rays']} rays"}
 
 
@@ -283,9 +362,11 @@ def main():
         value = rays_frame * args.steps / elapsed / 1e6
         # algorithmic bytes per launch of the dominant kernel (this rank's launch; N=1: the frame)
         alg = (st[gi.STAT_NODES] * NODE_BYTES[mode] + st[gi.STAT_PRIMS] * PRIM_BYTES[mode] +
-               st[gi.STAT_PBOX] * PBOX_BYTES + st[gi.STAT_PIXELS] * 27) / world
+               st[gi.STAT_PIXELS] * 27) / world
         achieved = alg / (kern_ms * 1e-3) / 1e9
-        traffic = pmc_traffic(args.workload) if world == 1 else None
+        ceil = counter_ceilings(args.workload, kern_ms) if world == 1 else None
+        traffic = ceil.get("hbm_counter_bytes") if ceil else None
+        resolved = st[gi.STAT_X_RESOLVED] if mode == 1 else 0
         out = {
             "metric": "Mray/s + ms/frame at 1920x1080, depth 8; %HBM roofline",
             "value": round(value, 3),
@@ -302,17 +383,24 @@ def main():
             "config": {"workload": f"{args.workload}: {desc}", "mode": "X" if mode == 1 else "R", "width": w,
                        "height": h, "spp": spp, "depth": depth, "seed": args.seed,
                        "rays_per_frame": rays_frame, "primary_rays_per_frame": w * h * spp,
+                       # rays that reached the BVH: rays_per_frame minus the primary samples resolved
+                       # by the pixel-frustum classify and the root-box pretest (each adds exactly +0)
+                       "rays_traced_per_frame": rays_frame - resolved,
                        "parallelism": f"tile-shard{world}"},
             # primary (w*h*spp) and total (primary + bounce + shadow) rays per second
             "mray_s_primary": round(w * h * spp * args.steps / elapsed / 1e6, 3),
+            "mray_s_traced": round((rays_frame - resolved) * args.steps / elapsed / 1e6, 3),
             "roofline": {"bound": "hbm", "kernel": "k_mode_x" if mode == 1 else "k_mode_r",
                          "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "alg_bytes_per_launch": int(alg),
                          "kernel_ms": round(kern_ms, 4), "render_call_ms": round(render_ms, 4),
                          "node_visits": st[gi.STAT_NODES], "prim_tests": st[gi.STAT_PRIMS],
-                         "prim_box_tests": st[gi.STAT_PBOX]},
+                         "alg_bytes_note": "algorithmic record bytes; for LDS-resident scenes (C2/C3) they "
+                                           "are served from LDS, see hbm_counter_frac / binding"},
         }
+        if ceil:
+            out["roofline"].update({k: v for k, v in ceil.items() if k != "hbm_counter_bytes"})
         if frame_check is not None:
             out["frame_check"] = frame_check
             if args.dist_backend != "nccl":
@@ -331,6 +419,9 @@ def main():
                                                 ("next_ray", gi.STAT_X_CYC_NEXT))}}
         if world == 1 and not args.no_host_path:
             out["host_path"] = host_path(dev, cam, sc.light, w, h, mode, spp, depth, args.seed)
+            # SURVEY §8(d) ms/frame: the end-to-end gi_render time with the framebuffer's D2H copy
+            # (RGB888, the reference Image's content) included
+            out["ms_per_frame_with_d2h"] = out["host_path"]["ms_per_frame"]["rgb8"]
         if not args.no_cpu_baseline and world == 1:
             scn = sc.to_scn()
             out["cpu_baseline"] = cpu_baseline(scn, w, h, mode, spp, depth, args.seed)

@@ -122,7 +122,7 @@ typedef struct gi_opts {
 #define GI_STAT_NODES 1       /* octree node records fetched & tested */
 #define GI_STAT_PRIMS 2       /* primitive records fetched & tested in fp64 */
 #define GI_STAT_PIXELS 3
-#define GI_STAT_PBOX 4        /* Mode X primitive prefilter boxes tested (32-B fp32 records) */
+#define GI_STAT_PBOX 4        /* unused (was: Mode X primitive prefilter boxes); always 0 */
 #define GI_STAT_X_ITERS 5     /* Mode X: wave loop iterations (per wave) */
 #define GI_STAT_X_TRAV 6      /* Mode X: lane traversal steps (sum of active lanes over iterations) */
 #define GI_STAT_X_HANDLE 7    /* Mode X: shading-handler executions (per wave) */
@@ -133,6 +133,8 @@ typedef struct gi_opts {
 #define GI_STAT_X_CYC_HIT 12  /* Mode X: wave clock cycles consuming finished rays (shading) */
 #define GI_STAT_X_CYC_NEXT 13 /* Mode X: wave clock cycles starting rays (raygen, pixel fetch, root test) */
 #define GI_STAT_X_CYC_ALL 14  /* Mode X: wave clock cycles in the whole loop */
+#define GI_STAT_X_RESOLVED 15 /* Mode X: primary samples resolved without traversal (pixel-frustum classify
+                                 and root-box pretest misses; each still adds exactly +0, as traced) */
 #define GI_STATS_N 16
 
 #define GI_TILE 8             /* shard granularity: 8x8 pixel tiles, dealt round-robin to ranks */

@@ -171,3 +171,30 @@ def test_cpp_dropin_octree_intersect_matches_reference(tmp_path, scene, w, h):
     z = np.load(os.path.join(U.GOLDEN, f"{scene}_{w}x{h}.npz"))
     assert c.size == w * h
     assert (c[z["y"] * w + z["x"]] == z["ncand"]).all()
+
+
+def test_allocation_failure_returns_nomem_not_abort(tmp_path):
+    """No exception crosses the C-ABI (gi.h): a scene too large for the host memory the process may
+    use makes gi_octree_create return GI_ERR_NOMEM (-5) instead of terminating the caller.  A child
+    process under RLIMIT_AS = 8 GiB asks for 2^31 - 1 entities (the builder's first vector alone
+    needs far more)."""
+    import sys
+    code = (
+        "import ctypes, resource, sys\n"
+        "resource.setrlimit(resource.RLIMIT_AS, (8 << 30, 8 << 30))\n"
+        "sys.path.insert(0, %r)\n"
+        "from importlib import import_module\n"
+        "gi = import_module('2019global_amd')\n"
+        "L = ctypes.CDLL(gi.LIB_PATH)\n"
+        "L.gi_last_error.restype = ctypes.c_char_p\n"
+        "d = gi.SceneDesc()\n"
+        "one = (gi.EntityDesc * 1)()\n"
+        "d.n_entities = 2**31 - 1\n"
+        "d.entities = ctypes.cast(one, ctypes.POINTER(gi.EntityDesc))\n"
+        "h = ctypes.c_void_p()\n"
+        "rc = L.gi_octree_create(ctypes.byref(d), ctypes.byref(h))\n"
+        "print('rc', rc, L.gi_last_error().decode())\n"
+    ) % U.ROOT
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "rc -5 host memory exhausted" in r.stdout, r.stdout
