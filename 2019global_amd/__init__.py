@@ -46,6 +46,7 @@ MODE_R, MODE_X = 0, 1
 FLAG_STATS = 1
 FLAG_R_DFS = 2   # Mode R: reverse-DFS over the whole reference octree (A/B against the default)
 FLAG_TIME = 4    # HIP events around the dominant kernel; read with DeviceScene.kernel_ms()
+FLAG_X_NO_SHADOW = 8   # Mode X, tests only: no shadow rays (reduces depth-1 Mode X to the reference's shading)
 STAT_RAYS, STAT_NODES, STAT_PRIMS, STAT_PIXELS, STAT_PBOX = 0, 1, 2, 3, 4
 STAT_X_ITERS, STAT_X_TRAV, STAT_X_HANDLE, STAT_X_HLANES, STAT_X_HCLOSE, STAT_X_HSHADOW = 5, 6, 7, 8, 9, 10
 STAT_X_CYC_TRAV, STAT_X_CYC_HIT, STAT_X_CYC_NEXT, STAT_X_CYC_ALL = 11, 12, 13, 14
@@ -410,7 +411,7 @@ class DeviceScene:
         return o
 
     def render(self, cam: Camera, light, w: int, h: int, mode=MODE_R, spp=1, depth=1, seed=0, band_rows=0,
-               cancel: Optional[ctypes.c_int] = None, callback=None, out=None):
+               cancel: Optional[ctypes.c_int] = None, callback=None, out=None, flags=0):
         """Host-buffer render (gi_render).  Returns (rgb float64 [h,w,3], rgb8 uint8 [h,w,3]).
         out=(rgb, rgb8): caller-owned C-contiguous arrays to fill instead (either may be None:
         that output is not copied back)."""
@@ -422,7 +423,7 @@ class DeviceScene:
             if a is not None and (a.dtype != dt or a.size != w * h * 3 or not a.flags.c_contiguous):
                 raise ValueError("render: out arrays must be C-contiguous [h, w, 3] float64 / uint8")
         cb = TILE_CB(callback) if callback is not None else TILE_CB()
-        o = self.opts(mode, spp, depth, seed, band_rows=band_rows)
+        o = self.opts(mode, spp, depth, seed, band_rows=band_rows, flags=flags)
         _check(lib().gi_render(self._h, ctypes.byref(cam._c), _d3(light), w, h, ctypes.byref(o),
                                rgb.ctypes.data_as(ctypes.POINTER(ctypes.c_double)) if rgb is not None else None,
                                rgb8.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)) if rgb8 is not None else None,

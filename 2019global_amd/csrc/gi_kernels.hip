@@ -729,6 +729,9 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 #ifndef GI_X_PAIR
 #define GI_X_PAIR 1   // LDS-resident scenes: leaf records tested two at a time (interleaved fp64 chains)
 #endif
+#ifndef GI_X_NSTK
+#define GI_X_NSTK 1   // HBM-resident scenes: the node index of every traversal level kept in LDS
+#endif
 #ifndef GI_X_MIN_WAVES
 #define GI_X_MIN_WAVES 3       // minimum waves per SIMD, HBM-resident scenes (<= 168 VGPRs)
 #endif
@@ -774,8 +777,12 @@ struct XWork {
 #define GI_X_MAX_RUN 1
 #endif
 
-template <bool STATS, bool PAIR, bool PSL, typename NodeP, typename HotP, typename PrimP, typename EntP>
+// NST: the wide-node index of every level of the current traversal path lives in LDS (nst[level *
+// 256], one column per lane), so climbing out of exhausted levels is one ds_read instead of a chain
+// of dependent parent-pointer loads from HBM / L2 (one per level climbed).
+template <bool STATS, bool PAIR, bool PSL, bool NST, typename NodeP, typename HotP, typename PrimP, typename EntP>
 __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H, PrimP XP, EntP EN, double* pslot,
+                                            int* nst,
                                             const CamDev& cam, V3 light,
                                             const TileMap& m, int spp, int depth, uint64_t seed, double* rgb,
                                             uint8_t* rgb8, unsigned* blk_list, const XWork& wk, int handle8,
@@ -800,6 +807,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     if (lane == 0) blk_meta[0] = 64u;
     __builtin_amdgcn_wave_barrier();
     const bool inline_shadow = (xflags & 1) != 0;
+    const bool no_shadow = (xflags & 4) != 0;   // GI_FLAG_X_NO_SHADOW (tests): every light visible
     uint32_t nnode = 0, nprim = 0, nrays = 0, nres = 0, npx = 0, nsteps = 0;
     long long idx = -1;
     int x = 0, y = 0;
@@ -920,15 +928,26 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                         node = ch;
                         ++level;
                         lvl_set(mlo, mhi, level, cm);
+                        if (NST) nst[level * 256] = ch;
                     }
                 }
             }
             if (raying) {                 // climb to the nearest level with children left
                 uint32_t rest = lvl_get(mlo, mhi, level);
-                while (rest == 0 && level > 0) {
-                    --level;
-                    node = level == 0 ? 0 : W[node].parent;   // the root is node 0: no load
-                    rest = lvl_get(mlo, mhi, level);
+                if constexpr (NST) {
+                    if (rest == 0 && level > 0) {
+                        do {
+                            --level;
+                            rest = lvl_get(mlo, mhi, level);
+                        } while (rest == 0 && level > 0);
+                        node = level == 0 ? 0 : nst[level * 256];
+                    }
+                } else {
+                    while (rest == 0 && level > 0) {
+                        --level;
+                        node = level == 0 ? 0 : W[node].parent;   // the root is node 0: no load
+                        rest = lvl_get(mlo, mhi, level);
+                    }
                 }
                 if (rest == 0) raying = false;   // ray finished
             }
@@ -1163,6 +1182,11 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     tbest = INFINITY;
                     tbest_f = INFINITY;
                 }
+                if (no_shadow && phase == PH_SHADOW) {   // unoccluded without a query
+                    best = -1;
+                    raying = false;
+                    break;
+                }
                 // start traversing the lane's ray (fp32 reciprocal, 1 ulp: the culling error stays
                 // far inside the 1e-5*extent box padding)
                 of = f3((float)o.x, (float)o.y, (float)o.z);
@@ -1240,11 +1264,13 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
         // (occluded sum, next direction, throughput T, RNG key) live in a per-lane LDS slot after
         // the scene instead of in VGPRs / scratch
         double* pslot = reinterpret_cast<double*>(lds_scene + nw + nh + np + ne) + 10 * threadIdx.x;
-        mode_x_wave<STATS, GI_X_PAIR != 0, W4 && GI_X_PSL>(sc, W, H, XP, EN, pslot, cam, light, m, spp, depth, seed, rgb,
-                                                          rgb8, blk, wk, handle8, xflags, c);
+        mode_x_wave<STATS, GI_X_PAIR != 0, W4 && GI_X_PSL, false>(sc, W, H, XP, EN, pslot, nullptr, cam, light, m, spp,
+                                                                 depth, seed, rgb, rgb8, blk, wk, handle8, xflags, c);
     } else {
-        mode_x_wave<STATS, false, false>(sc, sc.xwnodes, sc.xhot, sc.xprims, sc.ents, nullptr, cam, light, m, spp, depth,
-                                         seed, rgb, rgb8, blk, wk, handle8, xflags, c);
+        extern __shared__ int lds_nst[];   // GI_X_NSTK: 16 levels x 256 lanes of node indices
+        mode_x_wave<STATS, false, false, GI_X_NSTK != 0>(sc, sc.xwnodes, sc.xhot, sc.xprims, sc.ents, nullptr,
+                                                         lds_nst + threadIdx.x, cam, light, m, spp, depth, seed, rgb,
+                                                         rgb8, blk, wk, handle8, xflags, c);
     }
     if (STATS) {
         if ((threadIdx.x & 63) == 0) {
@@ -1421,7 +1447,8 @@ const XEnv& x_env() {
 
 hipError_t x_launch_config(const DevScene& sc, int device, XLaunchCfg& cfg) {
     const bool lds = x_env().lds != 0 && sc.x_lds_bytes > 0;
-    cfg.lds_bytes = lds ? (size_t)sc.x_lds_bytes + ((sc.x_waves4 && GI_X_PSL) ? 256 * 10 * sizeof(double) : 0) : 0;
+    cfg.lds_bytes = lds ? (size_t)sc.x_lds_bytes + ((sc.x_waves4 && GI_X_PSL) ? 256 * 10 * sizeof(double) : 0)
+                        : (GI_X_NSTK ? 16 * 256 * sizeof(int) : 0);
     cfg.kv = 2 * (int)lds + ((lds && sc.x_waves4) ? 1 : 0);
     int cus = 0, per_cu = 0;
     hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
@@ -1487,8 +1514,10 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
         // shading-handler threshold (eighths of the live lanes that must wait): the builder's
         // estimate for the scene (DevScene::x_handle8) unless GI_X_HANDLE8 overrides it
         const int h8 = env.h8 > 0 ? env.h8 : sc.x_handle8;
-        // schedule flags (bit 0: inline shadow) and the maximum run length (log2, bits 8-10)
-        const int xf = (env.xf >= 0 ? env.xf : sc.x_flags) | (env.run_log2 << 8);
+        // schedule flags (bit 0: inline shadow, bit 2: no shadow rays) and the maximum run length
+        // (log2, bits 8-10)
+        const int xf = (env.xf >= 0 ? env.xf : sc.x_flags) | (env.run_log2 << 8) |
+                       ((o.flags & GI_FLAG_X_NO_SHADOW) ? 4 : 0);
 #define GI_LAUNCH_X(S, L, W) hipLaunchKernelGGL((k_mode_x<S, L, W>), pgrid, block, lds_bytes, stream, sc, cam, light, m, o.spp, \
                                            o.depth, o.seed, rgb, rgb8, st, wk, h8, xf)
         mark(ev_begin);

@@ -103,6 +103,10 @@ typedef enum gi_mode {
                               reconstructing the candidate list (same result; A/B and tests) */
 #define GI_FLAG_TIME 4u    /* record HIP events around the frame's dominant kernel (k_mode_r / k_mode_x)
                               on the render's stream; averaged by gi_scene_kernel_ms */
+#define GI_FLAG_X_NO_SHADOW 8u   /* Mode X, test only: no shadow rays (every light is visible).  With
+                                    depth 1 and spp 1 this reduces Mode X to the reference's own
+                                    shading (raytracer.h:41-84, material.h:48-62), so its stages can
+                                    be checked against the reference's frames (tests) */
 
 typedef struct gi_opts {
     int32_t mode;          /* gi_mode */

@@ -935,6 +935,7 @@ struct OAccel {
     bool brute = true;
 };
 
+int g_no_shadow = 0;     // gio_set_no_shadow (tests): Mode X without shadow rays (GI_FLAG_X_NO_SHADOW)
 int g_accel_mode = -1;   // -1: BVH above 256 primitives; 0: always brute force; 1: always BVH
 
 void prim_bounds(const Prim& p, double lo[3], double hi[3]) {
@@ -1174,7 +1175,7 @@ void sample_mode_x(const Scene& s, const std::vector<Prim>& prims, const OAccel&
         const V3 lv = s.light - P;
         const double ldist = std::sqrt(dot(lv, lv));
         const V3 Ld = normalize(lv);
-        const bool vis = !mx_occluded(prims, A, P, Ld, ldist);
+        const bool vis = g_no_shadow || !mx_occluded(prims, A, P, Ld, ldist);
         ++rays;
         const V3 la = tc * e.mat.shader.x;
         V3 loc = la;
@@ -1236,6 +1237,8 @@ extern "C" {
 const char* gio_last_error(void) { return g_err.c_str(); }
 
 void gio_set_accel(int mode) { g_accel_mode = mode < 0 ? -1 : (mode ? 1 : 0); }
+
+void gio_set_no_shadow(int on) { g_no_shadow = on ? 1 : 0; }
 
 int gio_render(const char* scn, int w, int h, int mode, int spp, int depth, uint64_t seed, int x0, int y0,
                int x1, int y1, int threads, double* rgb, int32_t* hit, int32_t* uv, int32_t* ncand,

@@ -43,6 +43,7 @@ int gio_boxes(int n, const double* recs, int32_t* out);
 // Mode X closest-hit / shadow queries: -1 (default) = this oracle's BVH above 256 primitives,
 // brute force below; 0 = brute force always; 1 = BVH always.  Same results either way (tested).
 void gio_set_accel(int mode);
+void gio_set_no_shadow(int on);   /* Mode X without shadow rays (GI_FLAG_X_NO_SHADOW; tests) */
 
 const char* gio_last_error(void);
 

@@ -50,6 +50,7 @@ def oracle():
         lib.gio_boxes.argtypes = [ctypes.c_int, f64p, i32p]
         lib.gio_last_error.restype = ctypes.c_char_p
         lib.gio_set_accel.argtypes = [ctypes.c_int]
+        lib.gio_set_no_shadow.argtypes = [ctypes.c_int]
         _oracle = lib
     return _oracle
 
@@ -72,6 +73,11 @@ def oracle_render(scn: str, w: int, h: int, mode: int = 0, spp: int = 1, depth: 
     if rc != 0:
         raise RuntimeError(f"gio_render failed ({rc}): {lib.gio_last_error().decode()}")
     return out
+
+
+def oracle_no_shadow(on: bool) -> None:
+    """Mode X without shadow rays (the oracle side of GI_FLAG_X_NO_SHADOW)."""
+    oracle().gio_set_no_shadow(1 if on else 0)
 
 
 def oracle_accel(mode: int) -> None:
@@ -180,3 +186,50 @@ def ref_boxes(recs: np.ndarray) -> np.ndarray:
 def bits_equal(a: np.ndarray, b: np.ndarray) -> np.ndarray:
     """Elementwise bit equality of float64 arrays (NaN == NaN when the payload matches)."""
     return np.ascontiguousarray(a, np.float64).view(np.int64) == np.ascontiguousarray(b, np.float64).view(np.int64)
+
+
+# ---- reduced Mode X against the reference (VERDICT r01 next-7) --------------------------------
+# Mode X at depth 1, 1 spp, without shadow rays (GI_FLAG_X_NO_SHADOW) is the reference's own
+# per-pixel shading (raytracer.h:41-84, material.h:48-62) with three semantic differences, each of
+# which is a class of excluded pixels, counted exactly per fixture:
+#   ent  - a different entity: the reference keeps the LAST hitting candidate of Octree::intersect's
+#          list (SURVEY A.1) and loses entities the octree drops (A.6); Mode X takes the closest hit
+#          over all entities;
+#   tex  - same entity, different texel (u, v): the reference's hit point differs in rounding (fp32
+#          sphere root, A.2; glm's inverse for triangles, A.3) and its acos is libm's, so the x86 int()
+#          truncation of the texture coordinate (A.9) can land on the other side of a texel edge;
+#   far  - same entity and texel, but beyond 1e-5 relative in some channel: only scenes with
+#          ImpSpheres (the reference's fp32 root moves the hit point by ~1e-7 relative, A.2) or an
+#          ExpCone (float height and radius in its constructor, entities.h:823); always within ANCHOR_ABS.
+# Every other pixel must be within 1e-5 relative per channel of the reference's radiance (the
+# north_star tolerance); `exact` counts the bit-identical ones.  ExpBox frames (and the zoo, which
+# has one) are left out: ExpBox::intersect keeps the LAST face hit, not the nearest
+# (entities.h:421-437, min_dist_square reset per face), so its point and normal differ by design.
+# The fixtures' pixel sets are the goldens' own (tests/golden/*.npz).
+ANCHOR_ABS = 3e-5
+ANCHOR = {   # fixture: (ent, tex, far, exact) -- pinned from the oracle (the device is bit-identical)
+    "sphere_256x256": (0, 2, 2308, 36706),
+    "cornell_128x128": (7673, 4, 0, 4583),
+    "cornell_512x512_s61": (2398, 0, 0, 497),
+    "cornell_1920x1080_s509": (179, 0, 0, 3745),
+    "main_200x200": (297, 1813, 122, 25122),
+    "soup1000_160x160": (658, 1, 0, 24087),
+    "soup100000_1920x1080_win700-600-1220-1080_s29": (4191, 1, 0, 3517),
+    "only_exprectangle_96x96": (79, 0, 0, 4625),
+    "only_expcone_96x96": (96, 2, 8, 2315),
+    "only_expcube_96x96": (96, 231, 0, 0),
+}
+
+
+def anchor_counts(rgb, hit, uv, z):
+    """(ent, tex, far, exact, max |error| over `far`) of a reduced Mode X frame at the fixture's
+    pixels: `hit`/`uv` are Mode X's primary hit entity and texel (the oracle's), `z` the fixture."""
+    rgb = np.asarray(rgb, np.float64)
+    same_ent = hit == z["hit"]
+    same = same_ent & (uv == z["uv"]).all(1)
+    err = np.abs(rgb - z["rgb"])
+    within = (err <= 1e-5 * np.maximum(np.abs(z["rgb"]), 1e-300)).all(1)
+    far = same & ~within
+    exact = same & bits_equal(rgb, z["rgb"]).all(1)
+    return (int((~same_ent).sum()), int((same_ent & ~same).sum()), int(far.sum()), int(exact.sum()),
+            float(err[far].max()) if far.any() else 0.0)

@@ -818,3 +818,32 @@ def test_python_raytracer_sees_push_back_after_first_run(torch_cuda):
     s2.imp_sphere((2.0, 0.3, 0.3), 0.3, (0, 0, 1))
     o = U.oracle_render(s2.to_scn(), 64, 64)
     assert (b.reshape(-1, 3) == o["q"]).all()
+
+
+@pytest.mark.parametrize("name", sorted(U.ANCHOR))
+def test_reduced_mode_x_anchored_to_reference_on_device(torch_cuda, name):
+    """the DEVICE's Mode X stages tied to the compiled reference's frames where
+    the semantics coincide -- depth 1, 1 spp, no shadow rays (GI_FLAG_X_NO_SHADOW).  The device frame
+    equals the oracle's reduced frame bit for bit, and against the reference fixture the excluded
+    pixels are exactly the counted classes of oracle_util.ANCHOR (A.1/A.6 entity choice, texel
+    edges, fp32 sphere roots); every other pixel is within 1e-5 relative per channel."""
+    z = np.load(os.path.join(GOLD, name + ".npz"))
+    meta = json.loads(str(z["meta"]))
+    sc = _scene(meta["scene"])
+    w, h = meta["w"], meta["h"]
+    rgb, _ = dev_scene(meta["scene"]).render(cam_of(sc), sc.light, w, h, mode=gi.MODE_X, spp=1, depth=1,
+                                             flags=gi.FLAG_X_NO_SHADOW)
+    g = rgb[z["y"], z["x"]]
+    xs, ys = z["x"], z["y"]
+    x0, x1, y0, y1 = int(xs.min()), int(xs.max()) + 1, int(ys.min()), int(ys.max()) + 1
+    U.oracle_no_shadow(True)
+    try:
+        o = U.oracle_render(sc.to_scn(), w, h, mode=1, spp=1, depth=1, window=(x0, y0, x1, y1))
+    finally:
+        U.oracle_no_shadow(False)
+    i = (ys - y0) * (x1 - x0) + (xs - x0)
+    assert U.bits_equal(g, o["rgb"][i]).all(), "device reduced Mode X differs from the oracle's"
+    ent, tex, far, exact, far_max = U.anchor_counts(g, o["hit"][i], o["uv"][i], z)
+    assert (ent, tex, far, exact) == U.ANCHOR[name]
+    assert far_max <= U.ANCHOR_ABS
+    print(f"{name}: {exact} of {len(xs)} pixels bit-identical to the reference")

@@ -193,3 +193,21 @@ def test_oracle_mode_x_sample_parallel_window_equals_pixel_loop():
     assert U.bits_equal(aa, b["rgb"]).all()
     assert (a["ncand"].reshape(8, 8)[2:5, 2:5].reshape(-1) == b["ncand"]).all()
     assert (a["hit"].reshape(8, 8)[2:5, 2:5].reshape(-1) == b["hit"]).all()
+
+
+@pytest.mark.parametrize("name", sorted(U.ANCHOR))
+def test_reduced_mode_x_anchored_to_reference(name):
+    """Mode X's shared stages (raygen, fp64 hit points, polynomial acos texture mapping, square-and-
+    multiply Blinn-Phong) tied to the COMPILED REFERENCE's frames where the semantics coincide:
+    depth 1, 1 spp, no shadow rays.  Excluded pixels are counted exactly by class (oracle_util.ANCHOR:
+    A.1/A.6 entity choice, texel edges, fp32 sphere roots); all others within 1e-5 relative."""
+    z, meta = load_frame(name)
+    sc = _scene(meta["scene"])
+    U.oracle_no_shadow(True)
+    try:
+        o = render_pixels(sc.to_scn(), meta["w"], meta["h"], z["x"], z["y"], mode=1, spp=1, depth=1)
+    finally:
+        U.oracle_no_shadow(False)
+    ent, tex, far, exact, far_max = U.anchor_counts(o["rgb"], o["hit"], o["uv"], z)
+    assert (ent, tex, far, exact) == U.ANCHOR[name]
+    assert far_max <= U.ANCHOR_ABS
