@@ -715,7 +715,7 @@ __device__ __forceinline__ void x_texcoord(const DevScene& sc, const REnt& e, V3
 // live lanes have a finished ray, or when none is still traversing, so it executes with a
 // well-filled EXEC mask.  The per-path operation sequence is exactly the oracle's (pixel_mode_x in
 // oracle/gi_oracle.cpp), so results are bit-identical whatever the schedule.
-enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD = 4, PH_DONEPX = 5 };
+enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD = 4, PH_DONEPX = 5, PH_HELP = 6 };
 
 #ifndef GI_X_START_BURST
 #define GI_X_START_BURST 16   // primary rays a lane may resolve by the root test per handler run
@@ -728,6 +728,9 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 #endif
 #ifndef GI_X_PAIR
 #define GI_X_PAIR 1   // LDS-resident scenes: leaf records tested two at a time (interleaved fp64 chains)
+#endif
+#ifndef GI_X_HELP
+#define GI_X_HELP 1   // HBM-resident scenes: shadow rays handed to idle lanes of the wave (XHelp)
 #endif
 #ifndef GI_X_NSTK
 #define GI_X_NSTK 1   // HBM-resident scenes: the node index of every traversal level kept in LDS
@@ -777,12 +780,32 @@ struct XWork {
 #define GI_X_MAX_RUN 1
 #endif
 
+// Shadow-ray handoff (HELP, xflags bit 3).  Once a wave has lanes with no work left (PH_DEAD: the
+// end of the frame, or of a small shard), a lane that has shaded a hit whose path continues gives
+// that hit's shadow ray to an idle lane and starts its next bounce ray at once, instead of tracing
+// the two one after the other: the path's critical path becomes max(shadow_b, closest_{b+1}) per
+// bounce instead of their sum.  The owner keeps both candidate sums (Lv lit, Lo dark) as before and
+// picks one when the helper's answer arrives, before it shades the next hit, so the operations --
+// and the frame, bit for bit -- are the oracle's.  Per lane in LDS (column layout, 256 lanes):
+// ray[7][256] (origin, direction, tmax), own[256] (owner lane within the wave, -1: none) and
+// res[256] (the owner's answer: 0 pending, 1 lit, 2 occluded).
+struct XHelp {
+    double* ray;
+    int* own;
+    int* res;
+};
+__device__ __forceinline__ int nth_set_bit(unsigned long long m, unsigned n) {
+    for (unsigned i = 0; i < n; ++i) m &= m - 1;
+    return __ffsll((long long)m) - 1;
+}
+
 // NST: the wide-node index of every level of the current traversal path lives in LDS (nst[level *
 // 256], one column per lane), so climbing out of exhausted levels is one ds_read instead of a chain
 // of dependent parent-pointer loads from HBM / L2 (one per level climbed).
-template <bool STATS, bool PAIR, bool PSL, bool NST, typename NodeP, typename HotP, typename PrimP, typename EntP>
+template <bool STATS, bool PAIR, bool PSL, bool NST, bool HELP, typename NodeP, typename HotP, typename PrimP,
+          typename EntP>
 __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H, PrimP XP, EntP EN, double* pslot,
-                                            int* nst,
+                                            int* nst, XHelp hp_,
                                             const CamDev& cam, V3 light,
                                             const TileMap& m, int spp, int depth, uint64_t seed, double* rgb,
                                             uint8_t* rgb8, unsigned* blk_list, const XWork& wk, int handle8,
@@ -808,6 +831,15 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     __builtin_amdgcn_wave_barrier();
     const bool inline_shadow = (xflags & 1) != 0;
     const bool no_shadow = (xflags & 4) != 0;   // GI_FLAG_X_NO_SHADOW (tests): every light visible
+    const bool handoff = HELP && (xflags & 8) != 0 && !no_shadow;
+    const int tid = threadIdx.x, wbase = tid & ~63;
+    if (HELP) {
+        hp_.own[tid] = -1;
+        hp_.res[tid] = 0;
+    }
+    bool pend = false;       // this lane's last shadow ray is being traced by a helper
+    bool any_gave = false;   // some lane of the wave handed a shadow ray over in the last iteration
+    int howner = 0;          // PH_HELP: the owner lane
     uint32_t nnode = 0, nprim = 0, nrays = 0, nres = 0, npx = 0, nsteps = 0;
     long long idx = -1;
     int x = 0, y = 0;
@@ -832,8 +864,34 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
 
     const uint64_t t_begin = STATS ? clock64() : 0;
     for (;;) {
+        if (HELP && any_gave && phase == PH_DEAD) {   // an idle lane given a shadow ray starts it
+            const int ow = hp_.own[tid];
+            if (ow >= 0) {
+                hp_.own[tid] = -1;
+                howner = ow;
+                const double* r = hp_.ray + tid;
+                o = v3(r[0], r[256], r[512]);
+                d = v3(r[768], r[1024], r[1280]);
+                tmax = r[1536];
+                tbest = tmax;
+                tbest_f = up32(tmax);
+                phase = PH_HELP;
+                best = -1;
+                of = f3((float)o.x, (float)o.y, (float)o.z);
+                ivf = inv_dir(d);
+                dmask = (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
+                const uint32_t rm = children_mask<PAIR>(W, of, ivf, tbest_f, dmask);
+                node = 0;
+                level = 0;
+                mlo = mhi = 0;
+                lvl_set(mlo, mhi, 0, rm);
+                raying = rm != 0;
+            }
+        }
         const unsigned long long m_live = __ballot(phase != PH_DEAD);
         if (m_live == 0) break;
+        const unsigned long long m_idle = HELP ? ~m_live : 0ull;   // lanes free to take a shadow ray
+        bool gave = false;
         const bool trav = raying;
         const unsigned long long m_trav = __ballot(trav);
         const int n_wait = __popcll(m_live & ~m_trav);
@@ -886,7 +944,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                             ++nprim;
                             const double t = x_prim_t(rec.h, o, d, MX_TMIN);
                             const int pi = rec.h.prim;
-                            if (phase == PH_SHADOW) {
+                            if (phase != PH_CLOSEST) {   // shadow ray (own or a helper's)
                                 if (t < tmax) { best = pi; raying = false; break; }   // any hit occludes
                             } else if (t < tbest || (t == tbest && pi < best)) {
                                 tbest = t;
@@ -902,7 +960,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                         const double ta = x_prim_t(r0.h, o, d, MX_TMIN);
                         const double tb = two ? x_prim_t(r1.h, o, d, MX_TMIN) : INFINITY;
                         nprim += two ? 2 : 1;
-                        if (phase == PH_SHADOW) {
+                        if (phase != PH_CLOSEST) {
                             if (ta < tmax || tb < tmax) {   // any hit occludes
                                 best = ta < tmax ? r0.h.prim : r1.h.prim;
                                 raying = false;
@@ -979,7 +1037,26 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
         }
         const uint64_t t1 = STATS ? clock64() : 0;
         uint64_t t2 = t1;
-        if (handle) {
+        if (HELP && handle && phase == PH_HELP) {   // a helper's answer to its owner; idle again
+            ++nrays;
+            hp_.res[wbase + howner] = best >= 0 ? 2 : 1;
+            phase = PH_DEAD;
+        }
+        bool hold = false;   // an owner whose helper has not answered yet: no handling this time
+        if (HELP) {
+            __builtin_amdgcn_wave_barrier();
+            if (handle && pend) {
+                const int r = hp_.res[tid];
+                if (r == 0) {
+                    hold = true;
+                } else {
+                    if (r == 2) Lv = PSL ? v3(pslot[0], pslot[1], pslot[2]) : Lo;   // occluded: ambient only
+                    hp_.res[tid] = 0;
+                    pend = false;
+                }
+            }
+        }
+        if (handle && !hold && phase != PH_DEAD) {
             // ---- the lane's ray is finished: consume it, spawn the next one --------------------
             bool end_path = false;
             if (phase == PH_CLOSEST) {
@@ -1036,13 +1113,42 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                             has_next = true;
                         }
                     }
-                    // shadow ray toward the point light
-                    phase = PH_SHADOW;
-                    o = P;
-                    d = Ld;
-                    tmax = ldist;
-                    tbest = ldist;
-                    tbest_f = up32(ldist);
+                    // shadow ray toward the point light: handed to an idle lane of the wave when the
+                    // path continues and one is free (the k-th giver takes the k-th idle lane), the
+                    // lane then starts its next bounce at once; else traced here first
+                    bool give = handoff && has_next;
+                    if (HELP) {
+                        const unsigned long long m_give = __ballot(give);
+                        if (give) {
+                            const unsigned r = (unsigned)__popcll(m_give & ((1ull << lane) - 1));
+                            give = r < (unsigned)__popcll(m_idle);
+                            if (give) {
+                                const int ht = wbase + nth_set_bit(m_idle, r);
+                                double* hr = hp_.ray + ht;
+                                hr[0] = P.x; hr[256] = P.y; hr[512] = P.z;
+                                hr[768] = Ld.x; hr[1024] = Ld.y; hr[1280] = Ld.z;
+                                hr[1536] = ldist;
+                                hp_.own[ht] = lane;
+                                pend = true;
+                                gave = true;
+                                o = P;
+                                d = PSL ? v3(pslot[3], pslot[4], pslot[5]) : nextd;
+                                ++b;
+                                phase = PH_CLOSEST;
+                                tmax = INFINITY;
+                                tbest = INFINITY;
+                                tbest_f = INFINITY;
+                            }
+                        }
+                    }
+                    if (!give) {
+                        phase = PH_SHADOW;
+                        o = P;
+                        d = Ld;
+                        tmax = ldist;
+                        tbest = ldist;
+                        tbest_f = up32(ldist);
+                    }
                 }
             } else if (phase == PH_SHADOW) {
                 ++nrays;
@@ -1203,6 +1309,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 break;
             }
         }
+        if (HELP) any_gave = __ballot(gave) != 0;
         if (STATS) {
             const uint64_t t3 = clock64();
             cnt.cyc_trav += t1 - t0;
@@ -1232,6 +1339,9 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
 // W4: 4 waves per SIMD (<= 128 VGPRs) for LDS-resident scenes whose shading is light (triangles
 // without acos texture mapping: +7% on the Cornell box); scenes with spheres / cones / rectangles
 // keep 3 (their heavier handler spills at 128 VGPRs: -45% on the main.cpp scene at 4).
+// For HBM-resident scenes (!LDS) W4 selects the shadow-ray handoff build (GI_X_HELP, XHelp): chosen
+// per launch for small launches, whose frame time is their longest paths' latency (C4: 3.29 ->
+// 2.69 ms); in long launches (C5) the handoff build's heavier code costs 8%, so they run without.
 template <bool STATS, bool LDS, bool W4>
 __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WAVES) void k_mode_x(DevScene sc, CamDev cam, V3 light, TileMap m, int spp, int depth,
                                                  uint64_t seed, double* rgb, uint8_t* rgb8,
@@ -1264,13 +1374,21 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
         // (occluded sum, next direction, throughput T, RNG key) live in a per-lane LDS slot after
         // the scene instead of in VGPRs / scratch
         double* pslot = reinterpret_cast<double*>(lds_scene + nw + nh + np + ne) + 10 * threadIdx.x;
-        mode_x_wave<STATS, GI_X_PAIR != 0, W4 && GI_X_PSL, false>(sc, W, H, XP, EN, pslot, nullptr, cam, light, m, spp,
-                                                                 depth, seed, rgb, rgb8, blk, wk, handle8, xflags, c);
+        mode_x_wave<STATS, GI_X_PAIR != 0, W4 && GI_X_PSL, false, false>(sc, W, H, XP, EN, pslot, nullptr, XHelp{},
+                                                                        cam, light, m, spp, depth, seed, rgb, rgb8, blk,
+                                                                        wk, handle8, xflags, c);
     } else {
-        extern __shared__ int lds_nst[];   // GI_X_NSTK: 16 levels x 256 lanes of node indices
-        mode_x_wave<STATS, false, false, GI_X_NSTK != 0>(sc, sc.xwnodes, sc.xhot, sc.xprims, sc.ents, nullptr,
-                                                         lds_nst + threadIdx.x, cam, light, m, spp, depth, seed, rgb,
-                                                         rgb8, blk, wk, handle8, xflags, c);
+        // dynamic LDS: GI_X_NSTK's 16 levels x 256 lanes of node indices, then GI_X_HELP's handoff
+        // slots (7 x 256 doubles, 2 x 256 ints)
+        extern __shared__ int lds_nst[];
+        XHelp hp;
+        hp.ray = reinterpret_cast<double*>(lds_nst + (GI_X_NSTK ? 16 * 256 : 0));
+        hp.own = reinterpret_cast<int*>(hp.ray + 7 * 256);
+        hp.res = hp.own + 256;
+        mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0>(sc, sc.xwnodes, sc.xhot, sc.xprims, sc.ents,
+                                                                        nullptr, lds_nst + threadIdx.x, hp, cam, light,
+                                                                        m, spp, depth, seed, rgb, rgb8, blk, wk, handle8,
+                                                                        xflags, c);
     }
     if (STATS) {
         if ((threadIdx.x & 63) == 0) {
@@ -1427,7 +1545,7 @@ long long shard_tiles(int w, int h, int shard_count) { return make_map(w, h, sha
 // overrides the shading-handler threshold, GI_X_FLAGS the schedule flags, GI_X_MAX_RUN the largest
 // work-unit run length (scenes of cheap background samples such as the main.cpp scene prefer 8).
 struct XEnv {
-    int lds = 1, h8 = 0, xf = -1, run_log2 = 0;
+    int lds = 1, h8 = 0, xf = -1, run_log2 = 0, help = 1;
 };
 const XEnv& x_env() {
     static XEnv env;
@@ -1436,6 +1554,7 @@ const XEnv& x_env() {
         if (const char* v = std::getenv("GI_X_LDS")) env.lds = std::atoi(v);
         if (const char* v = std::getenv("GI_X_HANDLE8")) env.h8 = std::max(1, std::min(8, std::atoi(v)));
         if (const char* v = std::getenv("GI_X_FLAGS")) env.xf = std::atoi(v);
+        if (const char* v = std::getenv("GI_X_HELP")) env.help = std::atoi(v) != 0;
         const char* v = std::getenv("GI_X_MAX_RUN");
         const int r = v ? std::max(1, std::min(128, std::atoi(v))) : GI_X_MAX_RUN;
         int lg = 0;
@@ -1448,8 +1567,9 @@ const XEnv& x_env() {
 hipError_t x_launch_config(const DevScene& sc, int device, XLaunchCfg& cfg) {
     const bool lds = x_env().lds != 0 && sc.x_lds_bytes > 0;
     cfg.lds_bytes = lds ? (size_t)sc.x_lds_bytes + ((sc.x_waves4 && GI_X_PSL) ? 256 * 10 * sizeof(double) : 0)
-                        : (GI_X_NSTK ? 16 * 256 * sizeof(int) : 0);
-    cfg.kv = 2 * (int)lds + ((lds && sc.x_waves4) ? 1 : 0);
+                        : (GI_X_NSTK ? 16 * 256 * sizeof(int) : 0) +
+                              (GI_X_HELP ? 256 * (7 * sizeof(double) + 2 * sizeof(int)) : 0);
+    cfg.kv = 2 * (int)lds + ((lds && sc.x_waves4) ? 1 : 0);   // 0 / 1 (per launch, HELP): HBM-resident
     int cus = 0, per_cu = 0;
     hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
     if (e != hipSuccess) return e;
@@ -1493,9 +1613,13 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
         // persistent grid: as many 4-wave blocks as can be resident (xc, per scene), each wave pulls
         // blocks of work units
         const XEnv& env = x_env();
-        const int kv = xc.kv;
-        const size_t lds_bytes = xc.lds_bytes;
         const long long n_slots = m.n_local * (kTile * kTile);
+        // HBM-resident scenes: the shadow-ray handoff build for launches of at most 256 samples per
+        // resident lane (their time is the longest paths' latency, and lanes run out of work early)
+        const bool help = GI_X_HELP && xc.kv == 0 && env.help &&
+                          n_slots * (long long)o.spp <= 256ll * 256ll * (long long)xc.resident;
+        const int kv = xc.kv + (help ? 1 : 0);
+        const size_t lds_bytes = xc.lds_bytes;
         // up to one lane per (pixel slot, sample): single-sample units can occupy that many lanes
         const long long want = (n_slots * (long long)o.spp / 64 + kWavesPerBlock - 1) / kWavesPerBlock;
         const dim3 pgrid((unsigned)std::max<long long>(1, std::min<long long>(want, xc.resident)));
@@ -1517,14 +1641,16 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
         // schedule flags (bit 0: inline shadow, bit 2: no shadow rays) and the maximum run length
         // (log2, bits 8-10)
         const int xf = (env.xf >= 0 ? env.xf : sc.x_flags) | (env.run_log2 << 8) |
-                       ((o.flags & GI_FLAG_X_NO_SHADOW) ? 4 : 0);
+                       ((o.flags & GI_FLAG_X_NO_SHADOW) ? 4 : 0) | (env.help ? 8 : 0);
 #define GI_LAUNCH_X(S, L, W) hipLaunchKernelGGL((k_mode_x<S, L, W>), pgrid, block, lds_bytes, stream, sc, cam, light, m, o.spp, \
                                            o.depth, o.seed, rgb, rgb8, st, wk, h8, xf)
         mark(ev_begin);
         if (stats) {
-            if (kv == 3) GI_LAUNCH_X(true, true, true); else if (kv == 2) GI_LAUNCH_X(true, true, false); else GI_LAUNCH_X(true, false, false);
+            if (kv == 3) GI_LAUNCH_X(true, true, true); else if (kv == 2) GI_LAUNCH_X(true, true, false);
+            else if (kv == 1) GI_LAUNCH_X(true, false, true); else GI_LAUNCH_X(true, false, false);
         } else {
-            if (kv == 3) GI_LAUNCH_X(false, true, true); else if (kv == 2) GI_LAUNCH_X(false, true, false); else GI_LAUNCH_X(false, false, false);
+            if (kv == 3) GI_LAUNCH_X(false, true, true); else if (kv == 2) GI_LAUNCH_X(false, true, false);
+            else if (kv == 1) GI_LAUNCH_X(false, false, true); else GI_LAUNCH_X(false, false, false);
         }
         mark(ev_end);
 #undef GI_LAUNCH_X

@@ -847,3 +847,27 @@ def test_reduced_mode_x_anchored_to_reference_on_device(torch_cuda, name):
     assert (ent, tex, far, exact) == U.ANCHOR[name]
     assert far_max <= U.ANCHOR_ABS
     print(f"{name}: {exact} of {len(xs)} pixels bit-identical to the reference")
+
+
+def test_mode_x_shadow_handoff_frame_identical(torch_cuda, tmp_path):
+    """Shadow rays handed to idle lanes (GI_X_HELP, chosen for small launches of HBM-resident scenes
+    such as the whole C4 frame) change the schedule only: the frame equals the one rendered without
+    the handoff (GI_X_HELP=0, read once per process: a child process renders) bit for bit, for the
+    C4 workload and for the 1k soup at 4 spp."""
+    import subprocess
+    import sys
+    cases = (("soup100000", 1920, 1080, 1, 8), ("soup1000", 320, 240, 4, 6))
+    out = tmp_path / "nohelp.npz"
+    code = ("import sys, numpy as np; sys.path.insert(0, %r); sys.path.insert(0, %r); import oracle_util as U; "
+            "gi = U.pkg(); S = U.scenes(); res = {}\n"
+            "for name, w, h, spp, depth in %r:\n"
+            "    sc = S.named_scene(name); d = gi.DeviceScene.from_scene(sc)\n"
+            "    res[name] = d.render(gi.Camera(sc.cam_pos, sc.cam_look, sc.focal), sc.light, w, h, mode=gi.MODE_X, "
+            "spp=spp, depth=depth, seed=2019)[0]\n"
+            "np.savez(%r, **res)") % (U.ROOT, os.path.join(U.ROOT, "tests"), cases, str(out))
+    subprocess.run([sys.executable, "-c", code], check=True, timeout=300, env=dict(os.environ, GI_X_HELP="0"))
+    ref = np.load(out)
+    for name, w, h, spp, depth in cases:
+        sc = _scene(name)
+        rgb, _ = dev_scene(name).render(cam_of(sc), sc.light, w, h, mode=gi.MODE_X, spp=spp, depth=depth, seed=2019)
+        assert U.bits_equal(rgb, ref[name]).all(), name
