@@ -47,7 +47,7 @@ FLAG_STATS = 1
 FLAG_R_DFS = 2   # Mode R: reverse-DFS over the whole reference octree (A/B against the default)
 FLAG_TIME = 4    # HIP events around the dominant kernel; read with DeviceScene.kernel_ms()
 FLAG_X_NO_SHADOW = 8   # Mode X, tests only: no shadow rays (reduces depth-1 Mode X to the reference's shading)
-STAT_RAYS, STAT_NODES, STAT_PRIMS, STAT_PIXELS, STAT_PBOX = 0, 1, 2, 3, 4
+STAT_RAYS, STAT_NODES, STAT_PRIMS, STAT_PIXELS, STAT_X_PATH_MAX = 0, 1, 2, 3, 4
 STAT_X_ITERS, STAT_X_TRAV, STAT_X_HANDLE, STAT_X_HLANES, STAT_X_HCLOSE, STAT_X_HSHADOW = 5, 6, 7, 8, 9, 10
 STAT_X_CYC_TRAV, STAT_X_CYC_HIT, STAT_X_CYC_NEXT, STAT_X_CYC_ALL = 11, 12, 13, 14
 STAT_X_RESOLVED = 15

@@ -746,6 +746,10 @@ struct XCounters {
     uint64_t rays = 0, nodes = 0, prims = 0, px = 0, res = 0;   // res: samples resolved without traversal
     uint64_t iters = 0, trav = 0, handle = 0, hlanes = 0, hclose = 0, hshadow = 0;   // wave-level (lane 0)
     uint64_t cyc_trav = 0, cyc_hit = 0, cyc_next = 0, cyc_all = 0;                    // wave clock cycles
+    // the longest sample path (primary ray to its end): (wall_clock64 ticks << 32) | (wave iterations
+    // << 16) | traversal steps of that lane during it (both saturated at 65535), maximised as one word
+    uint64_t path_t0 = 0, path_max = 0;
+    uint32_t path_it = 0, path_st = 0;
 };
 
 // Mode X work list (k_x_classify -> k_mode_x -> k_x_reduce).  A pixel whose every jittered primary
@@ -823,7 +827,15 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
         while (2 * k <= max_run && 2 * k <= spp && samples / (2.0 * k) >= GI_X_UNITS_PER_LANE * lanes) k *= 2;
     }
     const unsigned runs = (unsigned)((spp + k - 1) / k);              // units per pixel
-    const unsigned n_blocks = ((n_list + 63u) >> 6) * runs;
+    const unsigned n_groups = (n_list + 63u) >> 6;
+    const unsigned n_blocks = n_groups * runs;
+    // xflags bit 4 (spread): group g holds list entries g, g + G, g + 2G, ... (G groups) instead of
+    // 64 consecutive ones, so a wave's 64 pixels come from all over the frame: the expensive pixels
+    // of a frame cluster in space (the soup's core), and consecutive entries would give all of them
+    // to a few waves, whose lanes then pace each other (every loop iteration waits for the others'
+    // shading) while the rest of the chip idles.  Spread, each long path shares its wave with
+    // cheap ones that finish early (fast iterations, idle lanes for its shadow rays).
+    const bool spread = (xflags & 16) != 0;
     // the wave's current block lives in its LDS row: blk_list[0..63] = the group's list entries,
     // blk_meta = {units handed out, group, run}; lanes that do not run the handler keep no copy
     unsigned* blk_meta = blk_list + 64;
@@ -912,13 +924,17 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             }
         }
         const uint64_t t0 = STATS ? clock64() : 0;
+        if (STATS) ++cnt.path_it;
         if (trav) {
             // up to GI_X_TRAV_UNROLL steps per loop iteration: the scheduling ballots and the handler
             // decision are paid once per iteration (a lane whose ray ends stops stepping)
 #pragma unroll 1
             for (int u = 0; u < GI_X_TRAV_UNROLL; ++u) {
             if (u > 0 && !raying) break;
-            if (STATS) ++nsteps;
+            if (STATS) {
+                ++nsteps;
+                ++cnt.path_st;
+            }
             // ---- one traversal step (stackless: 8-bit "children left" mask per level).  Invariant:
             // the current level has a child left; the step pops it, then climbs past exhausted
             // levels, so a ray ends in the step that exhausts the root level (no empty iteration).
@@ -1165,6 +1181,10 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 }
             }
             if (end_path) {
+                if (STATS)
+                    cnt.path_max = max(cnt.path_max, (((uint64_t)wall_clock64() - cnt.path_t0) << 32) |
+                                                         ((uint64_t)min(cnt.path_it, 65535u) << 16) |
+                                                         (uint64_t)min(cnt.path_st, 65535u));
                 if (spp == 1) {   // the pixel: min((0 + L) / 1, 1), the reduce pass's operations
                     const double c0 = smin((0.0 + Lv.x) / 1.0, 1.0), c1 = smin((0.0 + Lv.y) / 1.0, 1.0),
                                  c2 = smin((0.0 + Lv.z) / 1.0, 1.0);
@@ -1214,7 +1234,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                             const unsigned na = (unsigned)__popcll(m_act);
                             __builtin_amdgcn_wave_barrier();
                             for (unsigned e = ra; e < 64u; e += na) {
-                                const unsigned li = ng * 64u + e;
+                                const unsigned li = spread ? e * n_groups + ng : ng * 64u + e;
                                 blk_list[e] = li < n_list ? wk.list[li] : 0xFFFFFFFFu;
                             }
                             __builtin_amdgcn_wave_barrier();
@@ -1234,7 +1254,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     if (lane == leader) blk_meta[0] = used_new;
                     __builtin_amdgcn_wave_barrier();
                     if (phase == PH_NEED && have) {
-                        const unsigned i = g * 64u + j;            // list index
+                        const unsigned i = spread ? j * n_groups + g : g * 64u + j;   // list index
                         if (ps != 0xFFFFFFFFu) {                   // else a padding unit: take another
                             slot_pixel(m, (long long)(ps >> 6), (int)(ps & 63), idx, x, y);
                             y += m.y0;
@@ -1277,6 +1297,11 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                             phase = (smp < spp && (smp & (k - 1)) != 0) ? PH_START : PH_DONEPX;
                             continue;
                         }
+                    }
+                    if (STATS) {
+                        cnt.path_t0 = (uint64_t)wall_clock64();
+                        cnt.path_it = 0;
+                        cnt.path_st = 0;
                     }
                     o = cam.pos;
                     d = normalize(d0);
@@ -1340,8 +1365,9 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
 // without acos texture mapping: +7% on the Cornell box); scenes with spheres / cones / rectangles
 // keep 3 (their heavier handler spills at 128 VGPRs: -45% on the main.cpp scene at 4).
 // For HBM-resident scenes (!LDS) W4 selects the shadow-ray handoff build (GI_X_HELP, XHelp): chosen
-// per launch for small launches, whose frame time is their longest paths' latency (C4: 3.29 ->
-// 2.69 ms); in long launches (C5) the handoff build's heavier code costs 8%, so they run without.
+// per launch for small launches, whose frame time is their longest paths' latency (C4: 3.01 ->
+// 2.64 ms, with spread work groups 2.40 ms); in long launches (C5) the handoff build's heavier code
+// costs 8%, so they run without.
 template <bool STATS, bool LDS, bool W4>
 __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WAVES) void k_mode_x(DevScene sc, CamDev cam, V3 light, TileMap m, int spp, int depth,
                                                  uint64_t seed, double* rgb, uint8_t* rgb8,
@@ -1404,9 +1430,15 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
             atomicAdd(stats + GI_STAT_X_CYC_ALL, (unsigned long long)c.cyc_all);
         }
         wave_add_stats(stats, c.rays, c.nodes, c.prims, c.px);
-        uint64_t cr = c.res;
-        for (int off = 32; off > 0; off >>= 1) cr += __shfl_xor(cr, off);
-        if ((threadIdx.x & 63) == 0) atomicAdd(stats + GI_STAT_X_RESOLVED, (unsigned long long)cr);
+        uint64_t cr = c.res, pm = c.path_max;
+        for (int off = 32; off > 0; off >>= 1) {
+            cr += __shfl_xor(cr, off);
+            pm = max(pm, (uint64_t)__shfl_xor(pm, off));
+        }
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(stats + GI_STAT_X_RESOLVED, (unsigned long long)cr);
+            atomicMax(stats + GI_STAT_X_PATH_MAX, (unsigned long long)pm);
+        }
     }
 }
 
@@ -1545,7 +1577,7 @@ long long shard_tiles(int w, int h, int shard_count) { return make_map(w, h, sha
 // overrides the shading-handler threshold, GI_X_FLAGS the schedule flags, GI_X_MAX_RUN the largest
 // work-unit run length (scenes of cheap background samples such as the main.cpp scene prefer 8).
 struct XEnv {
-    int lds = 1, h8 = 0, xf = -1, run_log2 = 0, help = 1;
+    int lds = 1, h8 = 0, xf = -1, run_log2 = 0, help = 1, spread = -1;
 };
 const XEnv& x_env() {
     static XEnv env;
@@ -1555,6 +1587,7 @@ const XEnv& x_env() {
         if (const char* v = std::getenv("GI_X_HANDLE8")) env.h8 = std::max(1, std::min(8, std::atoi(v)));
         if (const char* v = std::getenv("GI_X_FLAGS")) env.xf = std::atoi(v);
         if (const char* v = std::getenv("GI_X_HELP")) env.help = std::atoi(v) != 0;
+        if (const char* v = std::getenv("GI_X_SPREAD")) env.spread = std::atoi(v);
         const char* v = std::getenv("GI_X_MAX_RUN");
         const int r = v ? std::max(1, std::min(128, std::atoi(v))) : GI_X_MAX_RUN;
         int lg = 0;
@@ -1614,10 +1647,12 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
         // blocks of work units
         const XEnv& env = x_env();
         const long long n_slots = m.n_local * (kTile * kTile);
-        // HBM-resident scenes: the shadow-ray handoff build for launches of at most 256 samples per
-        // resident lane (their time is the longest paths' latency, and lanes run out of work early)
+        // HBM-resident scenes: the shadow-ray handoff build (and spread work groups) for launches of
+        // at most 32 samples per resident lane -- their time is the longest paths' latency and lanes
+        // run out of work early (C4: 10 per lane; X-soup1000, 169 per lane, is throughput-bound and
+        // 25% slower spread)
         const bool help = GI_X_HELP && xc.kv == 0 && env.help &&
-                          n_slots * (long long)o.spp <= 256ll * 256ll * (long long)xc.resident;
+                          n_slots * (long long)o.spp <= 32ll * 256ll * (long long)xc.resident;
         const int kv = xc.kv + (help ? 1 : 0);
         const size_t lds_bytes = xc.lds_bytes;
         // up to one lane per (pixel slot, sample): single-sample units can occupy that many lanes
@@ -1638,10 +1673,12 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
         // shading-handler threshold (eighths of the live lanes that must wait): the builder's
         // estimate for the scene (DevScene::x_handle8) unless GI_X_HANDLE8 overrides it
         const int h8 = env.h8 > 0 ? env.h8 : sc.x_handle8;
-        // schedule flags (bit 0: inline shadow, bit 2: no shadow rays) and the maximum run length
-        // (log2, bits 8-10)
+        // schedule flags (bit 0: inline shadow, bit 2: no shadow rays, bit 3: shadow handoff, bit 4:
+        // spread work groups -- GI_X_SPREAD, by default with the handoff build) and the maximum run
+        // length (log2, bits 8-10)
         const int xf = (env.xf >= 0 ? env.xf : sc.x_flags) | (env.run_log2 << 8) |
-                       ((o.flags & GI_FLAG_X_NO_SHADOW) ? 4 : 0) | (env.help ? 8 : 0);
+                       ((o.flags & GI_FLAG_X_NO_SHADOW) ? 4 : 0) | (env.help ? 8 : 0) |
+                       ((env.spread > 0 || (env.spread < 0 && help)) ? 16 : 0);
 #define GI_LAUNCH_X(S, L, W) hipLaunchKernelGGL((k_mode_x<S, L, W>), pgrid, block, lds_bytes, stream, sc, cam, light, m, o.spp, \
                                            o.depth, o.seed, rgb, rgb8, st, wk, h8, xf)
         mark(ev_begin);

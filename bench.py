@@ -414,6 +414,10 @@ def main():
                                "handler_closest_lanes": st[gi.STAT_X_HCLOSE],
                                "handler_shadow_lanes": st[gi.STAT_X_HSHADOW],
                                "iterations_per_ray": round(it * 64.0 / max(1, rays_frame), 3),
+                               # the longest sample path (primary ray to its end), device constant clock
+                               "longest_path": {"ms": round((st[gi.STAT_X_PATH_MAX] >> 32) / 1e5, 4),
+                                                "wave_iterations": (st[gi.STAT_X_PATH_MAX] >> 16) & 0xFFFF,
+                                                "trav_steps": st[gi.STAT_X_PATH_MAX] & 0xFFFF},
                                "cycle_share": {k: round(st[i] / max(1, st[gi.STAT_X_CYC_ALL]), 4) for k, i in
                                                (("traverse", gi.STAT_X_CYC_TRAV), ("consume", gi.STAT_X_CYC_HIT),
                                                 ("next_ray", gi.STAT_X_CYC_NEXT))}}

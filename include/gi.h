@@ -126,7 +126,9 @@ typedef struct gi_opts {
 #define GI_STAT_NODES 1       /* octree node records fetched & tested */
 #define GI_STAT_PRIMS 2       /* primitive records fetched & tested in fp64 */
 #define GI_STAT_PIXELS 3
-#define GI_STAT_PBOX 4        /* unused (was: Mode X primitive prefilter boxes); always 0 */
+#define GI_STAT_X_PATH_MAX 4  /* Mode X: the longest sample path (primary ray to its end), a maximum:
+                                 (ticks of the device's 100 MHz constant clock << 32) | (wave loop
+                                 iterations << 16) | (that lane's traversal steps), both <= 65535 */
 #define GI_STAT_X_ITERS 5     /* Mode X: wave loop iterations (per wave) */
 #define GI_STAT_X_TRAV 6      /* Mode X: lane traversal steps (sum of active lanes over iterations) */
 #define GI_STAT_X_HANDLE 7    /* Mode X: shading-handler executions (per wave) */
