@@ -53,7 +53,7 @@ STAT_X_CYC_TRAV, STAT_X_CYC_HIT, STAT_X_CYC_NEXT, STAT_X_CYC_ALL = 11, 12, 13, 1
 STAT_X_RESOLVED = 15
 STATS_N = 16
 TILE = 8
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 
 class GIError(RuntimeError):
@@ -87,7 +87,8 @@ class Opts(ctypes.Structure):
 class SceneInfo(ctypes.Structure):
     _fields_ = [("n_entities", ctypes.c_int32), ("n_nodes", ctypes.c_int32), ("n_leaves", ctypes.c_int32),
                 ("max_depth", ctypes.c_int32), ("n_reachable", ctypes.c_int32), ("n_dropped", ctypes.c_int32),
-                ("x_nodes", ctypes.c_int32), ("x_prims", ctypes.c_int32), ("device_bytes", ctypes.c_int64)]
+                ("x_nodes", ctypes.c_int32), ("x_prims", ctypes.c_int32), ("device_bytes", ctypes.c_int64),
+                ("x_node_bytes", ctypes.c_int32), ("x_lds_resident", ctypes.c_int32)]
 
 
 class Hit(ctypes.Structure):

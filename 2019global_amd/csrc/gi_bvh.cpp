@@ -456,4 +456,53 @@ void build_rcand(HostScene& hs) {
     for (size_t j = 0; j < tmp.xhot.size(); ++j) hs.rc_ent[j] = atom_ent[tmp.xhot[j].prim];
 }
 
+
+// Quantised nodes (XCNode): per axis, org = the children's union minimum and the smallest scale 2^e
+// with (union max - org) / 2^e <= 255; each child's q are rounded outward and then checked -- and
+// moved outward while needed -- with the device's arithmetic (fmaf), so every decoded box contains
+// the padded fp32 box of XWNode.  Should the largest q need 256, the axis takes the next exponent.
+bool encode_xcnodes(const std::vector<XWNode>& w, std::vector<XCNode>& out) {
+    out.assign(w.size(), XCNode());
+    for (size_t i = 0; i < w.size(); ++i) {
+        const XWNode& n = w[i];
+        XCNode& q = out[i];
+        std::memset(&q, 0, sizeof q);
+        q.exists = (uint8_t)n.exists;
+        q.parent = n.parent;
+        for (int c = 0; c < 8; ++c) {
+            q.child[c] = n.child[c];
+            if (n.cnt[c] > 255) return false;
+            q.cnt[c] = (uint8_t)n.cnt[c];
+        }
+        for (int a = 0; a < 3; ++a) {
+            float ulo = INFINITY, uhi = -INFINITY;
+            for (int c = 0; c < 8; ++c)
+                if ((n.exists >> c) & 1) { ulo = std::min(ulo, n.lo[a][c]); uhi = std::max(uhi, n.hi[a][c]); }
+            if (!(ulo <= uhi)) { ulo = 0.0f; uhi = 0.0f; }   // no child
+            q.org[a] = ulo;
+            const double span = (double)uhi - (double)ulo;
+            int e = -126;
+            while (e < 127 && std::ldexp(255.0, e) < span) ++e;
+            for (;; ++e) {
+                if (e > 127) return false;
+                const float sc = std::ldexp(1.0f, e);
+                bool ok = true;
+                for (int c = 0; c < 8 && ok; ++c) {
+                    if (!((n.exists >> c) & 1)) { q.qlo[a][c] = 0; q.qhi[a][c] = 0; continue; }
+                    double fl = std::floor(((double)n.lo[a][c] - (double)ulo) / std::ldexp(1.0, e));
+                    double fh = std::ceil(((double)n.hi[a][c] - (double)ulo) / std::ldexp(1.0, e));
+                    int lo = (int)std::max(0.0, std::min(255.0, fl)), hi = (int)std::max(0.0, std::min(255.0, fh));
+                    while (lo > 0 && !(std::fmaf((float)lo, sc, ulo) <= n.lo[a][c])) --lo;
+                    while (hi <= 255 && !(std::fmaf((float)hi, sc, ulo) >= n.hi[a][c])) ++hi;
+                    if (!(std::fmaf((float)lo, sc, ulo) <= n.lo[a][c]) || hi > 255) { ok = false; break; }
+                    q.qlo[a][c] = (uint8_t)lo;
+                    q.qhi[a][c] = (uint8_t)hi;
+                }
+                if (ok) { q.ex[a] = (int8_t)e; break; }
+            }
+        }
+    }
+    return true;
+}
+
 }  // namespace gi

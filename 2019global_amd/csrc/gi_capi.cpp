@@ -375,6 +375,15 @@ int scene_create_on(const gi_scene_desc* desc, int device, gi_scene** out) {
             if (r.kind == K_IMP_SPHERE || r.kind == K_EXP_SPHERE || r.kind == K_EXP_CONE || r.kind == K_EXP_RECTANGLE)
                 d.x_waves4 = 0;
     }
+    // HBM-resident scenes whose XWNode tree outgrows an XCD's L2 share (> 2 MB) traverse quantised
+    // nodes (XCNode: one 128-byte line per node instead of two): C5 287 -> 270 ms; the 1k soup, whose
+    // 84 KB tree stays in L2 anyway, pays the decoding (+6%) and keeps XWNode.  GI_X_CNODE=0 / 1
+    // forces either (A/B).
+    const char* cn = std::getenv("GI_X_CNODE");
+    const bool want_cn = cn ? std::atoi(cn) != 0 : h.xwnodes.size() * sizeof(XWNode) > (size_t)2 << 20;
+    if (d.x_lds_bytes == 0 && want_cn && encode_xcnodes(h.xwnodes, s->host.xcnodes) &&
+        (e = upload(sp, h.xcnodes, &d.xcnodes)) != hipSuccess)
+        return hip_fail(e, "scene upload (quantised nodes)");
     for (int k = 0; k < 3; ++k) { d.root_lo[k] = INFINITY; d.root_hi[k] = -INFINITY; }
     if (!h.xwnodes.empty())
         for (int c = 0; c < 8; ++c)
@@ -463,6 +472,8 @@ int gi_scene_get_info(const gi_scene* s, gi_scene_info* info) {
     info->x_nodes = (int32_t)(s->host.xnodes.empty() ? s->host.xwnodes.size() : s->host.xnodes.size());
     info->x_prims = (int32_t)s->host.xprims.size();
     info->device_bytes = s->bytes;
+    info->x_node_bytes = s->dev.xcnodes ? (int32_t)sizeof(XCNode) : (int32_t)sizeof(XWNode);
+    info->x_lds_resident = s->dev.x_lds_bytes > 0 ? 1 : 0;
     return GI_OK;
 }
 

@@ -461,6 +461,63 @@ __device__ __forceinline__ uint32_t children_mask(const XWNode* nd, F3 of, F3 iv
     }
 }
 
+// Quantised nodes (XCNode, HBM-resident scenes): the 64 bytes the slab tests need arrive in four
+// 16-byte loads; each bound is decoded as fma(q, 2^e, org) -- the arithmetic the host checked the
+// encoding with -- and then tested exactly as an XWNode bound.
+__device__ __forceinline__ float xc_scale(int w, int a) {   // 2^e of axis a (e: signed byte a of w)
+    const int e = (int)(int8_t)((w >> (8 * a)) & 0xFF);
+    return __int_as_float((e + 127) << 23);
+}
+__device__ __forceinline__ float xc_q(int lo4, int hi4, int c) {   // byte c of the 8-byte pair
+    return (float)(((c < 4 ? lo4 : hi4) >> (8 * (c & 3))) & 0xFF);
+}
+template <bool AXIS>
+__device__ __forceinline__ uint32_t children_mask(const XCNode* nd, F3 of, F3 ivf, float tmax, int dmask) {
+    const int4* b = reinterpret_cast<const int4*>(nd);
+    const int4 h = b[0], q1 = b[1], q2 = b[2], q3 = b[3];
+    const F3 no = neg_oiv(of, ivf);
+    const float o3[3] = {__int_as_float(h.x), __int_as_float(h.y), __int_as_float(h.z)};
+    const float s3[3] = {xc_scale(h.w, 0), xc_scale(h.w, 1), xc_scale(h.w, 2)};
+    const int lw[3][2] = {{q1.x, q1.y}, {q1.z, q1.w}, {q2.x, q2.y}};   // qlo x, y, z
+    const int hw[3][2] = {{q2.z, q2.w}, {q3.x, q3.y}, {q3.z, q3.w}};   // qhi x, y, z
+    const float iv3[3] = {ivf.x, ivf.y, ivf.z}, no3[3] = {no.x, no.y, no.z};
+    uint32_t m = 0;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        float tn = 0.0f, tf = tmax;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const float lo = __builtin_fmaf(xc_q(lw[a][0], lw[a][1], c), s3[a], o3[a]);
+            const float hi = __builtin_fmaf(xc_q(hw[a][0], hw[a][1], c), s3[a], o3[a]);
+            const float t0 = __builtin_fmaf(lo, iv3[a], no3[a]), t1 = __builtin_fmaf(hi, iv3[a], no3[a]);
+            tn = fmaxf(tn, fminf(t0, t1));
+            tf = fminf(tf, fmaxf(t0, t1));
+        }
+        m |= tn <= tf ? 1u << c : 0u;
+    }
+    return xor_permute8(m & (uint32_t)((h.w >> 24) & 0xFF), dmask);
+}
+__device__ __forceinline__ bool child_hit(const XCNode* nd, int c, F3 of, F3 ivf, float tmax) {
+    const int4* b = reinterpret_cast<const int4*>(nd);
+    const int4 h = b[0], q1 = b[1], q2 = b[2], q3 = b[3];
+    const F3 no = neg_oiv(of, ivf);
+    const float o3[3] = {__int_as_float(h.x), __int_as_float(h.y), __int_as_float(h.z)};
+    const int lw[3][2] = {{q1.x, q1.y}, {q1.z, q1.w}, {q2.x, q2.y}};
+    const int hw[3][2] = {{q2.z, q2.w}, {q3.x, q3.y}, {q3.z, q3.w}};
+    const float iv3[3] = {ivf.x, ivf.y, ivf.z}, no3[3] = {no.x, no.y, no.z};
+    float tn = 0.0f, tf = tmax;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float sa = xc_scale(h.w, a);
+        const float lo = __builtin_fmaf(xc_q(lw[a][0], lw[a][1], c), sa, o3[a]);
+        const float hi = __builtin_fmaf(xc_q(hw[a][0], hw[a][1], c), sa, o3[a]);
+        const float t0 = __builtin_fmaf(lo, iv3[a], no3[a]), t1 = __builtin_fmaf(hi, iv3[a], no3[a]);
+        tn = fmaxf(tn, fminf(t0, t1));
+        tf = fminf(tf, fmaxf(t0, t1));
+    }
+    return tn <= tf;
+}
+
 __device__ __forceinline__ bool root_hit(const DevScene& sc, F3 of, F3 ivf) {
     const float tx0 = (sc.root_lo[0] - of.x) * ivf.x, tx1 = (sc.root_hi[0] - of.x) * ivf.x;
     const float ty0 = (sc.root_lo[1] - of.y) * ivf.y, ty1 = (sc.root_hi[1] - of.y) * ivf.y;
@@ -942,7 +999,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             const int kc = __builtin_ctz(msk);         // next child in front-to-back order
             lvl_set(mlo, mhi, level, msk & (msk - 1));
             const int c = kc ^ dmask;
-            const XWNode* nd = W + node;
+            const auto* nd = W + node;
             const int ch = nd->child[c];
             // a closer hit may have arrived since the mask was computed: re-cull this child
             bool keep = true;
@@ -1368,7 +1425,8 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
 // per launch for small launches, whose frame time is their longest paths' latency (C4: 3.01 ->
 // 2.64 ms, with spread work groups 2.40 ms); in long launches (C5) the handoff build's heavier code
 // costs 8%, so they run without.
-template <bool STATS, bool LDS, bool W4>
+// CN (HBM-resident scenes): traverse the quantised nodes (DevScene::xcnodes) instead of XWNode.
+template <bool STATS, bool LDS, bool W4, bool CN>
 __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WAVES) void k_mode_x(DevScene sc, CamDev cam, V3 light, TileMap m, int spp, int depth,
                                                  uint64_t seed, double* rgb, uint8_t* rgb8,
                                                  unsigned long long* stats, XWork wk, int handle8, int xflags) {
@@ -1411,10 +1469,16 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
         hp.ray = reinterpret_cast<double*>(lds_nst + (GI_X_NSTK ? 16 * 256 : 0));
         hp.own = reinterpret_cast<int*>(hp.ray + 7 * 256);
         hp.res = hp.own + 256;
-        mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0>(sc, sc.xwnodes, sc.xhot, sc.xprims, sc.ents,
-                                                                        nullptr, lds_nst + threadIdx.x, hp, cam, light,
-                                                                        m, spp, depth, seed, rgb, rgb8, blk, wk, handle8,
-                                                                        xflags, c);
+        if constexpr (CN)   // quantised nodes (the default for HBM-resident scenes)
+            mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0>(sc, sc.xcnodes, sc.xhot, sc.xprims,
+                                                                            sc.ents, nullptr, lds_nst + threadIdx.x, hp,
+                                                                            cam, light, m, spp, depth, seed, rgb, rgb8,
+                                                                            blk, wk, handle8, xflags, c);
+        else
+            mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0>(sc, sc.xwnodes, sc.xhot, sc.xprims,
+                                                                            sc.ents, nullptr, lds_nst + threadIdx.x, hp,
+                                                                            cam, light, m, spp, depth, seed, rgb, rgb8,
+                                                                            blk, wk, handle8, xflags, c);
     }
     if (STATS) {
         if ((threadIdx.x & 63) == 0) {
@@ -1607,9 +1671,10 @@ hipError_t x_launch_config(const DevScene& sc, int device, XLaunchCfg& cfg) {
     hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
     if (e != hipSuccess) return e;
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, cfg.kv == 3 ? reinterpret_cast<const void*>(k_mode_x<false, true, true>)
-                 : cfg.kv == 2 ? reinterpret_cast<const void*>(k_mode_x<false, true, false>)
-                               : reinterpret_cast<const void*>(k_mode_x<false, false, false>),
+        &per_cu, cfg.kv == 3 ? reinterpret_cast<const void*>(k_mode_x<false, true, true, false>)
+                 : cfg.kv == 2 ? reinterpret_cast<const void*>(k_mode_x<false, true, false, false>)
+                 : sc.xcnodes  ? reinterpret_cast<const void*>(k_mode_x<false, false, false, true>)
+                               : reinterpret_cast<const void*>(k_mode_x<false, false, false, false>),
         64 * kWavesPerBlock, cfg.lds_bytes);
     if (e != hipSuccess) return e;
     cfg.resident = std::max(1, cus) * std::max(1, per_cu);
@@ -1679,18 +1744,24 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
         const int xf = (env.xf >= 0 ? env.xf : sc.x_flags) | (env.run_log2 << 8) |
                        ((o.flags & GI_FLAG_X_NO_SHADOW) ? 4 : 0) | (env.help ? 8 : 0) |
                        ((env.spread > 0 || (env.spread < 0 && help)) ? 16 : 0);
-#define GI_LAUNCH_X(S, L, W) hipLaunchKernelGGL((k_mode_x<S, L, W>), pgrid, block, lds_bytes, stream, sc, cam, light, m, o.spp, \
+        const bool cn = kv < 2 && sc.xcnodes != nullptr;
+#define GI_LAUNCH_X(S, L, W) hipLaunchKernelGGL((k_mode_x<S, L, W, false>), pgrid, block, lds_bytes, stream, sc, cam, light, m, o.spp, \
                                            o.depth, o.seed, rgb, rgb8, st, wk, h8, xf)
+#define GI_LAUNCH_XC(S, W) hipLaunchKernelGGL((k_mode_x<S, false, W, true>), pgrid, block, lds_bytes, stream, sc, cam, light, m, \
+                                          o.spp, o.depth, o.seed, rgb, rgb8, st, wk, h8, xf)
         mark(ev_begin);
         if (stats) {
             if (kv == 3) GI_LAUNCH_X(true, true, true); else if (kv == 2) GI_LAUNCH_X(true, true, false);
+            else if (cn) { if (kv == 1) GI_LAUNCH_XC(true, true); else GI_LAUNCH_XC(true, false); }
             else if (kv == 1) GI_LAUNCH_X(true, false, true); else GI_LAUNCH_X(true, false, false);
         } else {
             if (kv == 3) GI_LAUNCH_X(false, true, true); else if (kv == 2) GI_LAUNCH_X(false, true, false);
+            else if (cn) { if (kv == 1) GI_LAUNCH_XC(false, true); else GI_LAUNCH_XC(false, false); }
             else if (kv == 1) GI_LAUNCH_X(false, false, true); else GI_LAUNCH_X(false, false, false);
         }
         mark(ev_end);
 #undef GI_LAUNCH_X
+#undef GI_LAUNCH_XC
         if (o.spp > 1) hipLaunchKernelGGL(k_x_reduce, sgrid, dim3(256), 0, stream, m, wk, o.spp, rgb, rgb8);
     }
     if (timed) kt->recorded++;

@@ -75,6 +75,26 @@ struct XWNode {            // 256 bytes, 2 cache lines
     int32_t pad[2];
 };
 static_assert(sizeof(XWNode) == 256, "XWNode layout");
+// The same node quantised into one 128-byte cache line (HBM-resident scenes, k_mode_x): child c's
+// box on axis a is lo = fma(qlo[a][c], 2^ex[a], org[a]), hi = fma(qhi[a][c], 2^ex[a], org[a]) in
+// fp32, with the 8-bit q chosen on the host -- by the device's own fused arithmetic -- so that the
+// decoded box contains XWNode's padded box (culling stays conservative).  Children, counts and
+// parent as in XWNode (counts <= 255; a scene with a larger leaf keeps XWNode).
+struct XCNode {            // 128 bytes
+    float org[3];
+    int8_t ex[3];
+    uint8_t exists;        // bit c set iff child[c] != XEMPTY
+    uint8_t qlo[3][8];
+    uint8_t qhi[3][8];     // bytes 0..63: what the slab tests read (four 16-byte loads)
+    int32_t child[8];
+    uint8_t cnt[8];
+    int32_t parent;
+    int32_t pad[5];
+};
+static_assert(sizeof(XCNode) == 128, "XCNode layout");
+// Encodes w as XCNode (the decode above contains every child's box); false if a count exceeds 255.
+bool encode_xcnodes(const std::vector<XWNode>& w, std::vector<XCNode>& out);
+
 // Leaf primitive records, duplicated per leaf reference and stored contiguously per leaf, so a
 // leaf costs one dependent load level: exactly what Moller-Trumbore / the sphere test read.
 struct XHot {              // 80 bytes
@@ -104,6 +124,7 @@ struct HostScene {
     // Mode X
     std::vector<XNode> xnodes;
     std::vector<XWNode> xwnodes;
+    std::vector<XCNode> xcnodes;     // xwnodes quantised (encode_xcnodes), for HBM-resident scenes
     std::vector<XLeaf> xleaves;
     std::vector<int32_t> xprim_idx;
     std::vector<XHot> xhot;
@@ -147,6 +168,7 @@ struct DevScene {
     const REnt* ents;
     const TriRec* tris;
     const XWNode* xwnodes;
+    const XCNode* xcnodes;   // quantised copy of xwnodes (null: the scene keeps XWNode everywhere)
     const XHot* xhot;
     const XBox* xbox;
     const XPrim* xprims;

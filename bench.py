@@ -19,8 +19,9 @@ HBM.  The ray count per frame is exact: a counting launch (GI_FLAG_STATS) of the
 deterministic frame runs before the timed region.
 
 roofline: the dominant kernel (k_mode_x) against HBM: achieved = algorithmic bytes per launch
-(Mode X: wide-node records x 256 B + primitive records x 80 B + 27 B/pixel output; Mode R: 64 B
-nodes + 144 B triangles) /
+(Mode X: wide-node records x 256 B -- 128 B for the quantised nodes of large HBM-resident scenes --
++ primitive records x 80 B + 27 B/pixel output; Mode R: 64 B nodes + 144 B triangles; DESIGN.md
+§Measurement) /
 average launch time of that kernel alone from HIP events recorded directly around it on the launch
 stream (GI_FLAG_TIME, read with gi_scene_kernel_ms); traffic = HBM bytes per launch from the
 committed rocprofv3 PMC summary when present (profiles/), else null.
@@ -43,7 +44,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-NODE_BYTES = {0: 64, 1: 256}   # RNode / XWNode (8 child boxes) records
+NODE_BYTES = {0: 64, 1: 256}   # RNode / XWNode (8 child boxes) records; Mode X on large HBM-resident
+                               # scenes: the quantised 128-B XCNode (gi_scene_info.x_node_bytes)
 PRIM_BYTES = {0: 144, 1: 80}   # Mode R: TriRec (sphere/quad records are <= 160 B) / Mode X: XHot fp64 record
 
 WORKLOADS = {
@@ -361,7 +363,8 @@ def main():
         ms_frame = elapsed / args.steps * 1e3
         value = rays_frame * args.steps / elapsed / 1e6
         # algorithmic bytes per launch of the dominant kernel (this rank's launch; N=1: the frame)
-        alg = (st[gi.STAT_NODES] * NODE_BYTES[mode] + st[gi.STAT_PRIMS] * PRIM_BYTES[mode] +
+        node_bytes = dev.info()["x_node_bytes"] if mode == 1 else NODE_BYTES[0]
+        alg = (st[gi.STAT_NODES] * node_bytes + st[gi.STAT_PRIMS] * PRIM_BYTES[mode] +
                st[gi.STAT_PIXELS] * 27) / world
         achieved = alg / (kern_ms * 1e-3) / 1e9
         ceil = counter_ceilings(args.workload, kern_ms) if world == 1 else None
@@ -396,6 +399,7 @@ def main():
                          "traffic": traffic, "alg_bytes_per_launch": int(alg),
                          "kernel_ms": round(kern_ms, 4), "render_call_ms": round(render_ms, 4),
                          "node_visits": st[gi.STAT_NODES], "prim_tests": st[gi.STAT_PRIMS],
+                         "node_record_bytes": node_bytes,
                          "alg_bytes_note": "algorithmic record bytes; for LDS-resident scenes (C2/C3) they "
                                            "are served from LDS, see hbm_counter_frac / binding"},
         }

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define GI_ABI_VERSION 5
+#define GI_ABI_VERSION 6
 
 typedef enum gi_status {
     GI_OK = 0,
@@ -157,6 +157,9 @@ typedef struct gi_scene_info {
     int32_t x_nodes;          /* Mode X octree nodes */
     int32_t x_prims;          /* Mode X primitives */
     int64_t device_bytes;     /* scene bytes resident in HBM */
+    int32_t x_node_bytes;     /* Mode X traversal node record: 256 (XWNode) or 128 (quantised XCNode,
+                                 large HBM-resident scenes) -- bench.py's algorithmic bytes per visit */
+    int32_t x_lds_resident;   /* 1: Mode X stages the scene in LDS per workgroup */
 } gi_scene_info;
 
 typedef struct gi_hit {

@@ -212,6 +212,37 @@ static int check_structure(const HostScene& s, bool exact_once) {
     return 0;
 }
 
+// Quantised nodes (XCNode, the HBM-resident kernel's): every decoded child box -- fma(q, 2^e, org)
+// in fp32, as the kernel decodes it -- must contain the XWNode box; returns the nodes with the
+// decoded boxes, so that the traversal can be checked on them as well.
+static int check_quantised(const HostScene& s, std::vector<XWNode>& dec) {
+    std::vector<XCNode> q;
+    dec = s.xwnodes;
+    if (!encode_xcnodes(s.xwnodes, q)) {   // a leaf of more than 255 records: the scene keeps XWNode
+        std::printf("quantised nodes: not encodable, XWNode kept\n");
+        return 0;
+    }
+    for (size_t w = 0; w < q.size(); ++w) {
+        const XCNode& n = q[w];
+        if (n.exists != (uint8_t)s.xwnodes[w].exists || n.parent != s.xwnodes[w].parent) { std::printf("xc header\n"); return 1; }
+        for (int c = 0; c < 8; ++c) {
+            if (n.child[c] != s.xwnodes[w].child[c] || n.cnt[c] != s.xwnodes[w].cnt[c]) { std::printf("xc refs\n"); return 1; }
+            if (!((n.exists >> c) & 1)) continue;
+            for (int a = 0; a < 3; ++a) {
+                const float sc = std::ldexp(1.0f, n.ex[a]);
+                const float lo = std::fmaf((float)n.qlo[a][c], sc, n.org[a]), hi = std::fmaf((float)n.qhi[a][c], sc, n.org[a]);
+                if (!(lo <= s.xwnodes[w].lo[a][c] && hi >= s.xwnodes[w].hi[a][c])) {
+                    std::printf("quantised box does not contain node %zu child %d axis %d\n", w, c, a);
+                    return 1;
+                }
+                dec[w].lo[a][c] = lo;
+                dec[w].hi[a][c] = hi;
+            }
+        }
+    }
+    return 0;
+}
+
 static gi_entity_desc tri(double* v) {
     gi_entity_desc e{};
     e.kind = GI_IMP_TRIANGLE;
@@ -269,7 +300,11 @@ int main(int argc, char** argv) {
         if (!build_host_scene(sd, hs, err)) { std::printf("build failed: %s\n", err.c_str()); return 2; }
         const bool bvh = hs.xnodes.empty();
         if (check_structure(hs, bvh)) return 1;
+        std::vector<XWNode> dec;
+        if (check_quantised(hs, dec)) return 1;
         const long visits0 = visits, prims0 = g_prim_tests;
+        for (int pass = 0; pass < 2; ++pass) {   // the XWNode boxes, then the quantised ones
+        if (pass == 1) hs.xwnodes = dec;
         for (int r = 0; r < nrays; ++r) {
             V3 o, tgt;
             if (r % 2 == 0) o = v3(-10, 0, 0);
@@ -285,10 +320,12 @@ int main(int argc, char** argv) {
             ++total;
             if (shadow ? ((a >= 0) != (b >= 0)) : (a != b || !(t1 == t2 || (std::isinf(t1) && std::isinf(t2))))) ++mism;
         }
+        }
         std::printf("scene %d: %zu prims, %zu wide nodes, %zu leaf records, depth %d; per ray: %.2f node visits, %.2f prim tests"
                     " (SAH estimate %.2f / %.2f)\n",
                     scene, hs.xprims.size(), hs.xwnodes.size(), hs.xhot.size(), hs.x_max_depth,
-                    (double)(visits - visits0) / nrays, (double)(g_prim_tests - prims0) / nrays, hs.x_est_nodes, hs.x_est_prims);
+                    (double)(visits - visits0) / (2.0 * nrays), (double)(g_prim_tests - prims0) / (2.0 * nrays), hs.x_est_nodes,
+                    hs.x_est_prims);
     }
     std::printf("rays %ld mismatches %ld wide-node visits %ld\n", total, mism, visits);
     return mism == 0 ? 0 : 1;
