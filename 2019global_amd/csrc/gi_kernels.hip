@@ -789,6 +789,9 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 #ifndef GI_X_HELP
 #define GI_X_HELP 1   // HBM-resident scenes: shadow rays handed to idle lanes of the wave (XHelp)
 #endif
+#ifndef GI_X_CLIMB_CLZ
+#define GI_X_CLIMB_CLZ 1   // NST climb: the target level by a leading-zero count (C5 -2%), not a loop
+#endif
 #ifndef GI_X_NSTK
 #define GI_X_NSTK 1   // HBM-resident scenes: the node index of every traversal level kept in LDS
 #endif
@@ -1067,10 +1070,18 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 uint32_t rest = lvl_get(mlo, mhi, level);
                 if constexpr (NST) {
                     if (rest == 0 && level > 0) {
+#if GI_X_CLIMB_CLZ
+                        // the deepest level below with children left, by one leading-zero count
+                        const uint64_t lm = level >= 8 ? mlo : mlo & ((1ull << (8 * level)) - 1);
+                        const uint64_t hm = level <= 8 ? 0ull : mhi & ((1ull << (8 * (level - 8))) - 1);
+                        level = hm ? 8 + (63 - __clzll((long long)hm)) / 8 : lm ? (63 - __clzll((long long)lm)) / 8 : 0;
+                        rest = lvl_get(mlo, mhi, level);
+#else
                         do {
                             --level;
                             rest = lvl_get(mlo, mhi, level);
                         } while (rest == 0 && level > 0);
+#endif
                         node = level == 0 ? 0 : nst[level * 256];
                     }
                 } else {
