@@ -382,13 +382,27 @@ __device__ __forceinline__ F3 inv_dir(V3 d) {
               __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf((float)d.z), -1e30f, 1e30f));
 }
 __device__ __forceinline__ F3 neg_oiv(F3 of, F3 ivf) { return f3(-(of.x * ivf.x), -(of.y * ivf.y), -(of.z * ivf.z)); }
+// Near / far planes: on axis a a box's entry plane is its min plane when iv_a >= 0 and its max
+// plane otherwise, for every box -- fma(b, iv, -o*iv) is monotone in the plane b, rounding included
+// -- so t_near = t(near plane) and t_far = t(far plane) with no per-box min / max: exactly the
+// interval of the min / max form.  The sign comes from the fp32 reciprocal itself (sm: bit a set
+// when iv_a < 0), so a -0 direction component (reciprocal -1e30) is ordered correctly too.
+__device__ __forceinline__ int iv_signs(F3 ivf) {
+    return (int)((__float_as_uint(ivf.x) >> 31) | ((__float_as_uint(ivf.y) >> 31) << 1) |
+                 ((__float_as_uint(ivf.z) >> 31) << 2));
+}
 __device__ __forceinline__ bool child_hit(const XWNode* nd, int c, F3 of, F3 ivf, float tmax) {
     const F3 no = neg_oiv(of, ivf);
-    const float tx0 = __builtin_fmaf(nd->lo[0][c], ivf.x, no.x), tx1 = __builtin_fmaf(nd->hi[0][c], ivf.x, no.x);
-    const float ty0 = __builtin_fmaf(nd->lo[1][c], ivf.y, no.y), ty1 = __builtin_fmaf(nd->hi[1][c], ivf.y, no.y);
-    const float tz0 = __builtin_fmaf(nd->lo[2][c], ivf.z, no.z), tz1 = __builtin_fmaf(nd->hi[2][c], ivf.z, no.z);
-    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
-    const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
+    const int sm = iv_signs(ivf);
+    const float* L = &nd->lo[0][0];
+    const float* Hh = &nd->hi[0][0];
+    const float nx = (sm & 1) ? Hh[c] : L[c], fx = (sm & 1) ? L[c] : Hh[c];
+    const float ny = (sm & 2) ? Hh[8 + c] : L[8 + c], fy = (sm & 2) ? L[8 + c] : Hh[8 + c];
+    const float nz = (sm & 4) ? Hh[16 + c] : L[16 + c], fz = (sm & 4) ? L[16 + c] : Hh[16 + c];
+    const float tn = fmaxf(fmaxf(__builtin_fmaf(nx, ivf.x, no.x), __builtin_fmaf(ny, ivf.y, no.y)),
+                           fmaxf(__builtin_fmaf(nz, ivf.z, no.z), 0.0f));
+    const float tf = fminf(fminf(__builtin_fmaf(fx, ivf.x, no.x), __builtin_fmaf(fy, ivf.y, no.y)),
+                           fminf(__builtin_fmaf(fz, ivf.z, no.z), tmax));
     return tn <= tf;
 }
 __device__ __forceinline__ bool box32_hit(const XBox& b, F3 of, F3 ivf, float tmax) {
@@ -416,25 +430,28 @@ template <bool AXIS>
 __device__ __forceinline__ uint32_t children_mask(const XWNode* nd, F3 of, F3 ivf, float tmax, int dmask) {
     const float4* b = reinterpret_cast<const float4*>(nd);
     const F3 no = neg_oiv(of, ivf);
+    const int sm = iv_signs(ivf);   // near / far planes per axis (see child_hit)
     if constexpr (AXIS) {
     float tn[8], tf[8];
 #pragma unroll
     for (int c = 0; c < 8; ++c) { tn[c] = 0.0f; tf[c] = tmax; }
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        const float4 l0 = b[2 * a], l1 = b[2 * a + 1], h0 = b[6 + 2 * a], h1 = b[6 + 2 * a + 1];
+        // the near and far planes' quads addressed directly (lo at quad 2a, hi at 6 + 2a)
+        const int nq = ((sm >> a) & 1) ? 6 + 2 * a : 2 * a, fq = ((sm >> a) & 1) ? 2 * a : 6 + 2 * a;
+        const float4 n0 = b[nq], n1 = b[nq + 1], f0 = b[fq], f1 = b[fq + 1];
         const float o = a == 0 ? no.x : (a == 1 ? no.y : no.z), iv = a == 0 ? ivf.x : (a == 1 ? ivf.y : ivf.z);
         // children in pairs: one packed fma (v_pk_fma_f32) gives two children's plane distances
-        const f32x2 lo[4] = {f32x2{l0.x, l0.y}, f32x2{l0.z, l0.w}, f32x2{l1.x, l1.y}, f32x2{l1.z, l1.w}};
-        const f32x2 hi[4] = {f32x2{h0.x, h0.y}, f32x2{h0.z, h0.w}, f32x2{h1.x, h1.y}, f32x2{h1.z, h1.w}};
+        const f32x2 nr[4] = {f32x2{n0.x, n0.y}, f32x2{n0.z, n0.w}, f32x2{n1.x, n1.y}, f32x2{n1.z, n1.w}};
+        const f32x2 fr[4] = {f32x2{f0.x, f0.y}, f32x2{f0.z, f0.w}, f32x2{f1.x, f1.y}, f32x2{f1.z, f1.w}};
         const f32x2 iv2 = {iv, iv}, o2 = {o, o};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const f32x2 t0 = __builtin_elementwise_fma(lo[q], iv2, o2), t1 = __builtin_elementwise_fma(hi[q], iv2, o2);
-            tn[2 * q] = fmaxf(tn[2 * q], fminf(t0.x, t1.x));
-            tf[2 * q] = fminf(tf[2 * q], fmaxf(t0.x, t1.x));
-            tn[2 * q + 1] = fmaxf(tn[2 * q + 1], fminf(t0.y, t1.y));
-            tf[2 * q + 1] = fminf(tf[2 * q + 1], fmaxf(t0.y, t1.y));
+            const f32x2 t0 = __builtin_elementwise_fma(nr[q], iv2, o2), t1 = __builtin_elementwise_fma(fr[q], iv2, o2);
+            tn[2 * q] = fmaxf(tn[2 * q], t0.x);
+            tf[2 * q] = fminf(tf[2 * q], t1.x);
+            tn[2 * q + 1] = fmaxf(tn[2 * q + 1], t0.y);
+            tf[2 * q + 1] = fminf(tf[2 * q + 1], t1.y);
         }
     }
     uint32_t m = 0;
@@ -442,19 +459,26 @@ __device__ __forceinline__ uint32_t children_mask(const XWNode* nd, F3 of, F3 iv
     for (int c = 0; c < 8; ++c) m |= tn[c] <= tf[c] ? 1u << c : 0u;
     return xor_permute8(m & (uint32_t)nd->exists, dmask);
     } else {
+    // all 12 quads at once (one memory round trip), the near and far planes' addressed directly
     float4 q[12];
 #pragma unroll
-    for (int i = 0; i < 12; ++i) q[i] = b[i];
+    for (int a = 0; a < 3; ++a) {
+        const int nq = ((sm >> a) & 1) ? 6 + 2 * a : 2 * a, fq = ((sm >> a) & 1) ? 2 * a : 6 + 2 * a;
+        q[2 * a] = b[nq];
+        q[2 * a + 1] = b[nq + 1];
+        q[6 + 2 * a] = b[fq];
+        q[6 + 2 * a + 1] = b[fq + 1];
+    }
     const int ex = nd->exists;
-    const float* v = reinterpret_cast<const float*>(q);   // lo[3][8] then hi[3][8]
+    const float* v = reinterpret_cast<const float*>(q);   // near[3][8] then far[3][8]
     uint32_t m = 0;
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
-        const float tx0 = __builtin_fmaf(v[c], ivf.x, no.x), tx1 = __builtin_fmaf(v[24 + c], ivf.x, no.x);
-        const float ty0 = __builtin_fmaf(v[8 + c], ivf.y, no.y), ty1 = __builtin_fmaf(v[32 + c], ivf.y, no.y);
-        const float tz0 = __builtin_fmaf(v[16 + c], ivf.z, no.z), tz1 = __builtin_fmaf(v[40 + c], ivf.z, no.z);
-        const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
-        const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
+        const float nx = v[c], fx = v[24 + c], ny = v[8 + c], fy = v[32 + c], nz = v[16 + c], fz = v[40 + c];
+        const float tn = fmaxf(fmaxf(__builtin_fmaf(nx, ivf.x, no.x), __builtin_fmaf(ny, ivf.y, no.y)),
+                               fmaxf(__builtin_fmaf(nz, ivf.z, no.z), 0.0f));
+        const float tf = fminf(fminf(__builtin_fmaf(fx, ivf.x, no.x), __builtin_fmaf(fy, ivf.y, no.y)),
+                               fminf(__builtin_fmaf(fz, ivf.z, no.z), tmax));
         m |= tn <= tf ? 1u << c : 0u;
     }
     return xor_permute8(m & (uint32_t)ex, dmask);
@@ -462,8 +486,11 @@ __device__ __forceinline__ uint32_t children_mask(const XWNode* nd, F3 of, F3 iv
 }
 
 // Quantised nodes (XCNode, HBM-resident scenes): the 64 bytes the slab tests need arrive in four
-// 16-byte loads; each bound is decoded as fma(q, 2^e, org) -- the arithmetic the host checked the
-// encoding with -- and then tested exactly as an XWNode bound.
+// 16-byte loads.  A bound's slab distance is taken straight from its 8-bit q: t = fma(q, 2^e * iv,
+// fma(org, iv, -o * iv)) -- the decode fma(q, 2^e, org) and the slab fma folded into one; the
+// difference from decoding first is a few fp32 ulps of t, inside the 1e-5 * extent padding that
+// the host-checked decoded box already exceeds (the CPU checker runs this form).  Near / far
+// planes per axis as for XWNode.
 __device__ __forceinline__ float xc_scale(int w, int a) {   // 2^e of axis a (e: signed byte a of w)
     const int e = (int)(int8_t)((w >> (8 * a)) & 0xFF);
     return __int_as_float((e + 127) << 23);
@@ -476,22 +503,31 @@ __device__ __forceinline__ uint32_t children_mask(const XCNode* nd, F3 of, F3 iv
     const int4* b = reinterpret_cast<const int4*>(nd);
     const int4 h = b[0], q1 = b[1], q2 = b[2], q3 = b[3];
     const F3 no = neg_oiv(of, ivf);
+    const int sm = iv_signs(ivf);
+    const float iv3[3] = {ivf.x, ivf.y, ivf.z}, no3[3] = {no.x, no.y, no.z};
     const float o3[3] = {__int_as_float(h.x), __int_as_float(h.y), __int_as_float(h.z)};
-    const float s3[3] = {xc_scale(h.w, 0), xc_scale(h.w, 1), xc_scale(h.w, 2)};
     const int lw[3][2] = {{q1.x, q1.y}, {q1.z, q1.w}, {q2.x, q2.y}};   // qlo x, y, z
     const int hw[3][2] = {{q2.z, q2.w}, {q3.x, q3.y}, {q3.z, q3.w}};   // qhi x, y, z
-    const float iv3[3] = {ivf.x, ivf.y, ivf.z}, no3[3] = {no.x, no.y, no.z};
+    float siv[3], base[3];
+    int nw[3][2], fw[3][2];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        siv[a] = xc_scale(h.w, a) * iv3[a];
+        base[a] = __builtin_fmaf(o3[a], iv3[a], no3[a]);
+        const bool neg = (sm >> a) & 1;
+        nw[a][0] = neg ? hw[a][0] : lw[a][0];
+        nw[a][1] = neg ? hw[a][1] : lw[a][1];
+        fw[a][0] = neg ? lw[a][0] : hw[a][0];
+        fw[a][1] = neg ? lw[a][1] : hw[a][1];
+    }
     uint32_t m = 0;
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
         float tn = 0.0f, tf = tmax;
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
-            const float lo = __builtin_fmaf(xc_q(lw[a][0], lw[a][1], c), s3[a], o3[a]);
-            const float hi = __builtin_fmaf(xc_q(hw[a][0], hw[a][1], c), s3[a], o3[a]);
-            const float t0 = __builtin_fmaf(lo, iv3[a], no3[a]), t1 = __builtin_fmaf(hi, iv3[a], no3[a]);
-            tn = fmaxf(tn, fminf(t0, t1));
-            tf = fminf(tf, fmaxf(t0, t1));
+            tn = fmaxf(tn, __builtin_fmaf(xc_q(nw[a][0], nw[a][1], c), siv[a], base[a]));
+            tf = fminf(tf, __builtin_fmaf(xc_q(fw[a][0], fw[a][1], c), siv[a], base[a]));
         }
         m |= tn <= tf ? 1u << c : 0u;
     }
@@ -501,19 +537,20 @@ __device__ __forceinline__ bool child_hit(const XCNode* nd, int c, F3 of, F3 ivf
     const int4* b = reinterpret_cast<const int4*>(nd);
     const int4 h = b[0], q1 = b[1], q2 = b[2], q3 = b[3];
     const F3 no = neg_oiv(of, ivf);
+    const int sm = iv_signs(ivf);
+    const float iv3[3] = {ivf.x, ivf.y, ivf.z}, no3[3] = {no.x, no.y, no.z};
     const float o3[3] = {__int_as_float(h.x), __int_as_float(h.y), __int_as_float(h.z)};
     const int lw[3][2] = {{q1.x, q1.y}, {q1.z, q1.w}, {q2.x, q2.y}};
     const int hw[3][2] = {{q2.z, q2.w}, {q3.x, q3.y}, {q3.z, q3.w}};
-    const float iv3[3] = {ivf.x, ivf.y, ivf.z}, no3[3] = {no.x, no.y, no.z};
     float tn = 0.0f, tf = tmax;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        const float sa = xc_scale(h.w, a);
-        const float lo = __builtin_fmaf(xc_q(lw[a][0], lw[a][1], c), sa, o3[a]);
-        const float hi = __builtin_fmaf(xc_q(hw[a][0], hw[a][1], c), sa, o3[a]);
-        const float t0 = __builtin_fmaf(lo, iv3[a], no3[a]), t1 = __builtin_fmaf(hi, iv3[a], no3[a]);
-        tn = fmaxf(tn, fminf(t0, t1));
-        tf = fminf(tf, fmaxf(t0, t1));
+        const float siv = xc_scale(h.w, a) * iv3[a], base = __builtin_fmaf(o3[a], iv3[a], no3[a]);
+        const bool neg = (sm >> a) & 1;
+        const float tl = __builtin_fmaf(xc_q(lw[a][0], lw[a][1], c), siv, base);
+        const float th = __builtin_fmaf(xc_q(hw[a][0], hw[a][1], c), siv, base);
+        tn = fmaxf(tn, neg ? th : tl);
+        tf = fminf(tf, neg ? tl : th);
     }
     return tn <= tf;
 }

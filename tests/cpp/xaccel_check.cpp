@@ -81,8 +81,26 @@ static float up32(double v) {
 struct F3 { float x, y, z; };
 // the kernel's inv_dir: reciprocal clamped to +-1e30 (finite plane distances for axis-parallel rays)
 static float inv_clamp(float v) { return std::fmin(std::fmax(1.0f / v, -1e30f), 1e30f); }
+// pass 3: the quantised nodes with the kernel's fused arithmetic (children_mask(const XCNode*)):
+// t = fma(q, 2^e * iv, fma(org, iv, -(o * iv))) per bound, set while g_xc is non-null
+static const XCNode* g_xc = nullptr;
+static const XWNode* g_xw_base = nullptr;
+static bool child_hit_xc(const XCNode& n, int c, F3 of, F3 ivf, float tmax) {
+    const float iv[3] = {ivf.x, ivf.y, ivf.z}, o[3] = {of.x, of.y, of.z};
+    float tn = 0.0f, tf = tmax;
+    for (int a = 0; a < 3; ++a) {
+        const float no = -(o[a] * iv[a]);
+        const float siv = std::ldexp(1.0f, n.ex[a]) * iv[a], base = std::fmaf(n.org[a], iv[a], no);
+        const float tl = std::fmaf((float)n.qlo[a][c], siv, base), th = std::fmaf((float)n.qhi[a][c], siv, base);
+        const bool neg = std::signbit(iv[a]);
+        tn = std::fmax(tn, neg ? th : tl);
+        tf = std::fmin(tf, neg ? tl : th);
+    }
+    return tn <= tf;
+}
 // the kernel's form: plane distance fma(b, iv, -(o * iv))
 static bool child_hit(const XWNode* nd, int c, F3 of, F3 ivf, float tmax) {
+    if (g_xc) return child_hit_xc(g_xc[nd - g_xw_base], c, of, ivf, tmax);
     const float nx = -(of.x * ivf.x), ny = -(of.y * ivf.y), nz = -(of.z * ivf.z);
     const float tx0 = std::fmaf(nd->lo[0][c], ivf.x, nx), tx1 = std::fmaf(nd->hi[0][c], ivf.x, nx);
     const float ty0 = std::fmaf(nd->lo[1][c], ivf.y, ny), ty1 = std::fmaf(nd->hi[1][c], ivf.y, ny);
@@ -302,9 +320,15 @@ int main(int argc, char** argv) {
         if (check_structure(hs, bvh)) return 1;
         std::vector<XWNode> dec;
         if (check_quantised(hs, dec)) return 1;
+        std::vector<XCNode> xc;
+        const bool have_xc = encode_xcnodes(hs.xwnodes, xc);
+        const std::vector<XWNode> orig = hs.xwnodes;
         const long visits0 = visits, prims0 = g_prim_tests;
-        for (int pass = 0; pass < 2; ++pass) {   // the XWNode boxes, then the quantised ones
+        // the XWNode boxes; the decoded quantised boxes; the quantised nodes with the kernel's
+        // fused slab arithmetic
+        for (int pass = 0; pass < (have_xc ? 3 : 2); ++pass) {
         if (pass == 1) hs.xwnodes = dec;
+        if (pass == 2) { hs.xwnodes = orig; g_xc = xc.data(); g_xw_base = hs.xwnodes.data(); }
         for (int r = 0; r < nrays; ++r) {
             V3 o, tgt;
             if (r % 2 == 0) o = v3(-10, 0, 0);
@@ -321,10 +345,12 @@ int main(int argc, char** argv) {
             if (shadow ? ((a >= 0) != (b >= 0)) : (a != b || !(t1 == t2 || (std::isinf(t1) && std::isinf(t2))))) ++mism;
         }
         }
+        g_xc = nullptr;
         std::printf("scene %d: %zu prims, %zu wide nodes, %zu leaf records, depth %d; per ray: %.2f node visits, %.2f prim tests"
                     " (SAH estimate %.2f / %.2f)\n",
                     scene, hs.xprims.size(), hs.xwnodes.size(), hs.xhot.size(), hs.x_max_depth,
-                    (double)(visits - visits0) / (2.0 * nrays), (double)(g_prim_tests - prims0) / (2.0 * nrays), hs.x_est_nodes,
+                    (double)(visits - visits0) / ((have_xc ? 3.0 : 2.0) * nrays),
+                    (double)(g_prim_tests - prims0) / ((have_xc ? 3.0 : 2.0) * nrays), hs.x_est_nodes,
                     hs.x_est_prims);
     }
     std::printf("rays %ld mismatches %ld wide-node visits %ld\n", total, mism, visits);
