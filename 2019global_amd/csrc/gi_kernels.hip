@@ -667,6 +667,120 @@ __device__ __forceinline__ void trace_mode_r_cand(const DevScene& sc, V3 o, V3 d
     }
 }
 
+// Mode R with a pixel's candidates split over NSUB lanes (large scenes).  The frame time of
+// k_mode_r on the 100k soup is a few pixels' serial work -- their lines cross ~100 entity boxes,
+// and a single 8x8 tile of them takes 5-6 ms alone on the GPU -- so here NSUB adjacent lanes take
+// one pixel: all of them walk the pixel's line BVH (the same decisions: the walk does not depend
+// on what was found), and the k-th candidate met is considered by lane k mod NSUB only.  After
+// each leaf the group shares its best list rank (pruning, r_consider), and at the end the lane
+// holding the highest rank -- the reference's last hitting reachable candidate, A.1; every
+// candidate is considered by exactly one lane, so the maximum is the same -- shades the pixel.
+template <int NSUB>
+__device__ __forceinline__ long long group_max(long long v) {
+#pragma unroll
+    for (int off = 1; off < NSUB; off <<= 1) {
+        const long long u = __shfl_xor(v, off);
+        v = u > v ? u : v;
+    }
+    return v;
+}
+template <int NSUB>
+__device__ __forceinline__ void trace_mode_r_split(const DevScene& sc, V3 o, V3 d, float tau, int sub, RResult& r,
+                                                   long long& mine, uint32_t& nnode, uint32_t& nprim) {
+    r.ent = -1;
+    mine = -1;
+    long long best = -1;   // the group's best rank so far (pruning bound)
+    unsigned k = 0;        // candidates met so far (the same count in every lane of the group)
+    auto consider = [&](int e) {
+        if ((int)(k++ % NSUB) != sub) return;
+        const long long before = best;
+        r_consider(sc, e, o, d, best, r, nnode, nprim);
+        if (best != before) mine = best;
+    };
+    for (int i = 0; i < sc.n_r_always; ++i) consider(sc.r_always[i]);
+    best = group_max<NSUB>(best);
+    const XWNode* W = sc.rc_nodes;
+    const F3 of = f3((float)o.x, (float)o.y, (float)o.z);
+    const F3 ivf = f3(__builtin_amdgcn_rcpf((float)d.x), __builtin_amdgcn_rcpf((float)d.y), __builtin_amdgcn_rcpf((float)d.z));
+    uint64_t mlo = 0, mhi = 0;
+    int node = 0, level = 0;
+    const uint32_t rm = children_mask_line(W, of, ivf, tau);
+    lvl_set(mlo, mhi, 0, rm);
+    bool going = rm != 0;
+    while (going) {
+        const uint32_t msk = lvl_get(mlo, mhi, level);
+        const int c = __builtin_ctz(msk);
+        lvl_set(mlo, mhi, level, msk & (msk - 1));
+        const XWNode* nd = W + node;
+        const int ch = nd->child[c];
+        if (ch < 0) {
+            const int cnt = nd->cnt[c];
+            for (int j = 0; j < cnt; ++j) consider(sc.rc_ent[~ch + j]);
+            best = group_max<NSUB>(best);
+        } else {
+            const uint32_t cm = children_mask_line(W + ch, of, ivf, tau);
+            if (cm) {
+                node = ch;
+                ++level;
+                lvl_set(mlo, mhi, level, cm);
+            }
+        }
+        uint32_t rest = lvl_get(mlo, mhi, level);
+        while (rest == 0 && level > 0) {
+            --level;
+            node = level == 0 ? 0 : W[node].parent;
+            rest = lvl_get(mlo, mhi, level);
+        }
+        going = rest != 0;
+    }
+}
+
+template <bool STATS, int NSUB>
+__global__ __launch_bounds__(256) void k_mode_r_split(DevScene sc, CamDev cam, V3 light, TileMap m, double* rgb,
+                                                       uint8_t* rgb8, unsigned long long* stats, float tau) {
+    const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long ps = g / NSUB;   // pixel slot (tile order)
+    const int sub = (int)(g % NSUB);
+    const long long lt = ps >> 6;
+    long long idx = -1;
+    int x = 0, y = 0;
+    const bool ok = lt < m.n_local && slot_pixel(m, lt, (int)(ps & 63), idx, x, y);
+    y += m.y0;
+    uint32_t nnode = 0, nprim = 0;
+    if (ok) {
+        const V3 o = cam.pos;
+        const V3 d = normalize(primary_dir(cam, (double)x, (double)y));   // Ray ctor (ray.h:6)
+        RResult r;
+        long long mine;
+        trace_mode_r_split<NSUB>(sc, o, d, tau, sub, r, mine, nnode, nprim);
+        const long long gmax = group_max<NSUB>(mine);
+        // the lowest sub-lane holding the maximum shades (ranks are unique: one lane at most)
+        const unsigned long long m_win = __ballot(mine == gmax);
+        const int base = (int)(threadIdx.x & 63) & ~(NSUB - 1);
+        const bool writer = gmax < 0 ? sub == 0
+                                     : (int)(threadIdx.x & 63) == base + __builtin_ctz((uint32_t)((m_win >> base) & ((1u << NSUB) - 1)));
+        if (writer) {
+            double c0 = 0, c1 = 0, c2 = 0;
+            if (gmax >= 0) {
+                const REnt e = sc.ents[r.ent];
+                int32_t u, v;
+                tex_coord(sc, e, r.P, u, v);
+                const V3 col = shade_ref(e, d, light, r.P, r.N, u, v);
+                c0 = col.x; c1 = col.y; c2 = col.z;
+            }
+            if (rgb) { rgb[3 * idx] = c0; rgb[3 * idx + 1] = c1; rgb[3 * idx + 2] = c2; }
+            if (rgb8) quantize(c0, c1, c2, rgb8 + 3 * idx);
+        }
+    } else if (sub == 0 && idx >= 0 && m.shard_count > 1) {   // padding slot of a packed tile
+        if (rgb) { rgb[3 * idx] = 0; rgb[3 * idx + 1] = 0; rgb[3 * idx + 2] = 0; }
+        if (rgb8) { rgb8[3 * idx] = 0; rgb8[3 * idx + 1] = 0; rgb8[3 * idx + 2] = 0; }
+    }
+    if (STATS) {
+        const bool px = ok && sub == 0;
+        wave_add_stats(stats, px ? 1 : 0, nnode, nprim, px ? 1 : 0);
+    }
+}
+
 template <bool STATS>
 __global__ __launch_bounds__(256) void k_mode_r(DevScene sc, CamDev cam, V3 light, TileMap m, double* rgb,
                                                  uint8_t* rgb8, unsigned long long* stats, float tau, int dfs) {
@@ -1689,7 +1803,7 @@ long long shard_tiles(int w, int h, int shard_count) { return make_map(w, h, sha
 // overrides the shading-handler threshold, GI_X_FLAGS the schedule flags, GI_X_MAX_RUN the largest
 // work-unit run length (scenes of cheap background samples such as the main.cpp scene prefer 8).
 struct XEnv {
-    int lds = 1, h8 = 0, xf = -1, run_log2 = 0, help = 1, spread = -1;
+    int lds = 1, h8 = 0, xf = -1, run_log2 = 0, help = 1, spread = -1, r_split = -1;
 };
 const XEnv& x_env() {
     static XEnv env;
@@ -1700,6 +1814,7 @@ const XEnv& x_env() {
         if (const char* v = std::getenv("GI_X_FLAGS")) env.xf = std::atoi(v);
         if (const char* v = std::getenv("GI_X_HELP")) env.help = std::atoi(v) != 0;
         if (const char* v = std::getenv("GI_X_SPREAD")) env.spread = std::atoi(v);
+        if (const char* v = std::getenv("GI_R_SPLIT")) env.r_split = std::atoi(v);
         const char* v = std::getenv("GI_X_MAX_RUN");
         const int r = v ? std::max(1, std::min(128, std::atoi(v))) : GI_X_MAX_RUN;
         int lg = 0;
@@ -1751,9 +1866,20 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
         // an octree that never split is one leaf: its list scanned backwards (first success) is
         // already the least work
         const int dfs = ((o.flags & GI_FLAG_R_DFS) || sc.n_rnodes <= 1) ? 1 : 0;
+        // large scenes: a pixel's candidates split over 8 lanes (k_mode_r_split); GI_R_SPLIT=0 / 1
+        // forces either
+        const XEnv& env = x_env();
+        const bool split = !dfs && (env.r_split >= 0 ? env.r_split != 0 : sc.n_ents > 4096);
         mark(ev_begin);
-        if (stats) hipLaunchKernelGGL(k_mode_r<true>, grid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, dfs);
-        else hipLaunchKernelGGL(k_mode_r<false>, grid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, dfs);
+        if (split) {
+            const dim3 sgrid((unsigned)((m.n_local * (kTile * kTile) * 8 + 255) / 256));
+            if (stats) hipLaunchKernelGGL((k_mode_r_split<true, 8>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
+            else hipLaunchKernelGGL((k_mode_r_split<false, 8>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
+        } else if (stats) {
+            hipLaunchKernelGGL(k_mode_r<true>, grid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, dfs);
+        } else {
+            hipLaunchKernelGGL(k_mode_r<false>, grid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, dfs);
+        }
         mark(ev_end);
     } else {
         // persistent grid: as many 4-wave blocks as can be resident (xc, per scene), each wave pulls

@@ -19,6 +19,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="C4")
     ap.add_argument("--tiles", default="28920,28921,28680,29160")
+    ap.add_argument("--top", type=int, default=0,
+                    help="Mode R: also time every tile of the frame alone and print the N slowest")
     a = ap.parse_args()
     import torch
     from importlib import import_module
@@ -55,7 +57,20 @@ def main():
                           "clk_share": {k: round(st[i] / max(1, st[gi.STAT_X_CYC_ALL]), 3) for k, i in
                                         (("trav", gi.STAT_X_CYC_TRAV), ("shade", gi.STAT_X_CYC_HIT),
                                          ("next", gi.STAT_X_CYC_NEXT))}}), flush=True)
-
+    if a.top:   # every tile alone: is the frame bound by a few tiles' serial work?
+        evs = []
+        for t in range(n_tiles):
+            kw = dict(mode=mode, spp=spp, depth=depth, seed=2019, shard_count=split, shard_index=t)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            dev.render_device(cam, sc.light, w, h, buf.data_ptr(), buf8.data_ptr(), s.cuda_stream, **kw)
+            e1.record(s)
+            evs.append((t, e0, e1))
+        torch.cuda.synchronize()
+        ms = sorted(((e0.elapsed_time(e1), t) for t, e0, e1 in evs), reverse=True)
+        tot = sum(m for m, _ in ms)
+        print(json.dumps({"tiles": len(ms), "sum_ms": round(tot, 3), "median_ms": round(ms[len(ms) // 2][0], 4),
+                          "slowest": [(t, round(m, 4)) for m, t in ms[:a.top]]}), flush=True)
 
 if __name__ == "__main__":
     main()
