@@ -871,3 +871,41 @@ def test_mode_x_shadow_handoff_frame_identical(torch_cuda, tmp_path):
         sc = _scene(name)
         rgb, _ = dev_scene(name).render(cam_of(sc), sc.light, w, h, mode=gi.MODE_X, spp=spp, depth=depth, seed=2019)
         assert U.bits_equal(rgb, ref[name]).all(), name
+
+
+def test_mode_r_split_candidates_frame_identical(torch_cuda, tmp_path):
+    """Mode R with a pixel's candidates split over 8 lanes (k_mode_r_split, chosen for scenes of
+    more than 4096 entities; GI_R_SPLIT=1 forces it, read once per process: a child process renders)
+    gives the same frames bit for bit as one lane per pixel on every small scene -- spheres (tested
+    by every ray), all entity classes, and the sharded packed layout."""
+    import subprocess
+    import sys
+    cases = (("main", 200, 200, 1), ("zoo", 160, 160, 1), ("cornell", 128, 128, 1), ("soup1000", 160, 160, 3))
+    out = tmp_path / "split.npz"
+    code = ("import sys, numpy as np; sys.path.insert(0, %r); sys.path.insert(0, %r); import oracle_util as U; "
+            "import torch; gi = U.pkg(); S = U.scenes(); res = {}\n"
+            "for name, w, h, n in %r:\n"
+            "    sc = S.named_scene(name); d = gi.DeviceScene.from_scene(sc)\n"
+            "    cam = gi.Camera(sc.cam_pos, sc.cam_look, sc.focal)\n"
+            "    res[name] = d.render(cam, sc.light, w, h)[0]\n"
+            "    if n > 1:\n"
+            "        per = gi.shard_tiles(w, h, n) * gi.TILE * gi.TILE * 3\n"
+            "        p = torch.zeros(n * per, dtype=torch.float64, device='cuda')\n"
+            "        for r in range(n): d.render_device(cam, sc.light, w, h, p.data_ptr() + r * per * 8, 0, shard_count=n, shard_index=r)\n"
+            "        torch.cuda.synchronize(); res[name + '_packed'] = p.cpu().numpy()\n"
+            "np.savez(%r, **res)") % (U.ROOT, os.path.join(U.ROOT, "tests"), cases, str(out))
+    subprocess.run([sys.executable, "-c", code], check=True, timeout=300, env=dict(os.environ, GI_R_SPLIT="1"))
+    ref = np.load(out)
+    torch = torch_cuda
+    for name, w, h, n in cases:
+        sc = _scene(name)
+        d = dev_scene(name)
+        rgb, _ = d.render(cam_of(sc), sc.light, w, h)
+        assert U.bits_equal(rgb, ref[name]).all(), name
+        if n > 1:
+            per = gi.shard_tiles(w, h, n) * gi.TILE * gi.TILE * 3
+            p = torch.zeros(n * per, dtype=torch.float64, device="cuda")
+            for r in range(n):
+                d.render_device(cam_of(sc), sc.light, w, h, p.data_ptr() + r * per * 8, 0, shard_count=n, shard_index=r)
+            torch.cuda.synchronize()
+            assert U.bits_equal(p.cpu().numpy(), ref[name + "_packed"]).all(), name + " packed"
