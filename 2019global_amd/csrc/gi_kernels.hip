@@ -307,10 +307,17 @@ struct F3 {
 };
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ F3 f3(float x, float y, float z) { F3 r; r.x = x; r.y = y; r.z = z; return r; }
+// Per-level "children left" masks, 8 bits per level in two 64-bit words.  SH (trees of depth <= 7,
+// i.e. at most 8 levels): the low word alone, without the per-access choice of word (C3 -3%, C4 -5%,
+// C5 -3%).
+template <bool SH = false>
 __device__ __forceinline__ uint32_t lvl_get(uint64_t lo, uint64_t hi, int l) {
+    if (SH) return (uint32_t)((lo >> (8 * l)) & 0xFF);
     return (uint32_t)((l < 8 ? lo >> (8 * l) : hi >> (8 * (l - 8))) & 0xFF);
 }
+template <bool SH = false>
 __device__ __forceinline__ void lvl_set(uint64_t& lo, uint64_t& hi, int l, uint32_t m) {
+    if (SH) { lo = (lo & ~(0xFFull << (8 * l))) | ((uint64_t)m << (8 * l)); return; }
     if (l < 8) lo = (lo & ~(0xFFull << (8 * l))) | ((uint64_t)m << (8 * l));
     else hi = (hi & ~(0xFFull << (8 * (l - 8)))) | ((uint64_t)m << (8 * (l - 8)));
 }
@@ -1017,7 +1024,7 @@ __device__ __forceinline__ int nth_set_bit(unsigned long long m, unsigned n) {
 // NST: the wide-node index of every level of the current traversal path lives in LDS (nst[level *
 // 256], one column per lane), so climbing out of exhausted levels is one ds_read instead of a chain
 // of dependent parent-pointer loads from HBM / L2 (one per level climbed).
-template <bool STATS, bool PAIR, bool PSL, bool NST, bool HELP, typename NodeP, typename HotP, typename PrimP,
+template <bool STATS, bool PAIR, bool PSL, bool NST, bool HELP, bool SH, typename NodeP, typename HotP, typename PrimP,
           typename EntP>
 __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H, PrimP XP, EntP EN, double* pslot,
                                             int* nst, XHelp hp_,
@@ -1107,7 +1114,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 node = 0;
                 level = 0;
                 mlo = mhi = 0;
-                lvl_set(mlo, mhi, 0, rm);
+                lvl_set<SH>(mlo, mhi, 0, rm);
                 raying = rm != 0;
             }
         }
@@ -1149,9 +1156,9 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             // ---- one traversal step (stackless: 8-bit "children left" mask per level).  Invariant:
             // the current level has a child left; the step pops it, then climbs past exhausted
             // levels, so a ray ends in the step that exhausts the root level (no empty iteration).
-            const uint32_t msk = lvl_get(mlo, mhi, level);
+            const uint32_t msk = lvl_get<SH>(mlo, mhi, level);
             const int kc = __builtin_ctz(msk);         // next child in front-to-back order
-            lvl_set(mlo, mhi, level, msk & (msk - 1));
+            lvl_set<SH>(mlo, mhi, level, msk & (msk - 1));
             const int c = kc ^ dmask;
             const auto* nd = W + node;
             const int ch = nd->child[c];
@@ -1212,13 +1219,13 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     if (cm) {
                         node = ch;
                         ++level;
-                        lvl_set(mlo, mhi, level, cm);
+                        lvl_set<SH>(mlo, mhi, level, cm);
                         if (NST) nst[level * 256] = ch;
                     }
                 }
             }
             if (raying) {                 // climb to the nearest level with children left
-                uint32_t rest = lvl_get(mlo, mhi, level);
+                uint32_t rest = lvl_get<SH>(mlo, mhi, level);
                 if constexpr (NST) {
                     if (rest == 0 && level > 0) {
 #if GI_X_CLIMB_CLZ
@@ -1226,11 +1233,11 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                         const uint64_t lm = level >= 8 ? mlo : mlo & ((1ull << (8 * level)) - 1);
                         const uint64_t hm = level <= 8 ? 0ull : mhi & ((1ull << (8 * (level - 8))) - 1);
                         level = hm ? 8 + (63 - __clzll((long long)hm)) / 8 : lm ? (63 - __clzll((long long)lm)) / 8 : 0;
-                        rest = lvl_get(mlo, mhi, level);
+                        rest = lvl_get<SH>(mlo, mhi, level);
 #else
                         do {
                             --level;
-                            rest = lvl_get(mlo, mhi, level);
+                            rest = lvl_get<SH>(mlo, mhi, level);
                         } while (rest == 0 && level > 0);
 #endif
                         node = level == 0 ? 0 : nst[level * 256];
@@ -1239,7 +1246,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     while (rest == 0 && level > 0) {
                         --level;
                         node = level == 0 ? 0 : W[node].parent;   // the root is node 0: no load
-                        rest = lvl_get(mlo, mhi, level);
+                        rest = lvl_get<SH>(mlo, mhi, level);
                     }
                 }
                 if (rest == 0) raying = false;   // ray finished
@@ -1265,7 +1272,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 node = 0;
                 level = 0;
                 mlo = mhi = 0;
-                lvl_set(mlo, mhi, 0, rm);
+                lvl_set<SH>(mlo, mhi, 0, rm);
                 raying = rm != 0;
             }
             }
@@ -1548,7 +1555,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 node = 0;   // root wide node
                 level = 0;
                 mlo = mhi = 0;
-                lvl_set(mlo, mhi, 0, rm);
+                lvl_set<SH>(mlo, mhi, 0, rm);
                 raying = rm != 0;   // no root child hit: finished (consumed by the next handler run)
                 break;
             }
@@ -1588,7 +1595,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
 // 2.64 ms, with spread work groups 2.40 ms); in long launches (C5) the handoff build's heavier code
 // costs 8%, so they run without.
 // CN (HBM-resident scenes): traverse the quantised nodes (DevScene::xcnodes) instead of XWNode.
-template <bool STATS, bool LDS, bool W4, bool CN>
+template <bool STATS, bool LDS, bool W4, bool CN, bool SH>
 __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WAVES) void k_mode_x(DevScene sc, CamDev cam, V3 light, TileMap m, int spp, int depth,
                                                  uint64_t seed, double* rgb, uint8_t* rgb8,
                                                  unsigned long long* stats, XWork wk, int handle8, int xflags) {
@@ -1620,7 +1627,7 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
         // (occluded sum, next direction, throughput T, RNG key) live in a per-lane LDS slot after
         // the scene instead of in VGPRs / scratch
         double* pslot = reinterpret_cast<double*>(lds_scene + nw + nh + np + ne) + 10 * threadIdx.x;
-        mode_x_wave<STATS, GI_X_PAIR != 0, W4 && GI_X_PSL, false, false>(sc, W, H, XP, EN, pslot, nullptr, XHelp{},
+        mode_x_wave<STATS, GI_X_PAIR != 0, W4 && GI_X_PSL, false, false, SH>(sc, W, H, XP, EN, pslot, nullptr, XHelp{},
                                                                         cam, light, m, spp, depth, seed, rgb, rgb8, blk,
                                                                         wk, handle8, xflags, c);
     } else {
@@ -1632,12 +1639,12 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
         hp.own = reinterpret_cast<int*>(hp.ray + 7 * 256);
         hp.res = hp.own + 256;
         if constexpr (CN)   // quantised nodes (the default for HBM-resident scenes)
-            mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0>(sc, sc.xcnodes, sc.xhot, sc.xprims,
+            mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0, SH>(sc, sc.xcnodes, sc.xhot, sc.xprims,
                                                                             sc.ents, nullptr, lds_nst + threadIdx.x, hp,
                                                                             cam, light, m, spp, depth, seed, rgb, rgb8,
                                                                             blk, wk, handle8, xflags, c);
         else
-            mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0>(sc, sc.xwnodes, sc.xhot, sc.xprims,
+            mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0, SH>(sc, sc.xwnodes, sc.xhot, sc.xprims,
                                                                             sc.ents, nullptr, lds_nst + threadIdx.x, hp,
                                                                             cam, light, m, spp, depth, seed, rgb, rgb8,
                                                                             blk, wk, handle8, xflags, c);
@@ -1834,10 +1841,10 @@ hipError_t x_launch_config(const DevScene& sc, int device, XLaunchCfg& cfg) {
     hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
     if (e != hipSuccess) return e;
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, cfg.kv == 3 ? reinterpret_cast<const void*>(k_mode_x<false, true, true, false>)
-                 : cfg.kv == 2 ? reinterpret_cast<const void*>(k_mode_x<false, true, false, false>)
-                 : sc.xcnodes  ? reinterpret_cast<const void*>(k_mode_x<false, false, false, true>)
-                               : reinterpret_cast<const void*>(k_mode_x<false, false, false, false>),
+        &per_cu, cfg.kv == 3 ? reinterpret_cast<const void*>(k_mode_x<false, true, true, false, false>)
+                 : cfg.kv == 2 ? reinterpret_cast<const void*>(k_mode_x<false, true, false, false, false>)
+                 : sc.xcnodes  ? reinterpret_cast<const void*>(k_mode_x<false, false, false, true, false>)
+                               : reinterpret_cast<const void*>(k_mode_x<false, false, false, false, false>),
         64 * kWavesPerBlock, cfg.lds_bytes);
     if (e != hipSuccess) return e;
     cfg.resident = std::max(1, cus) * std::max(1, per_cu);
@@ -1919,10 +1926,14 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
                        ((o.flags & GI_FLAG_X_NO_SHADOW) ? 4 : 0) | (env.help ? 8 : 0) |
                        ((env.spread > 0 || (env.spread < 0 && help)) ? 16 : 0);
         const bool cn = kv < 2 && sc.xcnodes != nullptr;
-#define GI_LAUNCH_X(S, L, W) hipLaunchKernelGGL((k_mode_x<S, L, W, false>), pgrid, block, lds_bytes, stream, sc, cam, light, m, o.spp, \
+#define GI_LAUNCH_X1(S, L, W, SH) hipLaunchKernelGGL((k_mode_x<S, L, W, false, SH>), pgrid, block, lds_bytes, stream, sc, cam, light, m, o.spp, \
                                            o.depth, o.seed, rgb, rgb8, st, wk, h8, xf)
-#define GI_LAUNCH_XC(S, W) hipLaunchKernelGGL((k_mode_x<S, false, W, true>), pgrid, block, lds_bytes, stream, sc, cam, light, m, \
+#define GI_LAUNCH_XC1(S, W, SH) hipLaunchKernelGGL((k_mode_x<S, false, W, true, SH>), pgrid, block, lds_bytes, stream, sc, cam, light, m, \
                                           o.spp, o.depth, o.seed, rgb, rgb8, st, wk, h8, xf)
+        // SH: the per-level masks in one 64-bit word when the tree has at most 8 levels
+        const bool sh = sc.x_max_depth <= 7;
+#define GI_LAUNCH_X(S, L, W) do { if (sh) GI_LAUNCH_X1(S, L, W, true); else GI_LAUNCH_X1(S, L, W, false); } while (0)
+#define GI_LAUNCH_XC(S, W) do { if (sh) GI_LAUNCH_XC1(S, W, true); else GI_LAUNCH_XC1(S, W, false); } while (0)
         mark(ev_begin);
         if (stats) {
             if (kv == 3) GI_LAUNCH_X(true, true, true); else if (kv == 2) GI_LAUNCH_X(true, true, false);
@@ -1936,6 +1947,8 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
         mark(ev_end);
 #undef GI_LAUNCH_X
 #undef GI_LAUNCH_XC
+#undef GI_LAUNCH_X1
+#undef GI_LAUNCH_XC1
         if (o.spp > 1) hipLaunchKernelGGL(k_x_reduce, sgrid, dim3(256), 0, stream, m, wk, o.spp, rgb, rgb8);
     }
     if (timed) kt->recorded++;

@@ -909,3 +909,26 @@ def test_mode_r_split_candidates_frame_identical(torch_cuda, tmp_path):
                 d.render_device(cam_of(sc), sc.light, w, h, p.data_ptr() + r * per * 8, 0, shard_count=n, shard_index=r)
             torch.cuda.synchronize()
             assert U.bits_equal(p.cpu().numpy(), ref[name + "_packed"]).all(), name + " packed"
+
+
+@pytest.mark.parametrize("accel", [{"GI_XACCEL": "octree"}, {"GI_XLEAF_MAX": "1"}])
+def test_mode_x_other_acceleration_structures_bit_exact(torch_cuda, accel):
+    """Mode X over the SAT octree (GI_XACCEL=octree: up to 12 levels, so the kernel keeps its two-word
+    level masks) and over a BVH of single-primitive leaves (GI_XLEAF_MAX=1), both read when the
+    scene is built: frames equal the oracle's bit for bit -- the result does not depend on the
+    acceleration structure."""
+    old = {k: os.environ.get(k) for k in accel}
+    os.environ.update(accel)
+    try:
+        devs = {name: gi.DeviceScene.from_scene(_scene(name)) for name in ("cornell", "soup1000")}
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    for name, (w, h, spp, depth) in (("cornell", (48, 40, 3, 5)), ("soup1000", (64, 48, 2, 8))):
+        sc = _scene(name)
+        rgb, _ = devs[name].render(cam_of(sc), sc.light, w, h, mode=gi.MODE_X, spp=spp, depth=depth, seed=7)
+        o = U.oracle_render(sc.to_scn(), w, h, mode=1, spp=spp, depth=depth, seed=7)
+        assert U.bits_equal(rgb.reshape(-1, 3), o["rgb"]).all(), (name, accel)
