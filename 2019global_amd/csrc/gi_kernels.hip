@@ -682,6 +682,9 @@ __device__ __forceinline__ void trace_mode_r_cand(const DevScene& sc, V3 o, V3 d
 // each leaf the group shares its best list rank (pruning, r_consider), and at the end the lane
 // holding the highest rank -- the reference's last hitting reachable candidate, A.1; every
 // candidate is considered by exactly one lane, so the maximum is the same -- shades the pixel.
+#ifndef GI_R_NSUB
+#define GI_R_NSUB 8   // lanes per pixel in k_mode_r_split (a power of two <= 32)
+#endif
 template <int NSUB>
 __device__ __forceinline__ long long group_max(long long v) {
 #pragma unroll
@@ -765,7 +768,7 @@ __global__ __launch_bounds__(256) void k_mode_r_split(DevScene sc, CamDev cam, V
         const unsigned long long m_win = __ballot(mine == gmax);
         const int base = (int)(threadIdx.x & 63) & ~(NSUB - 1);
         const bool writer = gmax < 0 ? sub == 0
-                                     : (int)(threadIdx.x & 63) == base + __builtin_ctz((uint32_t)((m_win >> base) & ((1u << NSUB) - 1)));
+                                     : (int)(threadIdx.x & 63) == base + __builtin_ctz((uint32_t)((m_win >> base) & ((1ull << NSUB) - 1)));
         if (writer) {
             double c0 = 0, c1 = 0, c2 = 0;
             if (gmax >= 0) {
@@ -1879,9 +1882,9 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
         const bool split = !dfs && (env.r_split >= 0 ? env.r_split != 0 : sc.n_ents > 4096);
         mark(ev_begin);
         if (split) {
-            const dim3 sgrid((unsigned)((m.n_local * (kTile * kTile) * 8 + 255) / 256));
-            if (stats) hipLaunchKernelGGL((k_mode_r_split<true, 8>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
-            else hipLaunchKernelGGL((k_mode_r_split<false, 8>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
+            const dim3 sgrid((unsigned)((m.n_local * (kTile * kTile) * GI_R_NSUB + 255) / 256));
+            if (stats) hipLaunchKernelGGL((k_mode_r_split<true, GI_R_NSUB>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
+            else hipLaunchKernelGGL((k_mode_r_split<false, GI_R_NSUB>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
         } else if (stats) {
             hipLaunchKernelGGL(k_mode_r<true>, grid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, dfs);
         } else {
