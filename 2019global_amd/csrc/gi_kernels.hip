@@ -584,19 +584,29 @@ __device__ __forceinline__ bool root_hit(const DevScene& sc, F3 of, F3 ivf) {
 // the 8 children of a line-BVH node against the whole line o + t d (t real), boxes widened by tau
 __device__ __forceinline__ uint32_t children_mask_line(const XWNode* nd, F3 of, F3 ivf, float tau) {
     const float4* b = reinterpret_cast<const float4*>(nd);
-    float4 q[12];
+    // near / far planes by the sign of the (clamped) reciprocal, as in the Mode X node tests: the
+    // distance ((b -+ tau) - o) * iv is monotone in b, so no per-child min / max; the planes' quads
+    // are addressed directly (lo of axis a at quad 2a, hi at 6 + 2a)
+    const int sm = iv_signs(ivf);
+    float4 q[12];   // near[3][8] then far[3][8]
 #pragma unroll
-    for (int i = 0; i < 12; ++i) q[i] = b[i];
+    for (int a = 0; a < 3; ++a) {
+        const int nq = ((sm >> a) & 1) ? 6 + 2 * a : 2 * a, fq = ((sm >> a) & 1) ? 2 * a : 6 + 2 * a;
+        q[2 * a] = b[nq];
+        q[2 * a + 1] = b[nq + 1];
+        q[6 + 2 * a] = b[fq];
+        q[6 + 2 * a + 1] = b[fq + 1];
+    }
     const int ex = nd->exists;
-    const float* v = reinterpret_cast<const float*>(q);   // lo[3][8] then hi[3][8]
+    const float* v = reinterpret_cast<const float*>(q);
+    const float sx = (sm & 1) ? tau : -tau, sy = (sm & 2) ? tau : -tau, sz = (sm & 4) ? tau : -tau;
     uint32_t m = 0;
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
-        const float tx0 = ((v[c] - tau) - of.x) * ivf.x, tx1 = ((v[24 + c] + tau) - of.x) * ivf.x;
-        const float ty0 = ((v[8 + c] - tau) - of.y) * ivf.y, ty1 = ((v[32 + c] + tau) - of.y) * ivf.y;
-        const float tz0 = ((v[16 + c] - tau) - of.z) * ivf.z, tz1 = ((v[40 + c] + tau) - of.z) * ivf.z;
-        const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
-        const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+        const float tn = fmaxf(fmaxf(((v[c] + sx) - of.x) * ivf.x, ((v[8 + c] + sy) - of.y) * ivf.y),
+                               ((v[16 + c] + sz) - of.z) * ivf.z);
+        const float tf = fminf(fminf(((v[24 + c] - sx) - of.x) * ivf.x, ((v[32 + c] - sy) - of.y) * ivf.y),
+                               ((v[40 + c] - sz) - of.z) * ivf.z);
         m |= (uint32_t)((tn <= tf) & ((ex >> c) & 1)) << c;
     }
     return m;
@@ -641,7 +651,7 @@ __device__ __forceinline__ void trace_mode_r_cand(const DevScene& sc, V3 o, V3 d
     for (int i = 0; i < sc.n_r_always; ++i) r_consider(sc, sc.r_always[i], o, d, best, r, nnode, nprim);
     const XWNode* W = sc.rc_nodes;
     const F3 of = f3((float)o.x, (float)o.y, (float)o.z);
-    const F3 ivf = f3(__builtin_amdgcn_rcpf((float)d.x), __builtin_amdgcn_rcpf((float)d.y), __builtin_amdgcn_rcpf((float)d.z));
+    const F3 ivf = inv_dir(d);   // clamped to +-1e30: finite plane distances, near / far by sign
     uint64_t mlo = 0, mhi = 0;
     int node = 0, level = 0;
     const uint32_t rm = children_mask_line(W, of, ivf, tau);
@@ -711,7 +721,7 @@ __device__ __forceinline__ void trace_mode_r_split(const DevScene& sc, V3 o, V3 
     best = group_max<NSUB>(best);
     const XWNode* W = sc.rc_nodes;
     const F3 of = f3((float)o.x, (float)o.y, (float)o.z);
-    const F3 ivf = f3(__builtin_amdgcn_rcpf((float)d.x), __builtin_amdgcn_rcpf((float)d.y), __builtin_amdgcn_rcpf((float)d.z));
+    const F3 ivf = inv_dir(d);   // clamped to +-1e30: finite plane distances, near / far by sign
     uint64_t mlo = 0, mhi = 0;
     int node = 0, level = 0;
     const uint32_t rm = children_mask_line(W, of, ivf, tau);

@@ -155,7 +155,9 @@ static Res candidates(const HostScene& s, V3 o, V3 d, long& considered) {
     const double reach = std::fmax(std::fabs(o.x), std::fmax(std::fabs(o.y), std::fabs(o.z))) + s.rc_ext;
     const float tau = (float)(1e-5 * reach + 1e-30);
     const float of[3] = {(float)o.x, (float)o.y, (float)o.z};
-    const float iv[3] = {1.0f / (float)d.x, 1.0f / (float)d.y, 1.0f / (float)d.z};
+    // the kernel's inv_dir: reciprocal clamped to +-1e30
+    auto inv = [](float v) { return std::fmin(std::fmax(1.0f / v, -1e30f), 1e30f); };
+    const float iv[3] = {inv((float)d.x), inv((float)d.y), inv((float)d.z)};
     std::vector<int> stack = {0};
     while (!stack.empty()) {
         const XWNode& nd = s.rc_nodes[stack.back()];
