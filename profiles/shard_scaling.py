@@ -54,7 +54,9 @@ def main():
             it, rays = st[gi.STAT_X_ITERS], max(1, st[gi.STAT_RAYS])
             sched = {"rays": rays, "wave_iters_per_kray": round(it * 1e3 / rays, 3),
                      "trav_lane_fill": round(st[gi.STAT_X_TRAV] / max(1, 64.0 * it), 4),
-                     "handler_lane_fill": round(st[gi.STAT_X_HLANES] / max(1, 64.0 * st[gi.STAT_X_HANDLE]), 4)}
+                     "handler_lane_fill": round(st[gi.STAT_X_HLANES] / max(1, 64.0 * st[gi.STAT_X_HANDLE]), 4),
+                     "longest_path_ms": round((st[gi.STAT_X_PATH_MAX] >> 32) / 1e5, 4),
+                     "longest_path_iters": (st[gi.STAT_X_PATH_MAX] >> 16) & 0xFFFF}
             if n == 1:
                 t1 = ms
             res[f"N{n}_rank{r}_ms"] = round(ms, 3)
