@@ -36,7 +36,7 @@ __all__ = [
     "GIError", "lib", "Camera", "Material", "Octree", "ImpSphere", "ImpTriangle", "ExpQuad",
     "ExpSphere", "ExpCube", "ExpCone", "ExpRectangle", "ExpBox",
     "RayTracer", "DeviceScene", "MODE_R", "MODE_X", "STAT_RAYS", "STAT_NODES", "STAT_PRIMS",
-    "STAT_PIXELS", "TILE", "MultiScene", "devices_from_env",
+    "STAT_PIXELS", "TILE", "MultiScene", "devices_from_env", "obj_entities",
 ]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -53,7 +53,7 @@ STAT_X_CYC_TRAV, STAT_X_CYC_HIT, STAT_X_CYC_NEXT, STAT_X_CYC_ALL = 11, 12, 13, 1
 STAT_X_RESOLVED = 15
 STATS_N = 16
 TILE = 8
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 class GIError(RuntimeError):
@@ -102,7 +102,8 @@ TILE_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ct
 EXPORTS = ["gi_abi_version", "gi_last_error", "gi_camera_init", "gi_scene_create", "gi_scene_destroy",
            "gi_scene_get_info", "gi_render", "gi_render_device", "gi_shard_tiles", "gi_unshard_device",
            "gi_trace_ray", "gi_kat_expbox", "gi_scene_kernel_ms", "gi_octree_create", "gi_octree_destroy",
-           "gi_octree_intersect", "gi_multi_create", "gi_multi_destroy", "gi_multi_info", "gi_multi_render", "gi_device_count"]
+           "gi_octree_intersect", "gi_multi_create", "gi_multi_destroy", "gi_multi_info", "gi_multi_render", "gi_device_count",
+           "gi_obj_parse"]
 
 _lib = None
 _lock = threading.Lock()
@@ -151,6 +152,8 @@ def lib():
                                     ctypes.POINTER(ctypes.c_int)]
         L.gi_multi_render.argtypes = [vp, ctypes.POINTER(CameraDesc), dp, i32, i32, ctypes.POINTER(Opts), dp,
                                       ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_int), TILE_CB, vp]
+        L.gi_obj_parse.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.POINTER(EntityDesc),
+                                   ctypes.POINTER(EntityDesc), ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
         if L.gi_abi_version() != ABI_VERSION:
             raise GIError(f"libgi ABI {L.gi_abi_version()} != {ABI_VERSION}")
         _lib = L
@@ -271,6 +274,33 @@ class ExpBox(_Entity):
 
     def __init__(self, mn, mx):
         super().__init__((*mn, *mx), None)
+
+
+def obj_entities(text, material: Optional[Material] = None) -> list:
+    """A Wavefront OBJ mesh (text or bytes) as ImpTriangle entities (entities.h:138), one per
+    triangle of each face's fan in file order, through libgi's gi_obj_parse (no device needed);
+    push them onto an Octree like hand-built entities.  `material` is set on every triangle (None:
+    the reference's default ImpTriangle material)."""
+    L = lib()
+    data = text.encode() if isinstance(text, str) else bytes(text)
+    tmpl = None
+    if material is not None:
+        tmpl = EntityDesc()
+        t = _Entity((), material)
+        t._desc(tmpl)
+    n = ctypes.c_int64()
+    _check(L.gi_obj_parse(data, len(data), tmpl, None, 0, ctypes.byref(n)), "gi_obj_parse")
+    arr = (EntityDesc * max(1, n.value))()
+    _check(L.gi_obj_parse(data, len(data), tmpl, arr, n.value, ctypes.byref(n)), "gi_obj_parse")
+    out = []
+    for i in range(n.value):
+        d = arr[i]
+        e = ImpTriangle(tuple(d.args[0:3]), tuple(d.args[3:6]), tuple(d.args[6:9]))
+        if material is not None:
+            e.material = Material(material.color, material.shader_parameters, material.specular_power,
+                                  material.reflectivity)
+        out.append(e)
+    return out
 
 
 class Octree:

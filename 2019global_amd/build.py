@@ -20,7 +20,7 @@ OUT = os.path.join(HERE, "libgi.so")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = "gfx950"
 
-HOST_SRCS = ["gi_build.cpp", "gi_bvh.cpp", "gi_capi.cpp", "gi_multi.cpp"]
+HOST_SRCS = ["gi_build.cpp", "gi_bvh.cpp", "gi_capi.cpp", "gi_multi.cpp", "gi_obj.cpp"]
 DEV_SRCS = ["gi_kernels.hip"]
 HEADERS = ["gi_math.h", "gi_scene.h", "gi_internal.h"]
 

@@ -171,6 +171,71 @@ def parse_scn(text: str) -> Scene:
     return s
 
 
+def load_obj(text: str, material: Optional[Material] = None, scene: Optional[Scene] = None) -> Scene:
+    """Wavefront OBJ text -> ImpTriangle entities appended to `scene` (a new Scene if None), one per
+    triangle of each face's fan (v0, v_k, v_k+1) in file order, each with `material` (None: the
+    reference's default ImpTriangle material).  The same rules as libgi's gi_obj_parse
+    (2019global_amd/csrc/gi_obj.cpp; tests compare the two): v (values after xyz ignored), f with
+    i, i/t, i//n, i/t/n references (1-based, negative = relative to the last vertex), '#' comments,
+    '\\' continuations; vt, vn, vp, o, g, s, usemtl, mtllib, l, p are skipped.  ValueError with the
+    line number on a malformed v / f line or a vertex reference out of range."""
+    s = scene if scene is not None else Scene(name="obj", entities=[])
+    verts: List[Vec3] = []
+    lines = text.split("\n")
+    k = 0
+    while k < len(lines):
+        parts = []
+        while True:   # one logical line: a physical line ending in '\' (before any comment) continues
+            raw = lines[k].rstrip("\r")
+            k += 1
+            h = raw.find("#")
+            body = raw if h < 0 else raw[:h]
+            if h < 0 and raw.endswith("\\"):
+                parts.append(raw[:-1])
+                if k >= len(lines):
+                    break
+                continue
+            parts.append(body)
+            break
+        lineno = k   # the logical line's last physical line, as gi_obj_parse reports it
+        tok = " ".join(parts).replace("\t", " ").replace("\r", " ").split(" ")
+        tok = [t for t in tok if t]
+        if not tok:
+            continue
+        if tok[0] == "v":
+            if len(tok) < 4:
+                raise ValueError(f"obj line {lineno}: v needs 3 coordinates")
+            try:
+                xyz = tuple(float(t) for t in tok[1:4])
+            except ValueError:
+                raise ValueError(f"obj line {lineno}: bad coordinate") from None
+            if not all(math.isfinite(c) for c in xyz):
+                raise ValueError(f"obj line {lineno}: bad coordinate")
+            verts.append(xyz)
+        elif tok[0] == "f":
+            if len(tok) < 4:
+                raise ValueError(f"obj line {lineno}: a face needs 3 vertices")
+            idx = []
+            for t in tok[1:]:
+                ref = t.split("/", 1)[0]
+                try:
+                    r = int(ref, 10)
+                except ValueError:
+                    raise ValueError(f"obj line {lineno}: bad vertex reference") from None
+                if r == 0:
+                    raise ValueError(f"obj line {lineno}: bad vertex reference")
+                z = r - 1 if r > 0 else len(verts) + r
+                if not 0 <= z < len(verts):
+                    raise ValueError(f"obj line {lineno}: vertex {r} out of range")
+                idx.append(z)
+            for j in range(1, len(idx) - 1):
+                e = s._add(IMP_TRIANGLE, (*verts[idx[0]], *verts[idx[j]], *verts[idx[j + 1]]))
+                if material is not None:
+                    e.material = Material(material.color, material.shader, material.specular_power,
+                                          material.reflectivity)
+    return s
+
+
 # ---------------------------------------------------------------------------------------------
 # Config scenes
 # ---------------------------------------------------------------------------------------------

@@ -20,6 +20,8 @@
  *   gi_octree_*          Octree(min,max) + push_back (octree.h:14-43) and the public query
  *                        Octree::intersect(const Ray&) (octree.h:46-68 -> Node::intersect :132-155)
  *                        on the host, for reference-side callers of the candidate list
+ *   gi_obj_parse         scene I/O: a Wavefront OBJ mesh as the run of
+ *                        ImpTriangle(p1, p2, p3) pushes (entities.h:138) main.cpp:24-48 would write
  *   gi_multi_*           RayTracer::run over several GPUs of one process: a scene replica per
  *                        device, 8x8 tiles dealt round-robin, RCCL send/recv gather over xGMI to
  *                        the first device (the drop-in RayTracer uses it when GI_DEVICES lists
@@ -40,7 +42,7 @@
 extern "C" {
 #endif
 
-#define GI_ABI_VERSION 6
+#define GI_ABI_VERSION 7
 
 typedef enum gi_status {
     GI_OK = 0,
@@ -247,6 +249,18 @@ void gi_multi_destroy(gi_multi* multi);
 int gi_multi_info(const gi_multi* multi, int* n_shards, int* n_devices, int* uses_rccl);
 int gi_multi_render(gi_multi* multi, const gi_camera* cam, const double light[3], int w, int h, const gi_opts* opts,
                     double* rgb, uint8_t* rgb8, const volatile int* cancel, gi_tile_cb cb, void* user);
+
+/* ---- scene I/O --------------------------------------------------------------------------------
+ * gi_obj_parse: Wavefront OBJ text (len bytes, need not be terminated) -> GI_IMP_TRIANGLE
+ * descriptors, one per triangle of each face's fan (v0, v_k, v_k+1) in file order, args = the three
+ * vertices.  Each descriptor is a copy of *tmpl (its material fields; NULL: zeroed, i.e. the
+ * reference's default ImpTriangle material) with kind and args set.  Accepts v (extra values
+ * ignored), f with i, i/t, i//n, i/t/n references (1-based, negative = relative), comments and
+ * '\' continuations; vt, vn, vp, o, g, s, usemtl, mtllib, l, p are skipped.  min(*n, cap)
+ * descriptors are written to out, *n = the full count (call with cap = 0 to size the buffer).
+ * GI_ERR_ARG with the line number on a malformed v / f line or a vertex reference out of range. */
+int gi_obj_parse(const char* text, int64_t len, const gi_entity_desc* tmpl, gi_entity_desc* out, int64_t cap,
+                 int64_t* n);
 
 /* Known-answer hook: the device's ExpBox node test (entities.h:379-440 as octree.h:141-146 uses
  * it) over n host records (min[3], max[3], origin[3], dir[3]); out[i] = 0/1. */

@@ -6,16 +6,21 @@
 // (gui.h:19,35).  Writes the RGB888 frame the Viewer would paint.
 // With "zoo" it builds the every-entity scene of scenes.zoo_scene() instead (entities.h's eight
 // entity classes, constructed by the reference's own constructors).
+// With "obj:<path>" it pushes the Wavefront OBJ mesh at <path> instead, through
+// gi_dropin/obj.h's push_obj (one ImpTriangle per fan triangle, white Material(color)).
 // With a 5th argument "cands" it writes, instead of a frame, the length of the drop-in
 // Octree::intersect(const Ray&) candidate list (octree.h:46-68) for every pixel's primary ray
 // (raytracer.h:26-30, 41-43), as int32 -- compared with the compiled reference's lists.
-//   dropin_demo <w> <h> <out> [zoo|main] [cands]
+//   dropin_demo <w> <h> <out> [zoo|main|obj:<path>] [cands]
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <fstream>
+#include <sstream>
 #include <string>
 
 #include "raytracer.h"   // resolves to include/gi_dropin/raytracer.h (first on the include path)
+#include "obj.h"
 
 int main(int argc, char** argv) {
     if (argc < 4) { std::fprintf(stderr, "usage: dropin_demo w h out.rgb\n"); return 2; }
@@ -24,7 +29,16 @@ int main(int argc, char** argv) {
     glm::dvec3 light{-10, 10, 10};
     RayTracer raytracer(camera, light);
     Octree scene({-20, -20, -20}, {20, 20, 20});
-    if (argc > 4 && std::string(argv[4]) == "zoo") {
+    std::vector<std::unique_ptr<Entity>> mesh;   // push_obj's entities, alive as long as the scene
+    if (argc > 4 && std::string(argv[4]).rfind("obj:", 0) == 0) {
+        std::ifstream in(std::string(argv[4]).substr(4), std::ios::binary);
+        std::stringstream text;
+        text << in.rdbuf();
+        const Material white(glm::dvec3{1, 1, 1});
+        bool ok = false;
+        mesh = gi_dropin::push_obj(scene, text.str(), &white, &ok);
+        if (!in || !ok) return 1;
+    } else if (argc > 4 && std::string(argv[4]) == "zoo") {
         scene.push_back(new ExpSphere(glm::dvec3{-2, 0, 0}, 2, {0, 1, 0}));
         scene.push_back(new ExpCube(glm::dvec3{0, 0, 0}, 2, 2, 2, {1, 0, 0}));
         scene.push_back(new ExpCone(glm::dvec3{0, 0, 2}, glm::dvec3{-1, 1, -3}, 5, 3, {1, 1, 0}));
