@@ -960,6 +960,14 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 #ifndef GI_X_HELP
 #define GI_X_HELP 1   // HBM-resident scenes: shadow rays handed to idle lanes of the wave (XHelp)
 #endif
+#ifndef GI_X_LEAFQ
+// quantised-node scenes, long launches: leaf tests postponed into leaf phases (LQ, mode_x_wave):
+// C5 245 -> 229 ms; the 1k soup (XWNode) +4% and C4 (short launches) +7% keep the plain step
+#define GI_X_LEAFQ 1
+#endif
+#ifndef GI_X_LEAF8
+#define GI_X_LEAF8 3   // LQ: leaf phase once 3/8 of the traversing lanes hold a leaf (C5 sweep 1-8)
+#endif
 #ifndef GI_X_CLIMB_CLZ
 #define GI_X_CLIMB_CLZ 1   // NST climb: the target level by a leading-zero count (C5 -2%), not a loop
 #endif
@@ -1037,8 +1045,8 @@ __device__ __forceinline__ int nth_set_bit(unsigned long long m, unsigned n) {
 // NST: the wide-node index of every level of the current traversal path lives in LDS (nst[level *
 // 256], one column per lane), so climbing out of exhausted levels is one ds_read instead of a chain
 // of dependent parent-pointer loads from HBM / L2 (one per level climbed).
-template <bool STATS, bool PAIR, bool PSL, bool NST, bool HELP, bool SH, typename NodeP, typename HotP, typename PrimP,
-          typename EntP>
+template <bool STATS, bool PAIR, bool PSL, bool NST, bool HELP, bool SH, bool LQ, typename NodeP, typename HotP,
+          typename PrimP, typename EntP>
 __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H, PrimP XP, EntP EN, double* pslot,
                                             int* nst, XHelp hp_,
                                             const CamDev& cam, V3 light,
@@ -1094,6 +1102,9 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     V3 o = cam.pos, d = v3(1, 0, 0);
     int dmask = 0, best = -1, node = 0, level = 0;
     bool raying = false;
+    int poff = 0, pcnt = 0;   // LQ: the pending leaf (records H[poff .. poff + pcnt)), pcnt 0: none
+    bool pdone = false;       // LQ: the ray ends once its pending leaf is tested
+    const int leaf8 = ((xflags >> 12) & 15) ? ((xflags >> 12) & 15) : GI_X_LEAF8;
     uint64_t mlo = 0, mhi = 0;
     double tbest = INFINITY, tmax = INFINITY;
     float tbest_f = INFINITY;
@@ -1156,12 +1167,79 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
         }
         const uint64_t t0 = STATS ? clock64() : 0;
         if (STATS) ++cnt.path_it;
+        // LQ (leaf postponement): a lane whose step reaches a leaf keeps it pending; the wave then
+        // runs node steps for the other lanes until leaf8 eighths (xflags bits 12-15, GI_X_LEAF8
+        // when 0) of its traversing lanes hold a pending leaf, and tests them in one leaf phase:
+        // node tests and fp64 primitive tests no longer share one divergent step.  Each lane's own
+        // sequence of node and leaf operations is unchanged (it pops nothing while a leaf is
+        // pending), so results and work counters are the same.
+        bool leaf_phase = false;
+        if constexpr (LQ) {
+            const unsigned long long m_pl = __ballot(trav && pcnt > 0);
+            leaf_phase = m_pl != 0 && (m_pl == m_trav || 8 * __popcll(m_pl) >= leaf8 * __popcll(m_trav));
+        }
+        // fp64 primitive tests of one leaf's records (these decide the result)
+        auto test_leaf = [&](const XHot* hp, int cntl) {
+            if constexpr (!PAIR) {   // global records: fetched one ahead of the test
+                XHotR cur = load_hot(hp);
+                for (int j = 0; j < cntl; ++j) {
+                    const XHotR rec = cur;
+                    cur = load_hot(hp + min(j + 1, cntl - 1));
+                    ++nprim;
+                    const double t = x_prim_t(rec.h, o, d, MX_TMIN);
+                    const int pi = rec.h.prim;
+                    if (phase != PH_CLOSEST) {   // shadow ray (own or a helper's)
+                        if (t < tmax) { best = pi; raying = false; break; }   // any hit occludes
+                    } else if (t < tbest || (t == tbest && pi < best)) {
+                        tbest = t;
+                        best = pi;
+                        tbest_f = up32(t);
+                    }
+                }
+            } else {
+                // LDS records: tested two at a time, the two fp64 dependency chains interleave
+                for (int j = 0; j < cntl; j += 2) {
+                    const bool two = j + 1 < cntl;
+                    const XHotR r0 = load_hot(hp + j), r1 = load_hot(hp + (two ? j + 1 : j));
+                    const double ta = x_prim_t(r0.h, o, d, MX_TMIN);
+                    const double tb = two ? x_prim_t(r1.h, o, d, MX_TMIN) : INFINITY;
+                    nprim += two ? 2 : 1;
+                    if (phase != PH_CLOSEST) {
+                        if (ta < tmax || tb < tmax) {   // any hit occludes
+                            best = ta < tmax ? r0.h.prim : r1.h.prim;
+                            raying = false;
+                            break;
+                        }
+                    } else {
+                        if (ta < tbest || (ta == tbest && r0.h.prim < best)) {
+                            tbest = ta;
+                            best = r0.h.prim;
+                        }
+                        if (tb < tbest || (tb == tbest && r1.h.prim < best)) {
+                            tbest = tb;
+                            best = r1.h.prim;
+                        }
+                        tbest_f = up32(tbest);
+                    }
+                }
+            }
+        };
         if (trav) {
             // up to GI_X_TRAV_UNROLL steps per loop iteration: the scheduling ballots and the handler
             // decision are paid once per iteration (a lane whose ray ends stops stepping)
 #pragma unroll 1
             for (int u = 0; u < GI_X_TRAV_UNROLL; ++u) {
             if (u > 0 && !raying) break;
+            if (LQ && leaf_phase) {
+                if (pcnt > 0) {
+                    test_leaf(H + poff, pcnt);
+                    pcnt = 0;
+                    if (pdone) {   // the step that popped this leaf exhausted the ray's last level
+                        pdone = false;
+                        raying = false;
+                    }
+                }
+            } else if (!LQ || pcnt == 0) {
             if (STATS) {
                 ++nsteps;
                 ++cnt.path_st;
@@ -1179,53 +1257,13 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             bool keep = true;
             if (phase == PH_CLOSEST && best >= 0) keep = child_hit(nd, c, of, ivf, tbest_f);
             if (keep) {
-                if (ch < 0) {             // leaf: fp64 primitive tests (these decide the result)
-                    const XHot* hp = H + ~ch;
-                    const XBox* bp = sc.xbox + ~ch;
-                    const int cntl = nd->cnt[c];
-                    if constexpr (!PAIR) {   // global records: fetched one ahead of the test
-                        XHotR cur = load_hot(hp);
-                        for (int j = 0; j < cntl; ++j) {
-                            const XHotR rec = cur;
-                            cur = load_hot(hp + min(j + 1, cntl - 1));
-                            ++nprim;
-                            const double t = x_prim_t(rec.h, o, d, MX_TMIN);
-                            const int pi = rec.h.prim;
-                            if (phase != PH_CLOSEST) {   // shadow ray (own or a helper's)
-                                if (t < tmax) { best = pi; raying = false; break; }   // any hit occludes
-                            } else if (t < tbest || (t == tbest && pi < best)) {
-                                tbest = t;
-                                best = pi;
-                                tbest_f = up32(t);
-                            }
-                        }
-                    } else
-                    // LDS records: tested two at a time, the two fp64 dependency chains interleave
-                    for (int j = 0; j < cntl; j += 2) {
-                        const bool two = j + 1 < cntl;
-                        const XHotR r0 = load_hot(hp + j), r1 = load_hot(hp + (two ? j + 1 : j));
-                        const double ta = x_prim_t(r0.h, o, d, MX_TMIN);
-                        const double tb = two ? x_prim_t(r1.h, o, d, MX_TMIN) : INFINITY;
-                        nprim += two ? 2 : 1;
-                        if (phase != PH_CLOSEST) {
-                            if (ta < tmax || tb < tmax) {   // any hit occludes
-                                best = ta < tmax ? r0.h.prim : r1.h.prim;
-                                raying = false;
-                                break;
-                            }
-                        } else {
-                            if (ta < tbest || (ta == tbest && r0.h.prim < best)) {
-                                tbest = ta;
-                                best = r0.h.prim;
-                            }
-                            if (tb < tbest || (tb == tbest && r1.h.prim < best)) {
-                                tbest = tb;
-                                best = r1.h.prim;
-                            }
-                            tbest_f = up32(tbest);
-                        }
+                if (ch < 0) {             // leaf
+                    if constexpr (LQ) {
+                        poff = ~ch;
+                        pcnt = nd->cnt[c];
+                    } else {
+                        test_leaf(H + ~ch, nd->cnt[c]);
                     }
-                    (void)bp;
                 } else {                  // descend if any of the child's 8 children is hit (fp32)
                     ++nnode;
                     const uint32_t cm = children_mask<PAIR>(W + ch, of, ivf, tbest_f, dmask);
@@ -1262,7 +1300,11 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                         rest = lvl_get<SH>(mlo, mhi, level);
                     }
                 }
-                if (rest == 0) raying = false;   // ray finished
+                if (rest == 0) {          // ray finished (after its pending leaf, if any)
+                    if (LQ && pcnt > 0) pdone = true;
+                    else raying = false;
+                }
+            }
             }
             // a finished shadow ray whose path continues: resolve it and start the next bounce
             // right here (the bounce direction was drawn when the hit was shaded), so the lane
@@ -1640,7 +1682,7 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
         // (occluded sum, next direction, throughput T, RNG key) live in a per-lane LDS slot after
         // the scene instead of in VGPRs / scratch
         double* pslot = reinterpret_cast<double*>(lds_scene + nw + nh + np + ne) + 10 * threadIdx.x;
-        mode_x_wave<STATS, GI_X_PAIR != 0, W4 && GI_X_PSL, false, false, SH>(sc, W, H, XP, EN, pslot, nullptr, XHelp{},
+        mode_x_wave<STATS, GI_X_PAIR != 0, W4 && GI_X_PSL, false, false, SH, false>(sc, W, H, XP, EN, pslot, nullptr, XHelp{},
                                                                         cam, light, m, spp, depth, seed, rgb, rgb8, blk,
                                                                         wk, handle8, xflags, c);
     } else {
@@ -1651,13 +1693,14 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
         hp.ray = reinterpret_cast<double*>(lds_nst + (GI_X_NSTK ? 16 * 256 : 0));
         hp.own = reinterpret_cast<int*>(hp.ray + 7 * 256);
         hp.res = hp.own + 256;
-        if constexpr (CN)   // quantised nodes (the default for HBM-resident scenes)
-            mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0, SH>(sc, sc.xcnodes, sc.xhot, sc.xprims,
+        if constexpr (CN)   // quantised nodes (the default for large HBM-resident scenes); LQ in
+                            // long launches (the handoff build's short launches are latency-bound)
+            mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0, SH, GI_X_LEAFQ != 0 && !W4>(sc, sc.xcnodes, sc.xhot, sc.xprims,
                                                                             sc.ents, nullptr, lds_nst + threadIdx.x, hp,
                                                                             cam, light, m, spp, depth, seed, rgb, rgb8,
                                                                             blk, wk, handle8, xflags, c);
         else
-            mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0, SH>(sc, sc.xwnodes, sc.xhot, sc.xprims,
+            mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0, SH, false>(sc, sc.xwnodes, sc.xhot, sc.xprims,
                                                                             sc.ents, nullptr, lds_nst + threadIdx.x, hp,
                                                                             cam, light, m, spp, depth, seed, rgb, rgb8,
                                                                             blk, wk, handle8, xflags, c);
@@ -1823,7 +1866,7 @@ long long shard_tiles(int w, int h, int shard_count) { return make_map(w, h, sha
 // overrides the shading-handler threshold, GI_X_FLAGS the schedule flags, GI_X_MAX_RUN the largest
 // work-unit run length (scenes of cheap background samples such as the main.cpp scene prefer 8).
 struct XEnv {
-    int lds = 1, h8 = 0, xf = -1, run_log2 = 0, help = 1, spread = -1, r_split = -1;
+    int lds = 1, h8 = 0, xf = -1, run_log2 = 0, help = 1, spread = -1, r_split = -1, leaf8 = 0;
 };
 const XEnv& x_env() {
     static XEnv env;
@@ -1835,6 +1878,7 @@ const XEnv& x_env() {
         if (const char* v = std::getenv("GI_X_HELP")) env.help = std::atoi(v) != 0;
         if (const char* v = std::getenv("GI_X_SPREAD")) env.spread = std::atoi(v);
         if (const char* v = std::getenv("GI_R_SPLIT")) env.r_split = std::atoi(v);
+        if (const char* v = std::getenv("GI_X_LEAF8")) env.leaf8 = std::max(0, std::min(8, std::atoi(v)));
         const char* v = std::getenv("GI_X_MAX_RUN");
         const int r = v ? std::max(1, std::min(128, std::atoi(v))) : GI_X_MAX_RUN;
         int lg = 0;
@@ -1937,7 +1981,7 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
         // length (log2, bits 8-10)
         const int xf = (env.xf >= 0 ? env.xf : sc.x_flags) | (env.run_log2 << 8) |
                        ((o.flags & GI_FLAG_X_NO_SHADOW) ? 4 : 0) | (env.help ? 8 : 0) |
-                       ((env.spread > 0 || (env.spread < 0 && help)) ? 16 : 0);
+                       ((env.spread > 0 || (env.spread < 0 && help)) ? 16 : 0) | (env.leaf8 << 12);
         const bool cn = kv < 2 && sc.xcnodes != nullptr;
 #define GI_LAUNCH_X1(S, L, W, SH) hipLaunchKernelGGL((k_mode_x<S, L, W, false, SH>), pgrid, block, lds_bytes, stream, sc, cam, light, m, o.spp, \
                                            o.depth, o.seed, rgb, rgb8, st, wk, h8, xf)
