@@ -1178,52 +1178,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             const unsigned long long m_pl = __ballot(trav && pcnt > 0);
             leaf_phase = m_pl != 0 && (m_pl == m_trav || 8 * __popcll(m_pl) >= leaf8 * __popcll(m_trav));
         }
-        // fp64 primitive tests of one leaf's records (these decide the result)
-        auto test_leaf = [&](const XHot* hp, int cntl) {
-            if constexpr (!PAIR) {   // global records: fetched one ahead of the test
-                XHotR cur = load_hot(hp);
-                for (int j = 0; j < cntl; ++j) {
-                    const XHotR rec = cur;
-                    cur = load_hot(hp + min(j + 1, cntl - 1));
-                    ++nprim;
-                    const double t = x_prim_t(rec.h, o, d, MX_TMIN);
-                    const int pi = rec.h.prim;
-                    if (phase != PH_CLOSEST) {   // shadow ray (own or a helper's)
-                        if (t < tmax) { best = pi; raying = false; break; }   // any hit occludes
-                    } else if (t < tbest || (t == tbest && pi < best)) {
-                        tbest = t;
-                        best = pi;
-                        tbest_f = up32(t);
-                    }
-                }
-            } else {
-                // LDS records: tested two at a time, the two fp64 dependency chains interleave
-                for (int j = 0; j < cntl; j += 2) {
-                    const bool two = j + 1 < cntl;
-                    const XHotR r0 = load_hot(hp + j), r1 = load_hot(hp + (two ? j + 1 : j));
-                    const double ta = x_prim_t(r0.h, o, d, MX_TMIN);
-                    const double tb = two ? x_prim_t(r1.h, o, d, MX_TMIN) : INFINITY;
-                    nprim += two ? 2 : 1;
-                    if (phase != PH_CLOSEST) {
-                        if (ta < tmax || tb < tmax) {   // any hit occludes
-                            best = ta < tmax ? r0.h.prim : r1.h.prim;
-                            raying = false;
-                            break;
-                        }
-                    } else {
-                        if (ta < tbest || (ta == tbest && r0.h.prim < best)) {
-                            tbest = ta;
-                            best = r0.h.prim;
-                        }
-                        if (tb < tbest || (tb == tbest && r1.h.prim < best)) {
-                            tbest = tb;
-                            best = r1.h.prim;
-                        }
-                        tbest_f = up32(tbest);
-                    }
-                }
-            }
-        };
+        static_assert(!(LQ && PAIR), "leaf postponement is built for global (HBM) leaf records");
         if (trav) {
             // up to GI_X_TRAV_UNROLL steps per loop iteration: the scheduling ballots and the handler
             // decision are paid once per iteration (a lane whose ray ends stops stepping)
@@ -1231,8 +1186,23 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             for (int u = 0; u < GI_X_TRAV_UNROLL; ++u) {
             if (u > 0 && !raying) break;
             if (LQ && leaf_phase) {
-                if (pcnt > 0) {
-                    test_leaf(H + poff, pcnt);
+                if (pcnt > 0) {   // the pending leaf's fp64 primitive tests, records fetched one ahead
+                    const XHot* hp = H + poff;
+                    XHotR cur = load_hot(hp);
+                    for (int j = 0; j < pcnt; ++j) {
+                        const XHotR rec = cur;
+                        cur = load_hot(hp + min(j + 1, pcnt - 1));
+                        ++nprim;
+                        const double t = x_prim_t(rec.h, o, d, MX_TMIN);
+                        const int pi = rec.h.prim;
+                        if (phase != PH_CLOSEST) {   // shadow ray (own or a helper's)
+                            if (t < tmax) { best = pi; raying = false; break; }   // any hit occludes
+                        } else if (t < tbest || (t == tbest && pi < best)) {
+                            tbest = t;
+                            best = pi;
+                            tbest_f = up32(t);
+                        }
+                    }
                     pcnt = 0;
                     if (pdone) {   // the step that popped this leaf exhausted the ray's last level
                         pdone = false;
@@ -1257,12 +1227,53 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             bool keep = true;
             if (phase == PH_CLOSEST && best >= 0) keep = child_hit(nd, c, of, ivf, tbest_f);
             if (keep) {
-                if (ch < 0) {             // leaf
-                    if constexpr (LQ) {
-                        poff = ~ch;
-                        pcnt = nd->cnt[c];
-                    } else {
-                        test_leaf(H + ~ch, nd->cnt[c]);
+                if (LQ && ch < 0) {       // leaf: pending until the wave's next leaf phase
+                    poff = ~ch;
+                    pcnt = nd->cnt[c];
+                } else if (ch < 0) {      // leaf: fp64 primitive tests (these decide the result)
+                    const XHot* hp = H + ~ch;
+                    const int cntl = nd->cnt[c];
+                    if constexpr (!PAIR) {   // global records: fetched one ahead of the test
+                        XHotR cur = load_hot(hp);
+                        for (int j = 0; j < cntl; ++j) {
+                            const XHotR rec = cur;
+                            cur = load_hot(hp + min(j + 1, cntl - 1));
+                            ++nprim;
+                            const double t = x_prim_t(rec.h, o, d, MX_TMIN);
+                            const int pi = rec.h.prim;
+                            if (phase != PH_CLOSEST) {   // shadow ray (own or a helper's)
+                                if (t < tmax) { best = pi; raying = false; break; }   // any hit occludes
+                            } else if (t < tbest || (t == tbest && pi < best)) {
+                                tbest = t;
+                                best = pi;
+                                tbest_f = up32(t);
+                            }
+                        }
+                    } else
+                    // LDS records: tested two at a time, the two fp64 dependency chains interleave
+                    for (int j = 0; j < cntl; j += 2) {
+                        const bool two = j + 1 < cntl;
+                        const XHotR r0 = load_hot(hp + j), r1 = load_hot(hp + (two ? j + 1 : j));
+                        const double ta = x_prim_t(r0.h, o, d, MX_TMIN);
+                        const double tb = two ? x_prim_t(r1.h, o, d, MX_TMIN) : INFINITY;
+                        nprim += two ? 2 : 1;
+                        if (phase != PH_CLOSEST) {
+                            if (ta < tmax || tb < tmax) {   // any hit occludes
+                                best = ta < tmax ? r0.h.prim : r1.h.prim;
+                                raying = false;
+                                break;
+                            }
+                        } else {
+                            if (ta < tbest || (ta == tbest && r0.h.prim < best)) {
+                                tbest = ta;
+                                best = r0.h.prim;
+                            }
+                            if (tb < tbest || (tb == tbest && r1.h.prim < best)) {
+                                tbest = tb;
+                                best = r1.h.prim;
+                            }
+                            tbest_f = up32(tbest);
+                        }
                     }
                 } else {                  // descend if any of the child's 8 children is hit (fp32)
                     ++nnode;
