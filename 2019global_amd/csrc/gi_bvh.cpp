@@ -55,7 +55,12 @@ struct Builder {
     std::vector<BNode> nodes;
     int leaf_max = 4;
     static constexpr int kBins = 32;
-    double kTraverse = 1.0;   // SAH cost of a node visit relative to one primitive test
+    // SAH cost of a (binary) node visit relative to one primitive test.  Measured on the 100k soup
+    // (GI_XSAH_CT sweep, profiles/r02_s4_sah.txt): 0.35 against 1.0 gives C4 2.10 -> 1.93 ms and C5
+    // 231 -> 218 ms (smaller leaves: fewer fp64 record tests per ray, the 8-wide collapse absorbs
+    // the extra binary levels); 2 and 4 are 15-20% slower; the Cornell box and the 1k soup are
+    // unchanged within noise.
+    double kTraverse = 0.35;
 
     int build(int first, int count, int depth) {
         const int ni = (int)nodes.size();
