@@ -54,7 +54,8 @@ struct Builder {
     std::vector<double> cen;   // 3 per primitive
     std::vector<BNode> nodes;
     int leaf_max = 4;
-    static constexpr int kBins = 32;
+    static constexpr int kMaxBins = 128;
+    int kBins = 32;   // SAH bins per axis (GI_XSAH_BINS, <= kMaxBins)
     // SAH cost of a (binary) node visit relative to one primitive test.  Measured on the 100k soup
     // (GI_XSAH_CT sweep, profiles/r02_s4_sah.txt): 0.35 against 1.0 gives C4 2.10 -> 1.93 ms and C5
     // 231 -> 218 ms (smaller leaves: fewer fp64 record tests per ray, the 8-wide collapse absorbs
@@ -83,8 +84,8 @@ struct Builder {
         for (int k = 0; k < 3; ++k) {
             const double lo = cb.mn[k], ext = cb.mx[k] - cb.mn[k];
             if (!(ext > 0)) continue;
-            BBox bb[kBins];
-            int bn[kBins] = {0};
+            BBox bb[kMaxBins];
+            int bn[kMaxBins] = {0};
             for (auto& b : bb) b.reset();
             const double sc = kBins / ext;
             for (int i = first; i < first + count; ++i) {
@@ -94,8 +95,8 @@ struct Builder {
                 ++bn[bi];
                 bb[bi].grow((*pb)[p]);
             }
-            double ra[kBins];
-            int rn[kBins];
+            double ra[kMaxBins];
+            int rn[kMaxBins];
             BBox acc;
             acc.reset();
             int n = 0;
@@ -188,7 +189,8 @@ void build_xbvh(const std::vector<XPrim>& prims, const std::vector<double>& boun
     Builder b;
     b.pb = &pb;
     b.leaf_max = std::max(1, leaf_max);
-    if (const char* ct = std::getenv("GI_XSAH_CT")) b.kTraverse = std::atof(ct);   // tuning knob
+    if (const char* ct = std::getenv("GI_XSAH_CT")) b.kTraverse = std::atof(ct);   // tuning knobs
+    if (const char* nb = std::getenv("GI_XSAH_BINS")) b.kBins = std::max(2, std::min(Builder::kMaxBins, std::atoi(nb)));
     b.order.resize(np);
     b.cen.resize(3 * np);
     for (size_t i = 0; i < np; ++i) {
