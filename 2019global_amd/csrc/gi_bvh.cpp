@@ -7,9 +7,9 @@
 //   2. collapse to 8-wide: a wide node takes its binary node's children and repeatedly opens the
 //      interior child of largest surface area until it has 8 children (Wald et al. 2008);
 //   3. child slots ordered so that visiting slot k ^ octant(ray) for k = 0..7 is approximately
-//      front to back for every ray octant (greedy form of the slot assignment of Ylitie, Karras &
-//      Laine 2017): child i goes to the slot s whose octant direction best matches the offset of
-//      its centroid from the parent's;
+//      front to back for every ray octant (the slot assignment of Ylitie, Karras & Laine 2017):
+//      the assignment of children to slots that minimises the summed cost -(octant direction of
+//      the slot . offset of the child's centroid from the parent's), by a DP over slot subsets;
 //   4. each primitive appears in exactly one leaf; a leaf's records (XHot) are contiguous.
 // The fp32 child boxes are rounded outward and padded, so culling is conservative and the fp64
 // primitive tests alone decide hits (bit-exact with the oracle's brute force).
@@ -232,6 +232,10 @@ void build_xbvh(const std::vector<XPrim>& prims, const std::vector<double>& boun
         gather(bn.right, out);
     };
 
+    // child-to-slot assignment of minimum total cost (C3 kernel -1%, the soups unchanged,
+    // profiles/r02_s4_sah.txt); GI_XSLOT=0 (tuning knob) restores the greedy assignment
+    const char* xs = std::getenv("GI_XSLOT");
+    const bool exact_slots = !(xs && std::atoi(xs) == 0);
     // fill wide node `wi` (depth `wd`) from binary node `bn`'s subtree
     std::function<void(int, int, int)> fill = [&](int wi, int bn, int wd) {
         hs.x_max_depth = std::max(hs.x_max_depth, wd);
@@ -269,7 +273,33 @@ void build_xbvh(const std::vector<XPrim>& prims, const std::vector<double>& boun
             }
         int slot_of[8];
         bool used_kid[8] = {false}, used_slot[8] = {false};
-        for (int it = 0; it < nk; ++it) {
+        if (exact_slots) {   // minimum-cost assignment: DP over the set of slots taken by kids 0..i-1
+            double dp[256];
+            int8_t pick[9][256];
+            for (int m = 0; m < 256; ++m) dp[m] = INFINITY;
+            dp[0] = 0.0;
+            for (int i = 0; i < nk; ++i) {
+                double nd[256];
+                for (int m = 0; m < 256; ++m) nd[m] = INFINITY;
+                for (int m = 0; m < 256; ++m) {
+                    if (dp[m] == INFINITY || __builtin_popcount(m) != i) continue;
+                    for (int sl = 0; sl < 8; ++sl) {
+                        if (m & (1 << sl)) continue;
+                        const double c = dp[m] + cost[i][sl];
+                        if (c < nd[m | (1 << sl)]) { nd[m | (1 << sl)] = c; pick[i][m | (1 << sl)] = (int8_t)sl; }
+                    }
+                }
+                for (int m = 0; m < 256; ++m) dp[m] = nd[m];
+            }
+            int bm = -1;
+            for (int m = 0; m < 256; ++m)
+                if (__builtin_popcount(m) == nk && dp[m] < INFINITY && (bm < 0 || dp[m] < dp[bm])) bm = m;
+            for (int i = nk - 1; i >= 0; --i) {
+                slot_of[i] = pick[i][bm];
+                bm &= ~(1 << slot_of[i]);
+            }
+        }
+        for (int it = 0; it < nk && !exact_slots; ++it) {
             int bi = -1, bs = -1;
             double bc = INFINITY;
             for (int i = 0; i < nk; ++i) {
