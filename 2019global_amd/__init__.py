@@ -53,7 +53,7 @@ STAT_X_CYC_TRAV, STAT_X_CYC_HIT, STAT_X_CYC_NEXT, STAT_X_CYC_ALL = 11, 12, 13, 1
 STAT_X_RESOLVED = 15
 STATS_N = 16
 TILE = 8
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 
 class GIError(RuntimeError):
@@ -103,7 +103,7 @@ EXPORTS = ["gi_abi_version", "gi_last_error", "gi_camera_init", "gi_scene_create
            "gi_scene_get_info", "gi_render", "gi_render_device", "gi_shard_tiles", "gi_unshard_device",
            "gi_trace_ray", "gi_kat_expbox", "gi_scene_kernel_ms", "gi_octree_create", "gi_octree_destroy",
            "gi_octree_intersect", "gi_multi_create", "gi_multi_destroy", "gi_multi_info", "gi_multi_render", "gi_device_count",
-           "gi_obj_parse"]
+           "gi_device_list", "gi_build_id", "gi_obj_parse"]
 
 _lib = None
 _lock = threading.Lock()
@@ -152,12 +152,19 @@ def lib():
                                     ctypes.POINTER(ctypes.c_int)]
         L.gi_multi_render.argtypes = [vp, ctypes.POINTER(CameraDesc), dp, i32, i32, ctypes.POINTER(Opts), dp,
                                       ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_int), TILE_CB, vp]
+        L.gi_device_list.argtypes = [ctypes.POINTER(ctypes.c_int32), i32]
+        L.gi_build_id.restype = ctypes.c_char_p
         L.gi_obj_parse.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.POINTER(EntityDesc),
                                    ctypes.POINTER(EntityDesc), ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
         if L.gi_abi_version() != ABI_VERSION:
             raise GIError(f"libgi ABI {L.gi_abi_version()} != {ABI_VERSION}")
         _lib = L
         return L
+
+
+def build_id() -> str:
+    """Source hash the loaded libgi was compiled from (build.py source_hash)."""
+    return lib().gi_build_id().decode()
 
 
 def _check(rc: int, what: str) -> None:

@@ -7,6 +7,7 @@ no FMA) never contracts a*b+c.  Run ``python -m 2019global_amd.build`` or ``__gr
 from __future__ import annotations
 
 import glob
+import hashlib
 import os
 import shutil
 import subprocess
@@ -25,6 +26,17 @@ DEV_SRCS = ["gi_kernels.hip"]
 HEADERS = ["gi_math.h", "gi_scene.h", "gi_internal.h"]
 
 COMMON = ["-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", f"-I{INCLUDE}", f"-I{CSRC}"]
+
+
+def source_hash() -> str:
+    """Provenance id of a build: sha256 (first 16 hex digits) over every source and header the
+    library is compiled from.  Compiled into libgi as gi_build_id(); tests compare the loaded
+    library's id with this hash of the tree, so a stale .so cannot pass unnoticed."""
+    h = hashlib.sha256()
+    for name in sorted(HOST_SRCS + DEV_SRCS + HEADERS):
+        h.update(name.encode() + b"\0" + open(os.path.join(CSRC, name), "rb").read() + b"\0")
+    h.update(b"gi.h\0" + open(os.path.join(INCLUDE, "gi.h"), "rb").read())
+    return h.hexdigest()[:16]
 
 
 def _run(cmd, verbose):
@@ -51,12 +63,20 @@ def build(verbose: bool = False, force: bool = False, variant: str = "", hip_def
         os.makedirs(os.path.dirname(out), exist_ok=True)
     os.makedirs(objdir, exist_ok=True)
     hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "gi.h")]
+    # the build id goes into gi_capi.o: recompiled whenever any source changed since its last build
+    bid = source_hash()
+    bid_file = os.path.join(objdir, "build_id")
+    old_bid = open(bid_file).read().strip() if os.path.exists(bid_file) else ""
     objs = []
     for s in HOST_SRCS:
         src, obj = os.path.join(CSRC, s), os.path.join(objdir, s + ".o")
-        if force or _stale(obj, [src] + hdrs):
-            _run(["g++", "-O2", *COMMON, "-D__HIP_PLATFORM_AMD__", f"-I{ROCM}/include", "-c", src, "-o", obj], verbose)
+        defs = [f'-DGI_BUILD_ID="{bid}"'] if s == "gi_capi.cpp" else []
+        if force or _stale(obj, [src] + hdrs) or (defs and old_bid != bid):
+            _run(["g++", "-O2", *COMMON, *defs, "-D__HIP_PLATFORM_AMD__", f"-I{ROCM}/include", "-c", src, "-o", obj],
+                 verbose)
         objs.append(obj)
+    with open(bid_file, "w") as f:
+        f.write(bid + "\n")
     for s in DEV_SRCS:
         src = os.path.join(CSRC, s)
         obj = os.path.join(objdir, s + (f".{variant}" if variant else "") + ".o")

@@ -423,15 +423,25 @@ extern "C" {
 int gi_abi_version(void) { return GI_ABI_VERSION; }
 const char* gi_last_error(void) { return g_err.c_str(); }
 
-int gi_device_count(void) {
+int gi_device_list(int32_t* out, int cap) {
     int ndev = 0, n = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess) return 0;
     for (int d = 0; d < ndev; ++d) {
         hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, d) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) == 0) ++n;
+        if (hipGetDeviceProperties(&prop, d) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) == 0) {
+            if (out && n < cap) out[n] = d;
+            ++n;
+        }
     }
     return n;
 }
+
+int gi_device_count(void) { return gi_device_list(nullptr, 0); }
+
+#ifndef GI_BUILD_ID
+#define GI_BUILD_ID "unknown"
+#endif
+const char* gi_build_id(void) { return GI_BUILD_ID; }
 
 int gi_camera_init(const double pos[3], const double look_at[3], double focal, gi_camera* out) {
     if (!pos || !look_at || !out) return fail(GI_ERR_ARG, "null argument");
@@ -485,6 +495,7 @@ int64_t gi_shard_tiles(int w, int h, int shard_count) {
 int gi_render_device(gi_scene* s, const gi_camera* cam, const double light[3], int w, int h, const gi_opts* o,
                      double* d_rgb, uint8_t* d_rgb8, void* stream) {
     return guard([&]() -> int {
+        DeviceRestore keep;   // the caller's current device, restored on return
         if (!s) return fail(GI_ERR_ARG, "null scene");
         int rc = check_opts(w, h, o);
         if (rc) return rc;
@@ -498,6 +509,7 @@ int gi_render_device(gi_scene* s, const gi_camera* cam, const double light[3], i
 int gi_render(gi_scene* s, const gi_camera* cam, const double light[3], int w, int h, const gi_opts* o, double* rgb,
               uint8_t* rgb8, const volatile int* cancel, gi_tile_cb cb, void* user) {
     return guard([&]() -> int {
+        DeviceRestore keep;   // the caller's current device, restored on return
         if (!s) return fail(GI_ERR_ARG, "null scene");
         int rc = check_opts(w, h, o);
         if (rc) return rc;
@@ -563,6 +575,7 @@ int gi_render(gi_scene* s, const gi_camera* cam, const double light[3], int w, i
 
 int gi_scene_kernel_ms(gi_scene* s, float* avg_ms, int64_t* n) {
     return guard([&]() -> int {
+        DeviceRestore keep;   // the caller's current device, restored on return
         if (!s || !avg_ms) return fail(GI_ERR_ARG, "null argument");
         std::lock_guard<std::mutex> lk(s->mu);
         KTimer& kt = s->kt;
@@ -596,6 +609,7 @@ int gi_unshard_device(int w, int h, int shard_count, const double* d_packed, con
 int gi_trace_ray(gi_scene* s, const double origin[3], const double dir[3], const double light[3], gi_hit* hit,
                  double rgb[3]) {
     return guard([&]() -> int {
+        DeviceRestore keep;   // the caller's current device, restored on return
         if (!s || !origin || !dir || !light || !hit || !rgb) return fail(GI_ERR_ARG, "null argument");
         std::lock_guard<std::mutex> lk(s->mu);
         int rc = bind_device(s->device);

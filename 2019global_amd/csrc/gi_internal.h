@@ -37,6 +37,21 @@ int scene_render_band(gi_scene* s, const CamDev& cd, const double light[3], int 
 int unshard(int w, int h, int n, const double* packed, const uint8_t* packed8, double* rgb, uint8_t* rgb8,
             hipStream_t stream);
 
+// Restores the calling thread's current HIP device on scope exit (entry points that switch devices
+// leave the caller's choice as they found it).
+struct DeviceRestore {
+    int dev = -1;
+    DeviceRestore() {
+        if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+    }
+    ~DeviceRestore() {
+        int cur = -1;
+        if (dev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != dev) (void)hipSetDevice(dev);
+    }
+    DeviceRestore(const DeviceRestore&) = delete;
+    DeviceRestore& operator=(const DeviceRestore&) = delete;
+};
+
 // Runs an entry point's body: no exception leaves the library (gi.h).
 template <typename F>
 int guard(F&& body) noexcept {

@@ -8,10 +8,11 @@
 // references in any of the forms i, i/t, i//n, i/t/n (1-based; negative = relative to the last
 // vertex), fan-triangulated in face order (v0, v_k, v_k+1); `#` comments; blank lines; `\` line
 // continuations.  Ignored (no reference counterpart): vt, vn, vp, o, g, s, usemtl, mtllib, l, p and
-// unknown keywords.  scenes.load_obj restates these rules in Python (tests compare the two).
-#include <cerrno>
+// unknown keywords.  Numbers follow one ASCII grammar (is_real below), parsed independently of the
+// C locale.  scenes.load_obj restates these rules in Python (tests compare the two).
+#include <charconv>
 #include <cmath>
-#include <cstdlib>
+#include <system_error>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -27,23 +28,54 @@ struct Tok {
     size_t n;
 };
 
+// The one number grammar both parsers accept (scenes.load_obj restates it as a regex):
+//   real    [+-]? ( D+ ( '.' D* )? | '.' D+ ) ( [eE] [+-]? D+ )?     D = ASCII 0-9
+//   integer [+-]? D+
+// Hex floats, inf / nan, digit separators and non-ASCII digits are malformed on both sides.
+size_t scan_digits(const char* p, size_t i, size_t n) {
+    while (i < n && p[i] >= '0' && p[i] <= '9') ++i;
+    return i;
+}
+bool is_real(const char* p, size_t n) {
+    size_t i = (n > 0 && (p[0] == '+' || p[0] == '-')) ? 1 : 0;
+    const size_t d0 = i;
+    i = scan_digits(p, i, n);
+    const bool int_part = i > d0;
+    bool frac_part = false;
+    if (i < n && p[i] == '.') {
+        const size_t f0 = ++i;
+        i = scan_digits(p, i, n);
+        frac_part = i > f0;
+    }
+    if (!int_part && !frac_part) return false;
+    if (i < n && (p[i] == 'e' || p[i] == 'E')) {
+        ++i;
+        if (i < n && (p[i] == '+' || p[i] == '-')) ++i;
+        const size_t e0 = i;
+        i = scan_digits(p, i, n);
+        if (i == e0) return false;
+    }
+    return i == n;
+}
+
+// std::from_chars: correctly rounded like Python's float(), and independent of the C locale (the
+// reference host is a Qt app: QApplication calls setlocale(LC_ALL, ""), so strtod would stop at
+// the '.' of "1.5" under a comma-decimal locale such as de_DE)
 bool parse_double(const Tok& t, double& v) {
-    std::string s(t.p, t.n);   // strtod needs a terminated string; correctly rounded, like Python float()
-    char* end = nullptr;
-    errno = 0;
-    v = std::strtod(s.c_str(), &end);
-    return end == s.c_str() + s.size() && !s.empty() && std::isfinite(v);
+    if (!is_real(t.p, t.n)) return false;
+    const char* b = t.p + (t.p[0] == '+' ? 1 : 0);   // from_chars takes no leading '+'
+    const std::from_chars_result r = std::from_chars(b, t.p + t.n, v);
+    return r.ec == std::errc() && r.ptr == t.p + t.n && std::isfinite(v);
 }
 
 bool parse_index(const Tok& t, long long& v) {
     size_t k = 0;
     while (k < t.n && t.p[k] != '/') ++k;   // the vertex index is the part before the first '/'
-    if (k == 0) return false;
-    std::string s(t.p, k);
-    char* end = nullptr;
-    errno = 0;
-    v = std::strtoll(s.c_str(), &end, 10);
-    return end == s.c_str() + s.size() && errno == 0 && v != 0;
+    size_t i = (k > 0 && (t.p[0] == '+' || t.p[0] == '-')) ? 1 : 0;
+    if (scan_digits(t.p, i, k) != k || k == i) return false;
+    const char* b = t.p + (t.p[0] == '+' ? 1 : 0);
+    const std::from_chars_result r = std::from_chars(b, t.p + k, v, 10);
+    return r.ec == std::errc() && r.ptr == t.p + k && v != 0;
 }
 
 }  // namespace

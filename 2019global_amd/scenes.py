@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import hashlib
 import math
+import re
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence, Tuple
 
@@ -171,6 +172,12 @@ def parse_scn(text: str) -> Scene:
     return s
 
 
+# gi_obj.cpp's number grammar (is_real / parse_index), ASCII digits only: float() and int() alone
+# would also take "1_0", "inf", "nan" and non-ASCII digits, which the C parser rejects
+_OBJ_REAL = re.compile(r"[+-]?(?:[0-9]+(?:\.[0-9]*)?|\.[0-9]+)(?:[eE][+-]?[0-9]+)?", re.ASCII)
+_OBJ_INT = re.compile(r"[+-]?[0-9]+", re.ASCII)
+
+
 def load_obj(text: str, material: Optional[Material] = None, scene: Optional[Scene] = None) -> Scene:
     """Wavefront OBJ text -> ImpTriangle entities appended to `scene` (a new Scene if None), one per
     triangle of each face's fan (v0, v_k, v_k+1) in file order, each with `material` (None: the
@@ -205,10 +212,9 @@ def load_obj(text: str, material: Optional[Material] = None, scene: Optional[Sce
         if tok[0] == "v":
             if len(tok) < 4:
                 raise ValueError(f"obj line {lineno}: v needs 3 coordinates")
-            try:
-                xyz = tuple(float(t) for t in tok[1:4])
-            except ValueError:
-                raise ValueError(f"obj line {lineno}: bad coordinate") from None
+            if not all(_OBJ_REAL.fullmatch(t) for t in tok[1:4]):
+                raise ValueError(f"obj line {lineno}: bad coordinate")
+            xyz = tuple(float(t) for t in tok[1:4])
             if not all(math.isfinite(c) for c in xyz):
                 raise ValueError(f"obj line {lineno}: bad coordinate")
             verts.append(xyz)
@@ -218,10 +224,9 @@ def load_obj(text: str, material: Optional[Material] = None, scene: Optional[Sce
             idx = []
             for t in tok[1:]:
                 ref = t.split("/", 1)[0]
-                try:
-                    r = int(ref, 10)
-                except ValueError:
-                    raise ValueError(f"obj line {lineno}: bad vertex reference") from None
+                if not _OBJ_INT.fullmatch(ref):
+                    raise ValueError(f"obj line {lineno}: bad vertex reference")
+                r = int(ref, 10)
                 if r == 0:
                     raise ValueError(f"obj line {lineno}: bad vertex reference")
                 z = r - 1 if r > 0 else len(verts) + r

@@ -25,7 +25,7 @@
  *   gi_multi_*           RayTracer::run over several GPUs of one process: a scene replica per
  *                        device, 8x8 tiles dealt round-robin, RCCL send/recv gather over xGMI to
  *                        the first device (the drop-in RayTracer uses it when GI_DEVICES lists
- *                        more than one device or the node has several)
+ *                        devices; by default it renders on the current device alone)
  *
  * Conventions: all pointers are plain C pointers; buffers are caller-owned; sizes are in elements;
  * every function returns 0 on success and a negative gi_status on error, with a thread-local
@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define GI_ABI_VERSION 7
+#define GI_ABI_VERSION 8
 
 typedef enum gi_status {
     GI_OK = 0,
@@ -177,6 +177,12 @@ int gi_abi_version(void);
 const char* gi_last_error(void);
 /* gfx950 devices visible to this process (0 when there is none). */
 int gi_device_count(void);
+/* Their HIP device indices (a node may mix architectures): min(count, cap) indices written to out
+ * (out may be NULL when cap is 0); returns the count. */
+int gi_device_list(int32_t* out, int cap);
+/* Provenance: a hash of the kernel and host sources this library was compiled from (build.py
+ * passes it at compile time; tests compare it with the sources in the tree). */
+const char* gi_build_id(void);
 
 int gi_camera_init(const double pos[3], const double look_at[3], double focal, gi_camera* out);
 

@@ -6,7 +6,7 @@
 // recorded, and libgi rebuilds the reference octree from it bit for bit (node boxes, lost entities
 // A.6, silent drop A.14) -- on the device for RayTracer::run (gi_scene_create), and on the host
 // for intersect() (gi_octree_create / gi_octree_intersect: DFS over children 0..7 with the ExpBox
-// node test, octree.h:132-155, duplicates kept), rebuilt lazily whenever the scene has changed.
+// node test, octree.h:132-155, duplicates kept), rebuilt lazily after push_back.
 #pragma once
 
 #include <cstddef>
@@ -38,11 +38,15 @@ class Octree {
     /// (octree.h:45-68): the reference's candidate list, in its order, duplicates included.
     std::vector<Entity*> intersect(const Ray& ray) const {
         std::vector<Entity*> out;
-        std::vector<gi_entity_desc> d;
-        if (!gi_dropin::describe_all(_objects, d)) return out;
-        const double mn[3] = {min.x, min.y, min.z}, mx[3] = {max.x, max.y, max.z};
-        const uint64_t h = gi_dropin::scene_hash(d, mn, mx);
-        if (!_host || _host_hash != h) {   // the entities or their materials changed: rebuild
+        // The host tree is rebuilt only when push_back has changed the entity list since the last
+        // query: the candidate list depends on the entities' geometry and push order alone, and an
+        // entity's geometry is fixed by its constructor (entities.h has no setters; materials do
+        // not enter Octree::intersect) -- and on a change of the public root box.  So a query costs the tree walk, not a re-description of the
+        // whole scene (O(N) per ray before).
+        if (!_host || _host_gen != _generation || _host_min != min || _host_max != max) {
+            std::vector<gi_entity_desc> d;
+            if (!gi_dropin::describe_all(_objects, d)) return out;
+            const double mn[3] = {min.x, min.y, min.z}, mx[3] = {max.x, max.y, max.z};
             gi_scene_desc sd = {};
             for (int k = 0; k < 3; ++k) { sd.octree_min[k] = mn[k]; sd.octree_max[k] = mx[k]; }
             sd.n_entities = (int32_t)d.size();
@@ -53,7 +57,9 @@ class Octree {
                 return out;
             }
             _host = std::shared_ptr<gi_octree>(t, gi_octree_destroy);
-            _host_hash = h;
+            _host_gen = _generation;
+            _host_min = min;
+            _host_max = max;
         }
         const double o[3] = {ray.origin.x, ray.origin.y, ray.origin.z}, dir[3] = {ray.dir.x, ray.dir.y, ray.dir.z};
         int64_t n = 0;
@@ -72,5 +78,6 @@ class Octree {
     std::vector<Entity*> _objects;   // non-owning, as the reference (octree.h:158)
     std::size_t _generation = 0;
     mutable std::shared_ptr<gi_octree> _host;   // host copy of the reference tree for intersect()
-    mutable uint64_t _host_hash = 0;
+    mutable std::size_t _host_gen = 0;   // _generation and root box the host tree was built for
+    mutable glm::dvec3 _host_min{0}, _host_max{0};
 };

@@ -11,6 +11,16 @@
 // Put the directory of this header BEFORE the reference's include/ on the include path and link
 // libgi.so.  camera.h, entities.h, image.h, material.h, ray.h, viewer.h, gui.h and
 // main.cpp stay untouched.
+//
+// Opt-ins (the defaults are the reference's behaviour, so an unmodified Viewer gets exactly it):
+//   * the integrator: setIntegrator(GI_MODE_X, spp, depth, seed), or the environment read once at
+//     construction -- GI_MODE=X (or 1), GI_SPP, GI_DEPTH, GI_SEED -- selects the build-defined
+//     depth / spp path tracer (DESIGN.md "Mode X": recursive secondary-ray spawn, jittered samples)
+//     behind the same run(w, h); default GI_MODE_R, 1 spp, depth 1 (raytracer.h:41-84).
+//   * several GPUs: GI_DEVICES="0,1,..." or "all" (every gfx950 of the node) renders each frame's
+//     8x8 tiles across them (gi_multi, RCCL gather).  Unset: one device, the one current on the
+//     thread that uploads the scene (hipSetDevice by the host app is honoured); if the multi-device
+//     handle cannot be created (no librccl, no peer access) the frame falls back to that device.
 #pragma once
 
 #include <algorithm>
@@ -33,7 +43,18 @@ class RayTracer {
   public:
     RayTracer() = delete;
     RayTracer(const Camera& camera, glm::dvec3 light)
-        : _camera(camera), _light(light), _image(std::make_shared<Image>(0, 0)) {}
+        : _camera(camera), _light(light), _image(std::make_shared<Image>(0, 0)), _integ(env_integrator()) {}
+
+    /// Extension (not in the reference): the integrator run() uses.  GI_MODE_R (default) is the
+    /// reference's per-pixel body; GI_MODE_X is the depth / spp path tracer.  Returns false (and
+    /// keeps the current choice) on an invalid combination.
+    bool setIntegrator(int mode, int spp, int depth, uint64_t seed = 0) {
+        if (mode != GI_MODE_R && mode != GI_MODE_X) return false;
+        if (mode == GI_MODE_X && (spp < 1 || depth < 1 || depth > 0xFFFF)) return false;
+        _integ = Integrator{mode, mode == GI_MODE_X ? spp : 1, mode == GI_MODE_X ? depth : 1, seed};
+        return true;
+    }
+    int integratorMode() const { return _integ.mode; }
 
     void setScene(const Octree* scene) {
         _scene = scene;
@@ -62,12 +83,14 @@ class RayTracer {
         cam.focal = _camera.focalDist;
         const double light[3] = {_light.x, _light.y, _light.z};
         gi_opts o = {};
-        o.mode = GI_MODE_R;
-        o.spp = 1;
-        o.depth = 1;
+        o.mode = _integ.mode;
+        o.spp = _integ.spp;
+        o.depth = _integ.depth;
+        o.seed = _integ.seed;
         o.shard_count = 1;
         o.band_rows = 32;
-        Band band{_image.get(), w};
+        Band band{_image.get(), w, _keep_radiance ? &_radiance : nullptr};
+        if (_keep_radiance) _radiance.assign((size_t)w * h * 3, 0.0);
         const int rc = _gpu->multi ? gi_multi_render(_gpu->multi, &cam, light, w, h, &o, nullptr, nullptr, &_cancel,
                                                      &RayTracer::on_band, &band)
                                    : gi_render(_gpu->scene, &cam, light, w, h, &o, nullptr, nullptr, &_cancel,
@@ -81,14 +104,39 @@ class RayTracer {
 
     std::shared_ptr<Image> getImage() const { return _image; }
 
+    /// Extension (tests, tools): keep the last run's fp64 radiance (w*h*3, row-major) beside the
+    /// Image, whose RGB888 is its (int)(255*c) quantisation (image.h:14-16).
+    void keepRadiance(bool on) { _keep_radiance = on; }
+    const std::vector<double>& radiance() const { return _radiance; }
+
   private:
+    struct Integrator {
+        int mode, spp, depth;
+        uint64_t seed;
+    };
     struct Band {
         Image* image;
         int w;
+        std::vector<double>* radiance;
     };
 
-    // the uploaded scene: one device (gi_scene) or several (gi_multi: GI_DEVICES="0,1,..." or
-    // "all"; by default every gfx950 of the node when there is more than one)
+    // GI_MODE / GI_SPP / GI_DEPTH / GI_SEED, read once per process; invalid values keep Mode R
+    static Integrator env_integrator() {
+        static const Integrator v = [] {
+            Integrator r{GI_MODE_R, 1, 1, 0};
+            const char* m = std::getenv("GI_MODE");
+            if (!m || !(std::strcmp(m, "X") == 0 || std::strcmp(m, "x") == 0 || std::strcmp(m, "1") == 0)) return r;
+            const char* sp = std::getenv("GI_SPP");
+            const char* dp = std::getenv("GI_DEPTH");
+            const char* sd = std::getenv("GI_SEED");
+            const long spp = sp ? std::strtol(sp, nullptr, 10) : 1, depth = dp ? std::strtol(dp, nullptr, 10) : 1;
+            if (spp < 1 || depth < 1 || depth > 0xFFFF || spp > (1L << 30)) return r;
+            return Integrator{GI_MODE_X, (int)spp, (int)depth, sd ? (uint64_t)std::strtoull(sd, nullptr, 10) : 0};
+        }();
+        return v;
+    }
+
+    // the uploaded scene: the current device (gi_scene) or the devices GI_DEVICES lists (gi_multi)
     struct Gpu {
         gi_scene* scene = nullptr;
         gi_multi* multi = nullptr;
@@ -106,24 +154,29 @@ class RayTracer {
                 const double* c = rgb + 3 * ((size_t)j * b->w + x);
                 b->image->setPixel(x, y0 + j, glm::dvec3{c[0], c[1], c[2]});
             }
+        if (b->radiance)
+            std::memcpy(b->radiance->data() + (size_t)y0 * b->w * 3, rgb, (size_t)rows * b->w * 3 * sizeof(double));
     }
 
+    // GI_DEVICES: "0,1,..." (those devices) or "all" (every gfx950 of the node, by its device
+    // index); unset or empty: none listed, the frame renders on the current device
     static std::vector<int> devices() {
         std::vector<int> d;
         const char* env = std::getenv("GI_DEVICES");
-        if (env && *env && std::strcmp(env, "all") != 0) {
-            for (const char* p = env; *p;) {
-                char* end = nullptr;
-                const long v = std::strtol(p, &end, 10);
-                if (end == p) break;
-                d.push_back((int)v);
-                p = *end == ',' ? end + 1 : end;
-            }
+        if (!env || !*env) return d;
+        if (std::strcmp(env, "all") == 0) {
+            const int n = gi_device_list(nullptr, 0);
+            d.resize((size_t)std::max(0, n));
+            if (n > 0) gi_device_list(d.data(), n);
             return d;
         }
-        const int n = gi_device_count();
-        if (env || n > 1)
-            for (int i = 0; i < n; ++i) d.push_back(i);
+        for (const char* p = env; *p;) {
+            char* end = nullptr;
+            const long v = std::strtol(p, &end, 10);
+            if (end == p) break;
+            d.push_back((int)v);
+            p = *end == ',' ? end + 1 : end;
+        }
         return d;
     }
 
@@ -141,12 +194,12 @@ class RayTracer {
         sd.entities = ents.data();
         auto g = std::make_shared<Gpu>();
         const std::vector<int> devs = devices();
-        if (devs.size() > 1) {
-            if (gi_multi_create(&sd, (int)devs.size(), devs.data(), &g->multi) != GI_OK) {
-                std::fprintf(stderr, "gi_multi_create: %s\n", gi_last_error());
-                return false;
-            }
-        } else if (gi_scene_create(&sd, &g->scene) != GI_OK) {
+        if (!devs.empty() && gi_multi_create(&sd, (int)devs.size(), devs.data(), &g->multi) != GI_OK) {
+            // e.g. no librccl: the frame still renders, on the current device alone
+            std::fprintf(stderr, "gi_multi_create: %s (rendering on one device)\n", gi_last_error());
+            g->multi = nullptr;
+        }
+        if (!g->multi && gi_scene_create(&sd, &g->scene) != GI_OK) {
             std::fprintf(stderr, "gi_scene_create: %s\n", gi_last_error());
             return false;
         }
@@ -161,4 +214,7 @@ class RayTracer {
     glm::dvec3 _light;
     std::shared_ptr<Image> _image;
     std::shared_ptr<Gpu> _gpu;   // shared by copies (Gui/Viewer copy the RayTracer by value)
+    Integrator _integ;
+    bool _keep_radiance = false;
+    std::vector<double> _radiance;
 };

@@ -42,6 +42,15 @@ def test_library_loads_and_abi_version():
     assert ctypes.sizeof(gi.CameraDesc) == 80
 
 
+def test_loaded_library_built_from_this_tree():
+    """Provenance: gi_build_id() of the libgi this process loaded equals the hash of
+    the sources in the tree (build.py source_hash), so the suite -- here and in `pytest -m gpu` on
+    the GPU box, which loads the same in-tree .so -- runs the kernels these sources define."""
+    from importlib import import_module
+    B = import_module("2019global_amd.build")
+    assert gi.build_id() == B.source_hash()
+
+
 def test_ctypes_layouts_match_header(tmp_path):
     """The Python mirror's structs against include/gi.h as the C compiler lays them out."""
     import subprocess
@@ -150,6 +159,7 @@ def test_error_paths_without_device():
         pytest.skip("GPU present")
     L = gi.lib()
     assert L.gi_device_count() == 0
+    assert L.gi_device_list(None, 0) == 0
     with pytest.raises(gi.GIError, match=r"\(-2\)"):
         gi.MultiScene.from_scene(S.sphere_scene(), [0, 0])
     h = ctypes.c_void_p()

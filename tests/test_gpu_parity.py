@@ -535,6 +535,43 @@ def test_cpp_dropin_raytracer_matches_reference_run(torch_cuda, tmp_path):
     assert (got == z["run_q"]).all()
 
 
+@pytest.mark.parametrize("band_env", [{}, {"GI_DEVICES": "0,0"}])
+def test_cpp_dropin_raytracer_mode_x_opt_in(torch_cuda, tmp_path, band_env):
+    """the north_star integrator through the reference's own boundary.  The
+    reference app's classes build the Cornell box (dropin_demo `scn:`), and the drop-in
+    RayTracer::run -- opted in by GI_MODE=X / GI_SPP / GI_DEPTH / GI_SEED, read once by its
+    constructor -- renders it in Mode X, band by band through Image::setPixel: its fp64 radiance
+    equals the oracle's pixel_mode_x bit for bit and its Image is that radiance's RGB888.  Without the
+    opt-in the same binary renders the reference's Mode R frame (the default is unchanged).  Also
+    over two tile shards (GI_DEVICES=0,0: gi_multi)."""
+    import subprocess
+    exe = os.path.join(U.ROOT, "integration", "_build", "dropin_demo")
+    if not os.path.exists(exe):
+        pytest.skip("integration/_build/dropin_demo not built (needs the reference tree)")
+    sc = S.cornell_scene()
+    scn = tmp_path / "c.scn"
+    scn.write_text(sc.to_scn())
+    w, h, spp, depth, seed = 72, 56, 4, 5, 11
+    env = dict(os.environ, QT_QPA_PLATFORM="offscreen", GI_MODE="X", GI_SPP=str(spp), GI_DEPTH=str(depth),
+               GI_SEED=str(seed), **band_env)
+    out, out8 = tmp_path / "f.f64", tmp_path / "f.rgb"
+    subprocess.run([exe, str(w), str(h), str(out), f"scn:{scn}", "rad"], check=True, env=env, timeout=120)
+    subprocess.run([exe, str(w), str(h), str(out8), f"scn:{scn}"], check=True, env=env, timeout=120)
+    got = np.frombuffer(out.read_bytes(), np.float64).reshape(-1, 3)
+    got8 = np.frombuffer(out8.read_bytes(), np.uint8).reshape(-1, 3)
+    o = U.oracle_render(sc.to_scn(), w, h, mode=1, spp=spp, depth=depth, seed=seed)
+    assert U.bits_equal(got, o["rgb"]).all()
+    assert (got8 == o["q"]).all()
+    assert (got8 != 0).any()
+    # default: the reference's integrator (Mode R) through the same binary
+    env_r = {k: v for k, v in env.items() if k not in ("GI_MODE", "GI_SPP", "GI_DEPTH", "GI_SEED")}
+    subprocess.run([exe, str(w), str(h), str(out), f"scn:{scn}", "rad"], check=True, env=env_r, timeout=120)
+    o_r = U.oracle_render(sc.to_scn(), w, h)
+    got_r = np.frombuffer(out.read_bytes(), np.float64).reshape(-1, 3)
+    err = np.abs(got_r - o_r["rgb"]) / np.maximum(np.abs(o_r["rgb"]), 1e-300)
+    assert float(err.max()) <= 1e-5
+
+
 @pytest.mark.parametrize("scene,w,h,spp,depth", [("cornell", 37, 29, 3, 5), ("zoo", 45, 19, 2, 4),
                                                   ("main", 13, 61, 1, 3)])
 def test_mode_x_ragged_frames_bit_exact(torch_cuda, scene, w, h, spp, depth):

@@ -118,12 +118,62 @@ def test_scene_round_trip(name):
 
 @pytest.mark.parametrize("bad", ["v 1 2\n", "v 1 2 x\n", "v 1 2 nan\n", "v 0 0 0\nv 1 0 0\nf 1 2\n",
                                  "v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 4\n", "v 0 0 0\nv 1 0 0\nv 0 1 0\nf 0 1 2\n",
-                                 "v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 -4\n", "v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 a/1\n"])
+                                 "v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 -4\n", "v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 a/1\n",
+                                 # one number grammar on both sides (gi_obj.cpp is_real): no hex floats,
+                                 # inf / nan, digit separators, non-ASCII digits, bare '.' or exponent
+                                 "v 0x1p3 0 0\n", "v 1_0 0 0\n", "v \u0661 0 0\n", "v inf 0 0\n", "v -Infinity 0 0\n",
+                                 "v . 0 0\n", "v 1e 0 0\n", "v 1e+ 0 0\n", "v 1,5 0 0\n", "v +-1 0 0\n",
+                                 "v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 0x3\n", "v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 3_\n",
+                                 "v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 \u0663\n", "v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 +\n"])
 def test_malformed_input_rejected(bad):
     with pytest.raises(gi.GIError, match="obj line"):
         c_parse(bad)
     with pytest.raises(ValueError, match="obj line"):
         py_parse(bad)
+
+
+def test_number_forms_agree():
+    """Every accepted number form parses to the same double on both sides."""
+    text = ("v +1. .5 -0\nv 1E+2 -2.5e-3 007\nv 1e308 -4.9e-324 123456789012345678901234567890\n"
+            "f +1 2/7 -1//3\n")
+    c, p = c_parse(text), py_parse(text)
+    assert c == p
+    assert c[0][2] == (1.0, 0.5, -0.0, 100.0, -0.0025, 7.0, 1e308, -5e-324, 1.2345678901234568e29)
+
+
+def test_parse_ignores_c_locale(tmp_path):
+    """the reference host is a Qt app (QApplication sets the C locale from the
+    environment), so gi_obj_parse must not read "1.5" as 1 under a comma-decimal LC_NUMERIC.  A
+    comma-decimal locale is compiled into tmp_path with localedef (the image ships none) and the
+    parse runs in a child process with it in force."""
+    import shutil
+    import subprocess
+    import sys
+    if not shutil.which("localedef"):
+        pytest.skip("localedef not available")
+    (tmp_path / "comma").write_text('LC_NUMERIC\ndecimal_point "<U002C>"\nthousands_sep "<U002E>"\n'
+                                    'grouping 3;3\nEND LC_NUMERIC\n')
+    cm = ["<escape_char> /", "<comment_char> %", "<code_set_name> ASCIITEST", "<mb_cur_min> 1", "<mb_cur_max> 1",
+          "CHARMAP"] + ["<U%04X> /x%02x C%d" % (i, i, i) for i in range(128)] + ["END CHARMAP"]
+    (tmp_path / "ascii.cm").write_text("\n".join(cm) + "\n")
+    subprocess.run(["localedef", "-c", "-i", str(tmp_path / "comma"), "-f", str(tmp_path / "ascii.cm"), "--no-archive",
+                    str(tmp_path / "xxcomma")], capture_output=True)
+    if not (tmp_path / "xxcomma" / "LC_NUMERIC").exists():
+        pytest.skip("localedef could not build a test locale")
+    child = f"""
+import ctypes, locale, sys
+sys.path.insert(0, {repr(__import__("os").path.join(U.ROOT, "tests"))})
+import test_obj as T
+locale.setlocale(locale.LC_NUMERIC, "xxcomma")
+libc = ctypes.CDLL(None)
+libc.strtod.restype = ctypes.c_double
+assert libc.strtod(b"1.5", None) == 1.0, "the test locale is not comma-decimal"
+print(repr(T.c_parse(T.CUBE.replace(" 1 1 1", " 1.5 0.25 1e-1"))))
+"""
+    env = dict(__import__("os").environ, LOCPATH=str(tmp_path))
+    r = subprocess.run([sys.executable, "-c", child], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip().splitlines()[-1] == repr(c_parse(CUBE.replace(" 1 1 1", " 1.5 0.25 1e-1")))
 
 
 def test_error_line_numbers_agree():
