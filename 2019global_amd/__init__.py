@@ -51,7 +51,9 @@ STAT_RAYS, STAT_NODES, STAT_PRIMS, STAT_PIXELS, STAT_X_PATH_MAX = 0, 1, 2, 3, 4
 STAT_X_ITERS, STAT_X_TRAV, STAT_X_HANDLE, STAT_X_HLANES, STAT_X_HCLOSE, STAT_X_HSHADOW = 5, 6, 7, 8, 9, 10
 STAT_X_CYC_TRAV, STAT_X_CYC_HIT, STAT_X_CYC_NEXT, STAT_X_CYC_ALL = 11, 12, 13, 14
 STAT_X_RESOLVED = 15
-STATS_N = 16
+STAT_X_IT_NODE, STAT_X_LN_NODE, STAT_X_IT_LEAF, STAT_X_LN_LEAF = 16, 17, 18, 19
+STAT_X_IT_RS, STAT_X_LN_RS, STAT_X_IT_ST, STAT_X_LN_ST = 20, 21, 22, 23
+STATS_N = 24
 TILE = 8
 ABI_VERSION = 8
 

@@ -612,12 +612,41 @@ __device__ __forceinline__ uint32_t children_mask_line(const XWNode* nd, F3 of, 
     return m;
 }
 
+// Per-ray memo of node-test results (k_mode_r_split): the candidates' root paths share their upper
+// levels -- every path starts at the root -- and an exact ExpBox node test is ~12 fp32/fp64 triangle
+// solves, so a ray that walks many appearances' paths would repeat the same tests.  Direct-mapped,
+// RMEMO entries per ray in LDS, shared by the NSUB lanes of the pixel (one ray, so a result found
+// by any of them holds for all); an entry is (node << 1) | passed, -1 when empty.  A lost or stale
+// slot only costs a recomputation: the answer never depends on the memo.
+#ifndef GI_R_MEMO
+#define GI_R_MEMO 64   // entries per ray (power of two); 0 disables the memo
+#endif
+struct RMemo {
+    int* e;   // GI_R_MEMO entries of this ray, or nullptr
+};
+__device__ __forceinline__ int r_memo_slot(int node) { return (int)(((unsigned)node * 2654435761u) >> 26) & (GI_R_MEMO - 1); }
+
 // is leaf `leaf` in the ray's candidate list?  (octree.h:139-150 on its root path, top-down)
-__device__ __forceinline__ bool r_leaf_reachable(const DevScene& sc, int leaf, V3 o, V3 d, uint32_t& nnode) {
+__device__ __forceinline__ bool r_leaf_reachable(const DevScene& sc, int leaf, V3 o, V3 d, uint32_t& nnode,
+                                                 RMemo memo = RMemo{nullptr}) {
     const int p1 = sc.rpath_off[leaf + 1];
     for (int i = sc.rpath_off[leaf]; i < p1; ++i) {
-        const RNode& nd = sc.rnodes[sc.rpath[i]];
+        const int ni = sc.rpath[i];
+        const RNode& nd = sc.rnodes[ni];
         if (nd.ent_cnt == 0) return false;   // octree.h:140
+        if (GI_R_MEMO > 0 && memo.e) {
+            int* slot = memo.e + r_memo_slot(ni);
+            const int m = *slot;
+            if ((m >> 1) == ni) {
+                if (!(m & 1)) return false;
+                continue;
+            }
+            ++nnode;
+            const bool ok = box_hit(ld3(nd.mn), ld3(nd.mx), o, d);
+            *slot = (ni << 1) | (ok ? 1 : 0);
+            if (!ok) return false;
+            continue;
+        }
         ++nnode;
         if (!box_hit(ld3(nd.mn), ld3(nd.mx), o, d)) return false;
     }
@@ -626,7 +655,7 @@ __device__ __forceinline__ bool r_leaf_reachable(const DevScene& sc, int leaf, V
 
 // entity e as a candidate: exact test, then its latest reachable appearance against the best so far
 __device__ __forceinline__ void r_consider(const DevScene& sc, int e, V3 o, V3 d, long long& best, RResult& r,
-                                           uint32_t& nnode, uint32_t& nprim) {
+                                           uint32_t& nnode, uint32_t& nprim, RMemo memo = RMemo{nullptr}) {
     const int a0 = sc.app_off[e], a1 = sc.app_off[e + 1];
     if (a0 == a1 || sc.app_rank[a0] <= best) return;
     V3 P, N;
@@ -634,7 +663,7 @@ __device__ __forceinline__ void r_consider(const DevScene& sc, int e, V3 o, V3 d
     for (int i = a0; i < a1; ++i) {
         const long long rk = sc.app_rank[i];
         if (rk <= best) return;
-        if (r_leaf_reachable(sc, sc.app_leaf[i], o, d, nnode)) {
+        if (r_leaf_reachable(sc, sc.app_leaf[i], o, d, nnode, memo)) {
             best = rk;
             r.ent = e;
             r.P = P;
@@ -706,7 +735,7 @@ __device__ __forceinline__ long long group_max(long long v) {
 }
 template <int NSUB>
 __device__ __forceinline__ void trace_mode_r_split(const DevScene& sc, V3 o, V3 d, float tau, int sub, RResult& r,
-                                                   long long& mine, uint32_t& nnode, uint32_t& nprim) {
+                                                   long long& mine, uint32_t& nnode, uint32_t& nprim, RMemo memo) {
     r.ent = -1;
     mine = -1;
     long long best = -1;   // the group's best rank so far (pruning bound)
@@ -714,7 +743,7 @@ __device__ __forceinline__ void trace_mode_r_split(const DevScene& sc, V3 o, V3 
     auto consider = [&](int e) {
         if ((int)(k++ % NSUB) != sub) return;
         const long long before = best;
-        r_consider(sc, e, o, d, best, r, nnode, nprim);
+        r_consider(sc, e, o, d, best, r, nnode, nprim, memo);
         if (best != before) mine = best;
     };
     for (int i = 0; i < sc.n_r_always; ++i) consider(sc.r_always[i]);
@@ -761,6 +790,13 @@ __global__ __launch_bounds__(256) void k_mode_r_split(DevScene sc, CamDev cam, V
     const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     const long long ps = g / NSUB;   // pixel slot (tile order)
     const int sub = (int)(g % NSUB);
+    // the ray's node-test memo: GI_R_MEMO entries per pixel group, cleared by its lanes
+    __shared__ int s_memo[GI_R_MEMO > 0 ? (256 / NSUB) * GI_R_MEMO : 1];
+    RMemo memo{GI_R_MEMO > 0 ? s_memo + (threadIdx.x / NSUB) * GI_R_MEMO : nullptr};
+    if (GI_R_MEMO > 0) {
+        for (int k = sub; k < GI_R_MEMO; k += NSUB) memo.e[k] = -1;
+        __builtin_amdgcn_wave_barrier();   // a group's lanes are in one wave (NSUB <= 64)
+    }
     const long long lt = ps >> 6;
     long long idx = -1;
     int x = 0, y = 0;
@@ -772,7 +808,7 @@ __global__ __launch_bounds__(256) void k_mode_r_split(DevScene sc, CamDev cam, V
         const V3 d = normalize(primary_dir(cam, (double)x, (double)y));   // Ray ctor (ray.h:6)
         RResult r;
         long long mine;
-        trace_mode_r_split<NSUB>(sc, o, d, tau, sub, r, mine, nnode, nprim);
+        trace_mode_r_split<NSUB>(sc, o, d, tau, sub, r, mine, nnode, nprim, memo);
         const long long gmax = group_max<NSUB>(mine);
         // the lowest sub-lane holding the maximum shades (ranks are unique: one lane at most)
         const unsigned long long m_win = __ballot(mine == gmax);
@@ -965,6 +1001,14 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 // C5 245 -> 229 ms; the 1k soup (XWNode) +4% and C4 (short launches) +7% keep the plain step
 #define GI_X_LEAFQ 1
 #endif
+#ifndef GI_X_LEAFQ_LDS
+#define GI_X_LEAFQ_LDS 0   // LDS-resident scenes: leaf postponement as above (leaf tests two at a time)
+#endif
+#ifndef GI_X_RSPEND
+// inline bounce restart (short-traversal scenes): the new ray's root test runs as the next
+// traversal step, in the node-test code the descending lanes run, instead of in a block of its own
+#define GI_X_RSPEND 0
+#endif
 #ifndef GI_X_LEAF8
 #define GI_X_LEAF8 3   // LQ: leaf phase once 3/8 of the traversing lanes hold a leaf (C5 sweep 1-8)
 #endif
@@ -989,6 +1033,9 @@ struct XCounters {
     // << 16) | traversal steps of that lane during it (both saturated at 65535), maximised as one word
     uint64_t path_t0 = 0, path_max = 0;
     uint32_t path_it = 0, path_st = 0;
+    // divergence profile (wave-level, lane 0): loop iterations in which some lane ran a node test /
+    // a leaf test / an inline bounce restart / a handler start-loop pass, and the lanes that did
+    uint64_t it_node = 0, ln_node = 0, it_leaf = 0, ln_leaf = 0, it_rs = 0, ln_rs = 0, it_st = 0, ln_st = 0;
 };
 
 // Mode X work list (k_x_classify -> k_mode_x -> k_x_reduce).  A pixel whose every jittered primary
@@ -1104,6 +1151,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     bool raying = false;
     int poff = 0, pcnt = 0;   // LQ: the pending leaf (records H[poff .. poff + pcnt)), pcnt 0: none
     bool pdone = false;       // LQ: the ray ends once its pending leaf is tested
+    bool rootp = false;       // RSPEND: the lane's next step is its restarted ray's root test
     const int leaf8 = ((xflags >> 12) & 15) ? ((xflags >> 12) & 15) : GI_X_LEAF8;
     uint64_t mlo = 0, mhi = 0;
     double tbest = INFINITY, tmax = INFINITY;
@@ -1115,6 +1163,54 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     V3 Lv = v3(0, 0, 0), Lo = v3(0, 0, 0), T = v3(1, 1, 1);
     V3 nextd = v3(0, 0, 0);   // carried across the shadow ray (its origin = the shadow ray's)
     bool has_next = false;
+
+    // fp64 primitive tests of one leaf's records hp[0 .. cntl) (these decide the result): global
+    // records fetched one ahead of the test; LDS records (PAIR) two at a time, the two fp64
+    // dependency chains interleaved.  A shadow ray (own or a helper's) stops at any hit.
+    auto leaf_test = [&](const auto* hp, int cntl) {
+        if constexpr (!PAIR) {
+            XHotR cur = load_hot(hp);
+            for (int j = 0; j < cntl; ++j) {
+                const XHotR rec = cur;
+                cur = load_hot(hp + min(j + 1, cntl - 1));
+                ++nprim;
+                const double t = x_prim_t(rec.h, o, d, MX_TMIN);
+                const int pi = rec.h.prim;
+                if (phase != PH_CLOSEST) {
+                    if (t < tmax) { best = pi; raying = false; return; }   // any hit occludes
+                } else if (t < tbest || (t == tbest && pi < best)) {
+                    tbest = t;
+                    best = pi;
+                    tbest_f = up32(t);
+                }
+            }
+        } else {
+            for (int j = 0; j < cntl; j += 2) {
+                const bool two = j + 1 < cntl;
+                const XHotR r0 = load_hot(hp + j), r1 = load_hot(hp + (two ? j + 1 : j));
+                const double ta = x_prim_t(r0.h, o, d, MX_TMIN);
+                const double tb = two ? x_prim_t(r1.h, o, d, MX_TMIN) : INFINITY;
+                nprim += two ? 2 : 1;
+                if (phase != PH_CLOSEST) {
+                    if (ta < tmax || tb < tmax) {   // any hit occludes
+                        best = ta < tmax ? r0.h.prim : r1.h.prim;
+                        raying = false;
+                        return;
+                    }
+                } else {
+                    if (ta < tbest || (ta == tbest && r0.h.prim < best)) {
+                        tbest = ta;
+                        best = r0.h.prim;
+                    }
+                    if (tb < tbest || (tb == tbest && r1.h.prim < best)) {
+                        tbest = tb;
+                        best = r1.h.prim;
+                    }
+                    tbest_f = up32(tbest);
+                }
+            }
+        }
+    };
 
     const uint64_t t_begin = STATS ? clock64() : 0;
     for (;;) {
@@ -1178,7 +1274,6 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             const unsigned long long m_pl = __ballot(trav && pcnt > 0);
             leaf_phase = m_pl != 0 && (m_pl == m_trav || 8 * __popcll(m_pl) >= leaf8 * __popcll(m_trav));
         }
-        static_assert(!(LQ && PAIR), "leaf postponement is built for global (HBM) leaf records");
         if (trav) {
             // up to GI_X_TRAV_UNROLL steps per loop iteration: the scheduling ballots and the handler
             // decision are paid once per iteration (a lane whose ray ends stops stepping)
@@ -1186,23 +1281,8 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             for (int u = 0; u < GI_X_TRAV_UNROLL; ++u) {
             if (u > 0 && !raying) break;
             if (LQ && leaf_phase) {
-                if (pcnt > 0) {   // the pending leaf's fp64 primitive tests, records fetched one ahead
-                    const XHot* hp = H + poff;
-                    XHotR cur = load_hot(hp);
-                    for (int j = 0; j < pcnt; ++j) {
-                        const XHotR rec = cur;
-                        cur = load_hot(hp + min(j + 1, pcnt - 1));
-                        ++nprim;
-                        const double t = x_prim_t(rec.h, o, d, MX_TMIN);
-                        const int pi = rec.h.prim;
-                        if (phase != PH_CLOSEST) {   // shadow ray (own or a helper's)
-                            if (t < tmax) { best = pi; raying = false; break; }   // any hit occludes
-                        } else if (t < tbest || (t == tbest && pi < best)) {
-                            tbest = t;
-                            best = pi;
-                            tbest_f = up32(t);
-                        }
-                    }
+                if (pcnt > 0) {   // the pending leaf's fp64 primitive tests
+                    leaf_test(H + poff, pcnt);
                     pcnt = 0;
                     if (pdone) {   // the step that popped this leaf exhausted the ray's last level
                         pdone = false;
@@ -1217,68 +1297,44 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             // ---- one traversal step (stackless: 8-bit "children left" mask per level).  Invariant:
             // the current level has a child left; the step pops it, then climbs past exhausted
             // levels, so a ray ends in the step that exhausts the root level (no empty iteration).
-            const uint32_t msk = lvl_get<SH>(mlo, mhi, level);
-            const int kc = __builtin_ctz(msk);         // next child in front-to-back order
-            lvl_set<SH>(mlo, mhi, level, msk & (msk - 1));
-            const int c = kc ^ dmask;
             const auto* nd = W + node;
-            const int ch = nd->child[c];
-            // a closer hit may have arrived since the mask was computed: re-cull this child
+            int c = 0, ch = 0;   // RSPEND root step: "child" 0 = the root wide node itself
             bool keep = true;
-            if (phase == PH_CLOSEST && best >= 0) keep = child_hit(nd, c, of, ivf, tbest_f);
+            if (!(GI_X_RSPEND && rootp)) {
+                const uint32_t msk = lvl_get<SH>(mlo, mhi, level);
+                const int kc = __builtin_ctz(msk);         // next child in front-to-back order
+                lvl_set<SH>(mlo, mhi, level, msk & (msk - 1));
+                c = kc ^ dmask;
+                ch = nd->child[c];
+                // a closer hit may have arrived since the mask was computed: re-cull this child
+                if (phase == PH_CLOSEST && best >= 0) keep = child_hit(nd, c, of, ivf, tbest_f);
+            }
+            if (STATS) {
+                const unsigned long long mn = __ballot(keep && ch >= 0), ml = __ballot(keep && ch < 0);
+                if (lane == 0) {
+                    cnt.it_node += mn != 0;
+                    cnt.ln_node += __popcll(mn);
+                    cnt.it_leaf += ml != 0;
+                    cnt.ln_leaf += __popcll(ml);
+                }
+            }
             if (keep) {
                 if (LQ && ch < 0) {       // leaf: pending until the wave's next leaf phase
                     poff = ~ch;
                     pcnt = nd->cnt[c];
                 } else if (ch < 0) {      // leaf: fp64 primitive tests (these decide the result)
-                    const XHot* hp = H + ~ch;
-                    const int cntl = nd->cnt[c];
-                    if constexpr (!PAIR) {   // global records: fetched one ahead of the test
-                        XHotR cur = load_hot(hp);
-                        for (int j = 0; j < cntl; ++j) {
-                            const XHotR rec = cur;
-                            cur = load_hot(hp + min(j + 1, cntl - 1));
-                            ++nprim;
-                            const double t = x_prim_t(rec.h, o, d, MX_TMIN);
-                            const int pi = rec.h.prim;
-                            if (phase != PH_CLOSEST) {   // shadow ray (own or a helper's)
-                                if (t < tmax) { best = pi; raying = false; break; }   // any hit occludes
-                            } else if (t < tbest || (t == tbest && pi < best)) {
-                                tbest = t;
-                                best = pi;
-                                tbest_f = up32(t);
-                            }
-                        }
-                    } else
-                    // LDS records: tested two at a time, the two fp64 dependency chains interleave
-                    for (int j = 0; j < cntl; j += 2) {
-                        const bool two = j + 1 < cntl;
-                        const XHotR r0 = load_hot(hp + j), r1 = load_hot(hp + (two ? j + 1 : j));
-                        const double ta = x_prim_t(r0.h, o, d, MX_TMIN);
-                        const double tb = two ? x_prim_t(r1.h, o, d, MX_TMIN) : INFINITY;
-                        nprim += two ? 2 : 1;
-                        if (phase != PH_CLOSEST) {
-                            if (ta < tmax || tb < tmax) {   // any hit occludes
-                                best = ta < tmax ? r0.h.prim : r1.h.prim;
-                                raying = false;
-                                break;
-                            }
-                        } else {
-                            if (ta < tbest || (ta == tbest && r0.h.prim < best)) {
-                                tbest = ta;
-                                best = r0.h.prim;
-                            }
-                            if (tb < tbest || (tb == tbest && r1.h.prim < best)) {
-                                tbest = tb;
-                                best = r1.h.prim;
-                            }
-                            tbest_f = up32(tbest);
-                        }
-                    }
+                    leaf_test(H + ~ch, (int)nd->cnt[c]);
                 } else {                  // descend if any of the child's 8 children is hit (fp32)
-                    ++nnode;
+                    if (!(GI_X_RSPEND && rootp)) ++nnode;   // (root tests are not node visits)
                     const uint32_t cm = children_mask<PAIR>(W + ch, of, ivf, tbest_f, dmask);
-                    if (cm) {
+                    if (GI_X_RSPEND && rootp) {   // the restarted ray's root mask: level 0
+                        rootp = false;
+                        node = 0;
+                        level = 0;
+                        mlo = mhi = 0;
+                        lvl_set<SH>(mlo, mhi, 0, cm);
+                        raying = cm != 0;         // no root child hit: finished
+                    } else if (cm) {
                         node = ch;
                         ++level;
                         lvl_set<SH>(mlo, mhi, level, cm);
@@ -1321,6 +1377,13 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             // right here (the bounce direction was drawn when the hit was shaded), so the lane
             // keeps traversing instead of waiting for the shading handler (short-traversal scenes;
             // for long ones the extra divergent root test costs more than it saves)
+            if (STATS) {
+                const unsigned long long mr = __ballot(inline_shadow && !raying && phase == PH_SHADOW && has_next);
+                if (lane == 0) {
+                    cnt.it_rs += mr != 0;
+                    cnt.ln_rs += __popcll(mr);
+                }
+            }
             if (inline_shadow && !raying && phase == PH_SHADOW && has_next) {
                 ++nrays;
                 if (best >= 0) Lv = PSL ? v3(pslot[0], pslot[1], pslot[2]) : Lo;   // occluded: ambient term only
@@ -1333,13 +1396,18 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 of = f3((float)o.x, (float)o.y, (float)o.z);
                 ivf = inv_dir(d);
                 dmask = (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
-                const uint32_t rm = children_mask<PAIR>(W, of, ivf, tbest_f, dmask);
                 best = -1;
-                node = 0;
-                level = 0;
-                mlo = mhi = 0;
-                lvl_set<SH>(mlo, mhi, 0, rm);
-                raying = rm != 0;
+                if (GI_X_RSPEND) {   // the root test waits for the next step's shared node test
+                    rootp = true;
+                    raying = true;
+                } else {
+                    const uint32_t rm = children_mask<PAIR>(W, of, ivf, tbest_f, dmask);
+                    node = 0;
+                    level = 0;
+                    mlo = mhi = 0;
+                    lvl_set<SH>(mlo, mhi, 0, rm);
+                    raying = rm != 0;
+                }
             }
             }
         }
@@ -1497,6 +1565,13 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             // GI_X_START_BURST primary rays per lane per handler run.
             int burst = 0;
             for (;;) {
+                if (STATS) {
+                    const unsigned long long mb = __ballot(true);
+                    if (lane == 0) {
+                        cnt.it_st += 1;
+                        cnt.ln_st += __popcll(mb);
+                    }
+                }
                 if (phase == PH_DONEPX) phase = PH_NEED;   // unit complete (its samples are stored)
                 const unsigned long long m_need = __ballot(phase == PH_NEED);
                 if (m_need) {
@@ -1693,7 +1768,7 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
         // (occluded sum, next direction, throughput T, RNG key) live in a per-lane LDS slot after
         // the scene instead of in VGPRs / scratch
         double* pslot = reinterpret_cast<double*>(lds_scene + nw + nh + np + ne) + 10 * threadIdx.x;
-        mode_x_wave<STATS, GI_X_PAIR != 0, W4 && GI_X_PSL, false, false, SH, false>(sc, W, H, XP, EN, pslot, nullptr, XHelp{},
+        mode_x_wave<STATS, GI_X_PAIR != 0, W4 && GI_X_PSL, false, false, SH, GI_X_LEAFQ_LDS != 0>(sc, W, H, XP, EN, pslot, nullptr, XHelp{},
                                                                         cam, light, m, spp, depth, seed, rgb, rgb8, blk,
                                                                         wk, handle8, xflags, c);
     } else {
@@ -1728,6 +1803,14 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
             atomicAdd(stats + GI_STAT_X_CYC_HIT, (unsigned long long)c.cyc_hit);
             atomicAdd(stats + GI_STAT_X_CYC_NEXT, (unsigned long long)c.cyc_next);
             atomicAdd(stats + GI_STAT_X_CYC_ALL, (unsigned long long)c.cyc_all);
+            atomicAdd(stats + GI_STAT_X_IT_NODE, (unsigned long long)c.it_node);
+            atomicAdd(stats + GI_STAT_X_LN_NODE, (unsigned long long)c.ln_node);
+            atomicAdd(stats + GI_STAT_X_IT_LEAF, (unsigned long long)c.it_leaf);
+            atomicAdd(stats + GI_STAT_X_LN_LEAF, (unsigned long long)c.ln_leaf);
+            atomicAdd(stats + GI_STAT_X_IT_RS, (unsigned long long)c.it_rs);
+            atomicAdd(stats + GI_STAT_X_LN_RS, (unsigned long long)c.ln_rs);
+            atomicAdd(stats + GI_STAT_X_IT_ST, (unsigned long long)c.it_st);
+            atomicAdd(stats + GI_STAT_X_LN_ST, (unsigned long long)c.ln_st);
         }
         wave_add_stats(stats, c.rays, c.nodes, c.prims, c.px);
         uint64_t cr = c.res, pm = c.path_max;

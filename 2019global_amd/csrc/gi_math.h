@@ -309,23 +309,21 @@ GI_HD void mx_sincos_q(double p, double& sn, double& cs) {
     sn = p + p * (z * ps);
     cs = 1.0 + z * pc;
 }
+// Branch-free form of the concentric map (the same operations per lane as the two-branch
+// statement of the oracle's mx_disk: the octant choice selects operands, one quotient, one
+// sincos), so a wave evaluates one polynomial pair instead of both branches' copies.
 GI_HD void mx_disk(double u1, double u2, double& dx, double& dy, double& r2) {
     const double a = 2.0 * u1 - 1.0, b = 2.0 * u2 - 1.0;
     const double QPI = 0x1.921fb54442d18p-1;   // pi/4
-    if (a == 0.0 && b == 0.0) { dx = 0.0; dy = 0.0; r2 = 0.0; return; }
-    double r, sn, cs;
-    if ((a < 0 ? -a : a) > (b < 0 ? -b : b)) {
-        r = a;
-        mx_sincos_q(QPI * (b / a), sn, cs);
-        dx = r * cs;
-        dy = r * sn;
-    } else {
-        r = b;
-        mx_sincos_q(QPI * (a / b), sn, cs);
-        dx = r * sn;
-        dy = r * cs;
-    }
-    r2 = r * r;
+    const bool ax = (a < 0 ? -a : a) > (b < 0 ? -b : b);
+    const double r = ax ? a : b, num = ax ? b : a;
+    const double q = num / r;
+    double sn, cs;
+    mx_sincos_q(QPI * q, sn, cs);
+    const bool zero = a == 0.0 && b == 0.0;
+    dx = zero ? 0.0 : r * (ax ? cs : sn);
+    dy = zero ? 0.0 : r * (ax ? sn : cs);
+    r2 = zero ? 0.0 : r * r;
 }
 
 GI_HD V3 texel(V3 color, int32_t u, int32_t v) {

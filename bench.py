@@ -95,7 +95,8 @@ def counter_ceilings(workload: str, kern_ms: float):
         and lane utilisation = SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU); their product is
         the fraction of the chip's VALU lane-slots doing work;
       * FP64 (Mode R): f64 VALU instructions / all VALU instructions, and the f64 FLOP
-        rate they imply (FMA = 2, every lane counted) against the 78.6 TF/s FP64 vector peak.
+        rate (SQ_INSTS_VALU_FLOPS_FP64, a per-wave-instruction count, x 64 lanes x lane utilisation)
+        against the 78.6 TF/s FP64 vector peak -- Mode R's roofline.
     `binding` names the tightest: valu_issue when the SIMDs issue in >= 75% of their slots,
     else hbm when counter traffic is >= 60% of peak, else latency (waiting on memory)."""
     got = pmc_summary(workload)
@@ -120,14 +121,16 @@ def counter_ceilings(workload: str, kern_ms: float):
     f64 = [c.get(k) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
                               "SQ_INSTS_VALU_TRANS_F64")]
     if all(v is not None for v in f64) and c.get("SQ_INSTS_VALU"):
-        add, mul, fma, trans = f64
-        out["f64_inst_share"] = round((add + mul + fma + trans) / c["SQ_INSTS_VALU"], 4)
-        flops = 64.0 * (add + mul + 2.0 * fma + trans)
-        out["f64_tflops_upper"] = round(flops / (kern_ms * 1e-3) / 1e12, 3)
-        out["f64_valu_frac"] = round(out["f64_tflops_upper"] / FP64_VALU_PEAK_TFS, 4)
-    if c.get("SQ_INSTS_VALU_FLOPS_FP64") is not None:   # the counter's own f64 FLOP count
-        out["f64_tflops_counter"] = round(c["SQ_INSTS_VALU_FLOPS_FP64"] / (kern_ms * 1e-3) / 1e12, 3)
-        out["f64_valu_frac_counter"] = round(out["f64_tflops_counter"] / FP64_VALU_PEAK_TFS, 4)
+        out["f64_inst_share"] = round(sum(f64) / c["SQ_INSTS_VALU"], 4)
+    # FP64 FLOP rate (Mode R's designated bound).  SQ_INSTS_VALU_FLOPS_FP64 counts per
+    # wave instruction (it equals add + 2 fma + mul + trans of the f64 instruction counters exactly,
+    # VERDICT r02), so the FLOPs are that count x 64 lanes x the fraction of lanes active -- the
+    # kernel-wide VALU lane utilisation, applied to its f64 instructions
+    if c.get("SQ_INSTS_VALU_FLOPS_FP64") is not None and "valu_lane_util" in out:
+        flops = c["SQ_INSTS_VALU_FLOPS_FP64"] * 64.0 * out["valu_lane_util"]
+        out["f64_flops_per_launch"] = int(flops)
+        out["f64_tflops"] = round(flops / (kern_ms * 1e-3) / 1e12, 4)
+        out["f64_valu_frac"] = round(out["f64_tflops"] / FP64_VALU_PEAK_TFS, 5)
     if out.get("valu_issue_frac", 0) >= 0.75:
         out["binding"] = "valu_issue"
     elif out.get("hbm_counter_frac", 0) >= 0.6:
@@ -405,6 +408,16 @@ def main():
         }
         if ceil:
             out["roofline"].update({k: v for k, v in ceil.items() if k != "hbm_counter_bytes"})
+        if mode == 0 and ceil and "f64_tflops" in ceil:
+            # Mode R is FP64-VALU bound by arithmetic intensity (the exact ExpBox node
+            # test is ~20-40 fp64 ops per record byte): the roofline is the FP64 vector peak; the
+            # algorithmic record bytes stay beside it as hbm_* fields
+            r = out["roofline"]
+            hbm_part = {"hbm_achieved_gbs": r.pop("achieved"), "hbm_peak_gbs": r.pop("peak"), "hbm_frac": r.pop("frac")}
+            r.update({"bound": "fp64_valu", "achieved": ceil["f64_tflops"], "peak": FP64_VALU_PEAK_TFS,
+                      "unit": "TFLOP/s", "frac": ceil["f64_valu_frac"],
+                      "achieved_note": "f64 FLOPs per launch (PMC SQ_INSTS_VALU_FLOPS_FP64 x 64 lanes x VALU "
+                                       "lane utilisation, pmc_source) / live kernel time", **hbm_part})
         if frame_check is not None:
             out["frame_check"] = frame_check
             if args.dist_backend != "nccl":
@@ -422,6 +435,13 @@ def main():
                                "longest_path": {"ms": round((st[gi.STAT_X_PATH_MAX] >> 32) / 1e5, 4),
                                                 "wave_iterations": (st[gi.STAT_X_PATH_MAX] >> 16) & 0xFFFF,
                                                 "trav_steps": st[gi.STAT_X_PATH_MAX] & 0xFFFF},
+                               # divergence profile: loop iterations that ran each block, and the
+                               # lanes that used it (fill = lanes / (64 x iterations))
+                               "blocks": {k: {"iterations": st[a], "lane_fill": round(st[b] / (64.0 * max(1, st[a])), 4)}
+                                          for k, a, b in (("node_test", gi.STAT_X_IT_NODE, gi.STAT_X_LN_NODE),
+                                                          ("leaf_test", gi.STAT_X_IT_LEAF, gi.STAT_X_LN_LEAF),
+                                                          ("bounce_restart", gi.STAT_X_IT_RS, gi.STAT_X_LN_RS),
+                                                          ("ray_start_pass", gi.STAT_X_IT_ST, gi.STAT_X_LN_ST))},
                                "cycle_share": {k: round(st[i] / max(1, st[gi.STAT_X_CYC_ALL]), 4) for k, i in
                                                (("traverse", gi.STAT_X_CYC_TRAV), ("consume", gi.STAT_X_CYC_HIT),
                                                 ("next_ray", gi.STAT_X_CYC_NEXT))}}

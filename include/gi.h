@@ -143,7 +143,18 @@ typedef struct gi_opts {
 #define GI_STAT_X_CYC_ALL 14  /* Mode X: wave clock cycles in the whole loop */
 #define GI_STAT_X_RESOLVED 15 /* Mode X: primary samples resolved without traversal (pixel-frustum classify
                                  and root-box pretest misses; each still adds exactly +0, as traced) */
-#define GI_STATS_N 16
+/* Mode X divergence profile (wave-level): loop iterations in which some lane ran a node test (IT_NODE)
+   and the lane node tests (LN_NODE); the same for leaf tests, inline bounce restarts (RS) and passes of
+   the handler's ray-start loop (ST: lanes = lanes in the handler during the pass) */
+#define GI_STAT_X_IT_NODE 16
+#define GI_STAT_X_LN_NODE 17
+#define GI_STAT_X_IT_LEAF 18
+#define GI_STAT_X_LN_LEAF 19
+#define GI_STAT_X_IT_RS 20
+#define GI_STAT_X_LN_RS 21
+#define GI_STAT_X_IT_ST 22
+#define GI_STAT_X_LN_ST 23
+#define GI_STATS_N 24
 
 #define GI_TILE 8             /* shard granularity: 8x8 pixel tiles, dealt round-robin to ranks */
 
