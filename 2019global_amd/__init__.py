@@ -528,13 +528,20 @@ class MultiScene:
         return {"shards": a.value, "devices": b.value, "rccl": bool(c.value)}
 
     def render(self, cam: Camera, light, w: int, h: int, mode=MODE_R, spp=1, depth=1, seed=0, band_rows=0,
-               cancel: Optional[ctypes.c_int] = None, callback=None):
-        rgb, rgb8 = np.zeros((h, w, 3), np.float64), np.zeros((h, w, 3), np.uint8)
+               cancel: Optional[ctypes.c_int] = None, callback=None, out=None):
+        """gi_multi_render into host arrays; out=(rgb, rgb8) as DeviceScene.render (either may be None)."""
+        if out is None:
+            rgb, rgb8 = np.zeros((h, w, 3), np.float64), np.zeros((h, w, 3), np.uint8)
+        else:
+            rgb, rgb8 = out
+        for a, dt in ((rgb, np.float64), (rgb8, np.uint8)):
+            if a is not None and (a.dtype != dt or a.size != w * h * 3 or not a.flags.c_contiguous):
+                raise ValueError("render: out arrays must be C-contiguous [h, w, 3] float64 / uint8")
         cb = TILE_CB(callback) if callback is not None else TILE_CB()
         o = DeviceScene.opts(mode, spp, depth, seed, band_rows=band_rows)
         _check(lib().gi_multi_render(self._h, ctypes.byref(cam._c), _d3(light), w, h, ctypes.byref(o),
-                                     rgb.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
-                                     rgb8.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                                     rgb.ctypes.data_as(ctypes.POINTER(ctypes.c_double)) if rgb is not None else None,
+                                     rgb8.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)) if rgb8 is not None else None,
                                      ctypes.byref(cancel) if cancel is not None else None, cb, None), "gi_multi_render")
         return rgb, rgb8
 

@@ -347,8 +347,11 @@ __device__ __forceinline__ XHotR load_hot(const XHot* p) {
 
 // Möller–Trumbore, two-sided, barycentric tests on the numerators (no 1/det); all products are
 // formed before the first branch.  Spheres (kind 1): the geometric quadratic.
+// TRI: the scene's primitives are all triangles (kernels chosen per scene): the sphere branch and the
+// kind test vanish, so a leaf test is one straight block the compiler schedules as a whole
+template <bool TRI = false>
 __device__ __forceinline__ double x_prim_t(const XHot& p, V3 o, V3 d, double tmin) {
-    if (p.kind == 0) {
+    if (TRI || p.kind == 0) {
         const V3 e1 = ld3(p.b), e2 = ld3(p.c), v0 = ld3(p.a);
         const V3 pv = fcross(d, e2);
         const double det = fdot(e1, pv);
@@ -898,7 +901,33 @@ __device__ __forceinline__ bool pixel_misses_box(const CamDev& cam, int x, int y
     return false;
 }
 
+// TRI: only the entity kinds of the 4-wave scenes (triangle meshes without acos texture mapping:
+// ImpTriangle, ExpQuad, ExpCube; ExpBox maps to (0, 0)) -- the other kinds' code is not emitted
+template <bool TRI = false>
 __device__ __forceinline__ void x_texcoord(const DevScene& sc, const REnt& e, V3 ip, int32_t& x, int32_t& y) {
+    if (TRI) {
+        if (e.kind == K_IMP_TRIANGLE) {
+            const V3 p1 = ld3(e.qv0), p21 = ld3(e.qv1), i1 = ip - p1;
+            const double i1l = gsqrt(sq3(i1));
+            const double c = dot(p21, i1) / (e.qv2[0] * i1l);
+            const double ixl = i1l * mx_sin_acos(c);
+            y = x86_trunc(i1l / e.qv2[2]);
+            x = x86_trunc(ixl / e.qv2[1]);
+        } else if (e.kind == K_EXP_QUAD || e.kind == K_EXP_CUBE) {
+            const bool q = e.kind == K_EXP_QUAD;
+            const double uv = (double)e.width / 160.0, uh = (double)e.length / 160.0;
+            const V3 i1 = ip - (q ? ld3(e.qv1) : ld3(e.qv0));
+            const double l = gsqrt(sq3(i1));
+            const double c = q ? dot(i1, ld3(e.qv0) - ld3(e.qv1)) / ((double)e.width * l)
+                               : dot(i1, v3(0, (double)e.width, 0)) / ((double)e.width * l);
+            y = x86_trunc(l * mx_sin_acos(c) / uh);
+            x = x86_trunc(l * mx_cos_acos(c) / uv);
+        } else {
+            x = 0;
+            y = 0;
+        }
+        return;
+    }
     if (e.kind == K_IMP_SPHERE) {
         const double r = e.radius;
         const double unit_v = 2.0 * REF_PI * r / 320.0;
@@ -1009,6 +1038,18 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 // traversal step, in the node-test code the descending lanes run, instead of in a block of its own
 #define GI_X_RSPEND 0
 #endif
+#ifndef GI_X_TRI
+#define GI_X_TRI 1   // 4-wave LDS kernel: triangle-only primitive tests and texture mapping (TRI)
+#endif
+#ifndef GI_X_SPEC
+// speculative shadow rays (LDS scenes with path slots, i.e. the Cornell-class kernel): a closest
+// ray that finds a hit starts its shadow ray at once, inside the traversal step, instead of
+// waiting idle for the wave's shading handler; the handler shades the hit whenever it next runs
+// (the shadow ray's origin, direction and length are the hit point, light direction and distance
+// the shading uses -- the same values) and the shadow answer is applied when both are known.
+// Lanes that used to wait for the handler trace their shadow ray meanwhile.
+#define GI_X_SPEC 0
+#endif
 #ifndef GI_X_LEAF8
 #define GI_X_LEAF8 3   // LQ: leaf phase once 3/8 of the traversing lanes hold a leaf (C5 sweep 1-8)
 #endif
@@ -1092,8 +1133,8 @@ __device__ __forceinline__ int nth_set_bit(unsigned long long m, unsigned n) {
 // NST: the wide-node index of every level of the current traversal path lives in LDS (nst[level *
 // 256], one column per lane), so climbing out of exhausted levels is one ds_read instead of a chain
 // of dependent parent-pointer loads from HBM / L2 (one per level climbed).
-template <bool STATS, bool PAIR, bool PSL, bool NST, bool HELP, bool SH, bool LQ, typename NodeP, typename HotP,
-          typename PrimP, typename EntP>
+template <bool STATS, bool PAIR, bool PSL, bool NST, bool HELP, bool SH, bool LQ, bool TRI, typename NodeP,
+          typename HotP, typename PrimP, typename EntP>
 __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H, PrimP XP, EntP EN, double* pslot,
                                             int* nst, XHelp hp_,
                                             const CamDev& cam, V3 light,
@@ -1163,6 +1204,11 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     V3 Lv = v3(0, 0, 0), Lo = v3(0, 0, 0), T = v3(1, 1, 1);
     V3 nextd = v3(0, 0, 0);   // carried across the shadow ray (its origin = the shadow ray's)
     bool has_next = false;
+    // SPEC: the lane's closest hit waits for shading while its shadow ray runs; the hit's primitive
+    // and incoming direction are kept in the path slot (pslot[0] as int, pslot[3..5]: free until the
+    // shading writes Lo and the next direction there)
+    constexpr bool SPEC = GI_X_SPEC != 0 && PSL && !HELP && !LQ;
+    bool need_shade = false;
 
     // fp64 primitive tests of one leaf's records hp[0 .. cntl) (these decide the result): global
     // records fetched one ahead of the test; LDS records (PAIR) two at a time, the two fp64
@@ -1174,7 +1220,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 const XHotR rec = cur;
                 cur = load_hot(hp + min(j + 1, cntl - 1));
                 ++nprim;
-                const double t = x_prim_t(rec.h, o, d, MX_TMIN);
+                const double t = x_prim_t<TRI>(rec.h, o, d, MX_TMIN);
                 const int pi = rec.h.prim;
                 if (phase != PH_CLOSEST) {
                     if (t < tmax) { best = pi; raying = false; return; }   // any hit occludes
@@ -1188,8 +1234,8 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             for (int j = 0; j < cntl; j += 2) {
                 const bool two = j + 1 < cntl;
                 const XHotR r0 = load_hot(hp + j), r1 = load_hot(hp + (two ? j + 1 : j));
-                const double ta = x_prim_t(r0.h, o, d, MX_TMIN);
-                const double tb = two ? x_prim_t(r1.h, o, d, MX_TMIN) : INFINITY;
+                const double ta = x_prim_t<TRI>(r0.h, o, d, MX_TMIN);
+                const double tb = two ? x_prim_t<TRI>(r1.h, o, d, MX_TMIN) : INFINITY;
                 nprim += two ? 2 : 1;
                 if (phase != PH_CLOSEST) {
                     if (ta < tmax || tb < tmax) {   // any hit occludes
@@ -1245,8 +1291,13 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
         const bool trav = raying;
         const unsigned long long m_trav = __ballot(trav);
         const int n_wait = __popcll(m_live & ~m_trav);
-        const bool handle = phase != PH_DEAD && !trav &&
-                            (8 * n_wait >= handle8 * __popcll(m_live) || m_trav == 0);
+        // SPEC: a lane whose hit waits for shading is ready for the handler even while its shadow
+        // ray runs; the handler runs once the ready share of the live lanes reaches handle8 eighths,
+        // or when no lane traces anything else
+        const bool ready = phase != PH_DEAD && (!trav || (SPEC && need_shade));
+        const unsigned long long m_busy = SPEC ? __ballot(trav && !need_shade) : m_trav;
+        const int n_ready = SPEC ? __popcll(__ballot(ready)) : n_wait;
+        const bool handle = ready && (8 * n_ready >= handle8 * __popcll(m_live) || m_busy == 0);
         if (STATS) {   // ballots over the whole wave, accumulated by lane 0
             const unsigned long long m_h = __ballot(handle);
             const unsigned long long m_hc = __ballot(handle && phase == PH_CLOSEST);
@@ -1384,8 +1435,24 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     cnt.ln_rs += __popcll(mr);
                 }
             }
-            if (inline_shadow && !raying && phase == PH_SHADOW && has_next) {
+            // SPEC: a closest ray that has just found its hit starts the hit's shadow ray here
+            const bool spec_start = SPEC && !raying && phase == PH_CLOSEST && best >= 0;
+            if ((inline_shadow && !raying && phase == PH_SHADOW && has_next && !(SPEC && need_shade)) || spec_start) {
                 ++nrays;
+                if (spec_start) {   // the shading's own P, light direction and distance (pixel_mode_x)
+                    const V3 P = o + tbest * d;
+                    const V3 lv = light - P;
+                    const double ldist = gsqrt(dot(lv, lv));
+                    reinterpret_cast<int*>(pslot)[0] = best;   // free until the shading writes Lo there
+                    pslot[3] = d.x; pslot[4] = d.y; pslot[5] = d.z;
+                    need_shade = true;
+                    o = P;
+                    d = normalize(lv);
+                    phase = PH_SHADOW;
+                    tmax = ldist;
+                    tbest = ldist;
+                    tbest_f = up32(ldist);
+                } else {
                 if (best >= 0) Lv = PSL ? v3(pslot[0], pslot[1], pslot[2]) : Lo;   // occluded: ambient term only
                 d = PSL ? v3(pslot[3], pslot[4], pslot[5]) : nextd;                // o is still the hit point
                 ++b;
@@ -1393,6 +1460,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 tmax = INFINITY;
                 tbest = INFINITY;
                 tbest_f = INFINITY;
+                }
                 of = f3((float)o.x, (float)o.y, (float)o.z);
                 ivf = inv_dir(d);
                 dmask = (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
@@ -1408,6 +1476,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     lvl_set<SH>(mlo, mhi, 0, rm);
                     raying = rm != 0;
                 }
+                if (spec_start && no_shadow) raying = false;   // GI_FLAG_X_NO_SHADOW: always lit
             }
             }
         }
@@ -1435,25 +1504,38 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
         if (handle && !hold && phase != PH_DEAD) {
             // ---- the lane's ray is finished: consume it, spawn the next one --------------------
             bool end_path = false;
-            if (phase == PH_CLOSEST) {
-                ++nrays;
-                if (best < 0) {
+            bool keep_ray = false;   // SPEC: the lane's shadow ray is still in flight after its shading
+            const bool sh = SPEC && need_shade;   // SPEC: shade the hit whose shadow ray is under way
+            if (sh || phase == PH_CLOSEST) {
+                if (!sh) ++nrays;
+                if (!sh && best < 0) {
                     end_path = true;
                 } else {
-                    const XPrim& p = XP[best];   // by reference: only used fields are loaded
+                    // the hit: primitive, incoming direction, point -- for SPEC lanes kept from the
+                    // step that found it (the shadow ray's origin is the hit point o + tbest * d)
+                    const int hb = sh ? reinterpret_cast<const int*>(pslot)[0] : best;
+                    const V3 din = sh ? v3(pslot[3], pslot[4], pslot[5]) : d;
+                    const V3 P = sh ? o : o + tbest * d;
+                    const XPrim& p = XP[hb];   // by reference: only used fields are loaded
                     const REnt& e = EN[p.ent];
-                    const V3 P = o + tbest * d;
-                    V3 N = p.kind == 0 ? ld3(p.n) : normalize(P - ld3(p.a));
-                    if (!(dot(d, N) < 0)) N = -N;
+                    V3 N = (TRI || p.kind == 0) ? ld3(p.n) : normalize(P - ld3(p.a));
+                    if (!(dot(din, N) < 0)) N = -N;
                     int32_t tu, tv;
-                    x_texcoord(sc, e, P, tu, tv);
+                    x_texcoord<TRI>(sc, e, P, tu, tv);
                     const V3 tc = texel(ld3(e.color), tu, tv);
-                    const V3 lv = light - P;
-                    const double ldist = gsqrt(dot(lv, lv));
-                    const V3 Ld = normalize(lv);
+                    V3 Ld;
+                    double ldist;
+                    if (sh) {   // the shadow ray is (P, normalize(light - P), |light - P|)
+                        Ld = d;
+                        ldist = tmax;
+                    } else {
+                        const V3 lv = light - P;
+                        ldist = gsqrt(dot(lv, lv));
+                        Ld = normalize(lv);
+                    }
                     const V3 la = tc * e.shader[0];
                     const V3 ldf = (smax(0.0, dot(N, Ld)) * (tc * 0.5)) * e.shader[1];
-                    const V3 bis = normalize(normalize(-d) + Ld);
+                    const V3 bis = normalize(normalize(-din) + Ld);
                     const double spw = mx_pow(smax(0.0, dot(N, bis)), e.spec_pow);
                     const V3 ls = v3(spw, spw, spw) * e.shader[2];
                     const V3 lo = (la + ldf) + ls;
@@ -1467,7 +1549,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     const bool mirror = b != depth - 1 && e.refl > 0.0 &&
                                         mx_u01k(PSL ? reinterpret_cast<const uint64_t*>(pslot)[9] : key, smp, b, 4) < e.refl;
                     if (mirror) {
-                        nextd = normalize(d - N * (2.0 * dot(d, N)));
+                        nextd = normalize(din - N * (2.0 * dot(din, N)));
                         if (PSL) { pslot[3] = nextd.x; pslot[4] = nextd.y; pslot[5] = nextd.z; }
                         has_next = true;
                     } else if (b != depth - 1) {
@@ -1492,7 +1574,26 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     // shadow ray toward the point light: handed to an idle lane of the wave when the
                     // path continues and one is free (the k-th giver takes the k-th idle lane), the
                     // lane then starts its next bounce at once; else traced here first
-                    bool give = handoff && has_next;
+                    if (sh) {   // the shadow answer: now, or when the ray ends (inline restart)
+                        need_shade = false;
+                        if (raying) {
+                            keep_ray = true;
+                        } else {
+                            ++nrays;
+                            if (best >= 0) Lv = v3(pslot[0], pslot[1], pslot[2]);   // occluded: ambient only
+                            if (!has_next) {
+                                end_path = true;
+                            } else {
+                                d = v3(pslot[3], pslot[4], pslot[5]);   // o is still the hit point
+                                ++b;
+                                phase = PH_CLOSEST;
+                                tmax = INFINITY;
+                                tbest = INFINITY;
+                                tbest_f = INFINITY;
+                            }
+                        }
+                    }
+                    bool give = !sh && handoff && has_next;
                     if (HELP) {
                         const unsigned long long m_give = __ballot(give);
                         if (give) {
@@ -1517,7 +1618,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                             }
                         }
                     }
-                    if (!give) {
+                    if (!give && !sh) {
                         phase = PH_SHADOW;
                         o = P;
                         d = Ld;
@@ -1565,6 +1666,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             // GI_X_START_BURST primary rays per lane per handler run.
             int burst = 0;
             for (;;) {
+                if (SPEC && keep_ray) break;   // still tracing its shadow ray: no new ray
                 if (STATS) {
                     const unsigned long long mb = __ballot(true);
                     if (lane == 0) {
@@ -1768,7 +1870,7 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
         // (occluded sum, next direction, throughput T, RNG key) live in a per-lane LDS slot after
         // the scene instead of in VGPRs / scratch
         double* pslot = reinterpret_cast<double*>(lds_scene + nw + nh + np + ne) + 10 * threadIdx.x;
-        mode_x_wave<STATS, GI_X_PAIR != 0, W4 && GI_X_PSL, false, false, SH, GI_X_LEAFQ_LDS != 0>(sc, W, H, XP, EN, pslot, nullptr, XHelp{},
+        mode_x_wave<STATS, GI_X_PAIR != 0, W4 && GI_X_PSL, false, false, SH, GI_X_LEAFQ_LDS != 0, W4 && GI_X_TRI>(sc, W, H, XP, EN, pslot, nullptr, XHelp{},
                                                                         cam, light, m, spp, depth, seed, rgb, rgb8, blk,
                                                                         wk, handle8, xflags, c);
     } else {
@@ -1781,12 +1883,12 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
         hp.res = hp.own + 256;
         if constexpr (CN)   // quantised nodes (the default for large HBM-resident scenes); LQ in
                             // long launches (the handoff build's short launches are latency-bound)
-            mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0, SH, GI_X_LEAFQ != 0 && !W4>(sc, sc.xcnodes, sc.xhot, sc.xprims,
+            mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0, SH, GI_X_LEAFQ != 0 && !W4, false>(sc, sc.xcnodes, sc.xhot, sc.xprims,
                                                                             sc.ents, nullptr, lds_nst + threadIdx.x, hp,
                                                                             cam, light, m, spp, depth, seed, rgb, rgb8,
                                                                             blk, wk, handle8, xflags, c);
         else
-            mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0, SH, false>(sc, sc.xwnodes, sc.xhot, sc.xprims,
+            mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0, SH, false, false>(sc, sc.xwnodes, sc.xhot, sc.xprims,
                                                                             sc.ents, nullptr, lds_nst + threadIdx.x, hp,
                                                                             cam, light, m, spp, depth, seed, rgb, rgb8,
                                                                             blk, wk, handle8, xflags, c);

@@ -14,8 +14,9 @@ grows ("scaling": "strong").
 
 Default workload C3 (BASELINE.json configs[2]): Cornell box (34 ImpTriangles), 1920x1080,
 depth 8, 64 spp, Mode X (the build-defined integrator: the reference itself renders depth 1 only).
-`value` = total rays traced (primary + bounce + shadow, all ranks) per second, inputs resident in
-HBM.  The ray count per frame is exact: a counting launch (GI_FLAG_STATS) of the same
+`value` = rays traced (primary + bounce + shadow rays that reached the BVH, all ranks) per second,
+inputs resident in HBM; `mray_s_all_rays` also counts the primary samples resolved
+exactly without traversal.  The ray count per frame is exact: a counting launch (GI_FLAG_STATS) of the same
 deterministic frame runs before the timed region.
 
 roofline: the dominant kernel (k_mode_x) against HBM: achieved = algorithmic bytes per launch
@@ -217,23 +218,44 @@ def reference_cpu(scn_text, w, h):
             "sample": f"depth 1 (the reference's only depth), every {stride}th pixel, {r['rays']} rays"}
 
 
-def host_path(dev, cam, light, w, h, mode, spp, depth, seed, reps=3):
+def host_path(gi, sc, dev, cam, light, w, h, mode, spp, depth, seed, reps=3):
     """gi_render with host buffers (the drop-in RayTracer's path): render + PCIe copy-back, ms per
-    frame.  Reported beside `value`, never as it (inputs are not HBM-resident here)."""
+    frame, and the same frame through gi_multi_render (the drop-in's GI_DEVICES route) on this one
+    device: two tile shards on it, and one shard whose tiles travel through RCCL to itself
+    (GI_MULTI_RCCL=1).  Reported beside `value`, never as it (inputs are not HBM-resident here)."""
     import numpy as np
     rgb = np.empty((h, w, 3), np.float64)
     rgb8 = np.empty((h, w, 3), np.uint8)
     res = {}
-    for name, out, band in (("rgb8", (None, rgb8), 0), ("rgb8+fp64", (rgb, rgb8), 0),
-                            ("rgb8_bands32", (None, rgb8), 32)):
-        dev.render(cam, light, w, h, mode=mode, spp=spp, depth=depth, seed=seed, band_rows=band, out=out)   # warm
+
+    def timed(name, fn, out, band):
+        fn(cam, light, w, h, mode=mode, spp=spp, depth=depth, seed=seed, band_rows=band, out=out)   # warm
         t = time.perf_counter()
         for _ in range(reps):
-            dev.render(cam, light, w, h, mode=mode, spp=spp, depth=depth, seed=seed, band_rows=band, out=out)
+            fn(cam, light, w, h, mode=mode, spp=spp, depth=depth, seed=seed, band_rows=band, out=out)
         res[name] = round((time.perf_counter() - t) / reps * 1e3, 3)
-    return {"ms_per_frame": res, "note": "gi_render into host buffers: PCIe copy-back included (rgb8 = the "
-            "reference Image's RGB888; +fp64 radiance; bands32 = 32-row progressive bands as the drop-in "
-            "RayTracer::run uses); not `value`"}
+
+    for name, out, band in (("rgb8", (None, rgb8), 0), ("rgb8+fp64", (rgb, rgb8), 0),
+                            ("rgb8_bands32", (None, rgb8), 32), ("rgb8+fp64_bands32", (rgb, rgb8), 32)):
+        timed(name, dev.render, out, band)
+    multi = {}
+    try:
+        m2 = gi.MultiScene.from_scene(sc, [0, 0])
+        timed("multi_2shards_1dev_rgb8+fp64_bands32", m2.render, (rgb, rgb8), 32)
+        m2.close()
+        os.environ["GI_MULTI_RCCL"] = "1"   # read by gi_multi_create
+        m1 = gi.MultiScene.from_scene(sc, [0])
+        del os.environ["GI_MULTI_RCCL"]
+        if m1.info()["rccl"]:
+            timed("multi_rccl_self_rgb8+fp64_bands32", m1.render, (rgb, rgb8), 32)
+            timed("multi_rccl_self_rgb8+fp64", m1.render, (rgb, rgb8), 0)
+        m1.close()
+    except Exception as e:   # never fail the bench on this side measurement
+        multi["error"] = str(e)[:200]
+    return {"ms_per_frame": res, **multi,
+            "note": "host buffers: PCIe copy-back included (rgb8 = the reference Image's RGB888; +fp64 "
+                    "radiance; bands32 = 32-row progressive bands as the drop-in RayTracer::run uses; multi_* "
+                    "= gi_multi_render, the drop-in's GI_DEVICES route, on this one device); not `value`"}
 
 
 def main():
@@ -364,7 +386,12 @@ def main():
 
     if rank == 0:
         ms_frame = elapsed / args.steps * 1e3
-        value = rays_frame * args.steps / elapsed / 1e6
+        resolved = st[gi.STAT_X_RESOLVED] if mode == 1 else 0
+        # Mray/s = rays TRACED per second -- primary + bounce + shadow rays that
+        # reached the acceleration structure; the primary samples the pixel-frustum classify and the
+        # root-box pretest resolve without traversal (each adds exactly +0) are counted apart
+        rays_traced = rays_frame - resolved
+        value = rays_traced * args.steps / elapsed / 1e6
         # algorithmic bytes per launch of the dominant kernel (this rank's launch; N=1: the frame)
         node_bytes = dev.info()["x_node_bytes"] if mode == 1 else NODE_BYTES[0]
         alg = (st[gi.STAT_NODES] * node_bytes + st[gi.STAT_PRIMS] * PRIM_BYTES[mode] +
@@ -372,7 +399,6 @@ def main():
         achieved = alg / (kern_ms * 1e-3) / 1e9
         ceil = counter_ceilings(args.workload, kern_ms) if world == 1 else None
         traffic = ceil.get("hbm_counter_bytes") if ceil else None
-        resolved = st[gi.STAT_X_RESOLVED] if mode == 1 else 0
         out = {
             "metric": "Mray/s + ms/frame at 1920x1080, depth 8; %HBM roofline",
             "value": round(value, 3),
@@ -384,6 +410,9 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
+            "value_basis": "rays traced per second (primary + bounce + shadow rays that reached the BVH, all "
+                           "ranks; SURVEY §8(d)); mray_s_all_rays adds the primary samples resolved exactly "
+                           "without traversal",
             "dtype": "f64",
             "data": "synthetic (procedural scene, no external data)",
             "config": {"workload": f"{args.workload}: {desc}", "mode": "X" if mode == 1 else "R", "width": w,
@@ -391,11 +420,11 @@ def main():
                        "rays_per_frame": rays_frame, "primary_rays_per_frame": w * h * spp,
                        # rays that reached the BVH: rays_per_frame minus the primary samples resolved
                        # by the pixel-frustum classify and the root-box pretest (each adds exactly +0)
-                       "rays_traced_per_frame": rays_frame - resolved,
+                       "rays_traced_per_frame": rays_traced,
                        "parallelism": f"tile-shard{world}"},
             # primary (w*h*spp) and total (primary + bounce + shadow) rays per second
             "mray_s_primary": round(w * h * spp * args.steps / elapsed / 1e6, 3),
-            "mray_s_traced": round((rays_frame - resolved) * args.steps / elapsed / 1e6, 3),
+            "mray_s_all_rays": round(rays_frame * args.steps / elapsed / 1e6, 3),
             "roofline": {"bound": "hbm", "kernel": "k_mode_x" if mode == 1 else "k_mode_r",
                          "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
@@ -446,7 +475,7 @@ def main():
                                                (("traverse", gi.STAT_X_CYC_TRAV), ("consume", gi.STAT_X_CYC_HIT),
                                                 ("next_ray", gi.STAT_X_CYC_NEXT))}}
         if world == 1 and not args.no_host_path:
-            out["host_path"] = host_path(dev, cam, sc.light, w, h, mode, spp, depth, args.seed)
+            out["host_path"] = host_path(gi, sc, dev, cam, sc.light, w, h, mode, spp, depth, args.seed)
             # SURVEY §8(d) ms/frame: the end-to-end gi_render time with the framebuffer's D2H copy
             # (RGB888, the reference Image's content) included
             out["ms_per_frame_with_d2h"] = out["host_path"]["ms_per_frame"]["rgb8"]

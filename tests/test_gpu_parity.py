@@ -509,6 +509,13 @@ def test_unshard_matches_host_layout(torch_cuda):
         assert (got[pp < 0] == 0).all()
 
 
+def test_gpu_run_loads_library_built_from_this_tree(torch_cuda):
+    """Provenance on the GPU box: the libgi.so this GPU process loaded was compiled from
+    the sources in the tree it runs from (gi_build_id == build.py source_hash)."""
+    from importlib import import_module
+    assert gi.build_id() == import_module("2019global_amd.build").source_hash()
+
+
 def test_expbox_node_test_kat_on_device(torch_cuda):
     z = np.load(os.path.join(GOLD, "boxes.npz"))
     got = gi.kat_expbox(z["recs"])
