@@ -371,9 +371,14 @@ int scene_create_on(const gi_scene_desc* desc, int device, gi_scene** out) {
         // (256 lanes x 80 B) and the per-wave unit blocks (4 x 68 x 4 B)
         const size_t per_wg = bytes + 256 * 10 * sizeof(double) + 4 * 68 * sizeof(unsigned);
         d.x_waves4 = (d.x_lds_bytes > 0 && 4 * per_wg <= 160 * 1024) ? 1 : 0;
+        d.x_tri_only = 1;
         for (const REnt& r : h.ents)
-            if (r.kind == K_IMP_SPHERE || r.kind == K_EXP_SPHERE || r.kind == K_EXP_CONE || r.kind == K_EXP_RECTANGLE)
+            if (r.kind == K_IMP_SPHERE || r.kind == K_EXP_SPHERE || r.kind == K_EXP_CONE || r.kind == K_EXP_RECTANGLE) {
                 d.x_waves4 = 0;
+                d.x_tri_only = 0;
+            }
+        for (const XPrim& xp : h.xprims)
+            if (xp.kind != 0) d.x_tri_only = 0;
     }
     // HBM-resident scenes whose XWNode tree outgrows an XCD's L2 share (> 2 MB) traverse quantised
     // nodes (XCNode: one 128-byte line per node instead of two): C5 287 -> 270 ms; the 1k soup, whose

@@ -1838,7 +1838,9 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
 // 2.64 ms, with spread work groups 2.40 ms); in long launches (C5) the handoff build's heavier code
 // costs 8%, so they run without.
 // CN (HBM-resident scenes): traverse the quantised nodes (DevScene::xcnodes) instead of XWNode.
-template <bool STATS, bool LDS, bool W4, bool CN, bool SH>
+// TR (HBM-resident scenes): the scene is triangle meshes of the 4-wave kinds only (DevScene::x_tri_only,
+// e.g. the 100k soup): mode_x_wave's TRI specialisation
+template <bool STATS, bool LDS, bool W4, bool CN, bool SH, bool TR = false>
 __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WAVES) void k_mode_x(DevScene sc, CamDev cam, V3 light, TileMap m, int spp, int depth,
                                                  uint64_t seed, double* rgb, uint8_t* rgb8,
                                                  unsigned long long* stats, XWork wk, int handle8, int xflags) {
@@ -1883,12 +1885,12 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
         hp.res = hp.own + 256;
         if constexpr (CN)   // quantised nodes (the default for large HBM-resident scenes); LQ in
                             // long launches (the handoff build's short launches are latency-bound)
-            mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0, SH, GI_X_LEAFQ != 0 && !W4, false>(sc, sc.xcnodes, sc.xhot, sc.xprims,
+            mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0, SH, GI_X_LEAFQ != 0 && !W4, TR && GI_X_TRI>(sc, sc.xcnodes, sc.xhot, sc.xprims,
                                                                             sc.ents, nullptr, lds_nst + threadIdx.x, hp,
                                                                             cam, light, m, spp, depth, seed, rgb, rgb8,
                                                                             blk, wk, handle8, xflags, c);
         else
-            mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0, SH, false, false>(sc, sc.xwnodes, sc.xhot, sc.xprims,
+            mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0, SH, false, TR && GI_X_TRI>(sc, sc.xwnodes, sc.xhot, sc.xprims,
                                                                             sc.ents, nullptr, lds_nst + threadIdx.x, hp,
                                                                             cam, light, m, spp, depth, seed, rgb, rgb8,
                                                                             blk, wk, handle8, xflags, c);
@@ -2096,7 +2098,9 @@ hipError_t x_launch_config(const DevScene& sc, int device, XLaunchCfg& cfg) {
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
         &per_cu, cfg.kv == 3 ? reinterpret_cast<const void*>(k_mode_x<false, true, true, false, false>)
                  : cfg.kv == 2 ? reinterpret_cast<const void*>(k_mode_x<false, true, false, false, false>)
-                 : sc.xcnodes  ? reinterpret_cast<const void*>(k_mode_x<false, false, false, true, false>)
+                 : sc.xcnodes  ? (sc.x_tri_only ? reinterpret_cast<const void*>(k_mode_x<false, false, false, true, false, true>)
+                                                : reinterpret_cast<const void*>(k_mode_x<false, false, false, true, false>))
+                 : sc.x_tri_only ? reinterpret_cast<const void*>(k_mode_x<false, false, false, false, false, true>)
                                : reinterpret_cast<const void*>(k_mode_x<false, false, false, false, false>),
         64 * kWavesPerBlock, cfg.lds_bytes);
     if (e != hipSuccess) return e;
@@ -2179,10 +2183,13 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
                        ((o.flags & GI_FLAG_X_NO_SHADOW) ? 4 : 0) | (env.help ? 8 : 0) |
                        ((env.spread > 0 || (env.spread < 0 && help)) ? 16 : 0) | (env.leaf8 << 12);
         const bool cn = kv < 2 && sc.xcnodes != nullptr;
-#define GI_LAUNCH_X1(S, L, W, SH) hipLaunchKernelGGL((k_mode_x<S, L, W, false, SH>), pgrid, block, lds_bytes, stream, sc, cam, light, m, o.spp, \
+#define GI_LAUNCH_X2(S, L, W, SH, TR) hipLaunchKernelGGL((k_mode_x<S, L, W, false, SH, TR>), pgrid, block, lds_bytes, stream, sc, cam, light, m, o.spp, \
                                            o.depth, o.seed, rgb, rgb8, st, wk, h8, xf)
-#define GI_LAUNCH_XC1(S, W, SH) hipLaunchKernelGGL((k_mode_x<S, false, W, true, SH>), pgrid, block, lds_bytes, stream, sc, cam, light, m, \
+#define GI_LAUNCH_XC2(S, W, SH, TR) hipLaunchKernelGGL((k_mode_x<S, false, W, true, SH, TR>), pgrid, block, lds_bytes, stream, sc, cam, light, m, \
                                           o.spp, o.depth, o.seed, rgb, rgb8, st, wk, h8, xf)
+        // TR: triangle-only HBM-resident scenes (the LDS kernels do not use it: theirs is W4)
+#define GI_LAUNCH_X1(S, L, W, SH) do { if (!(L) && sc.x_tri_only) GI_LAUNCH_X2(S, L, W, SH, true); else GI_LAUNCH_X2(S, L, W, SH, false); } while (0)
+#define GI_LAUNCH_XC1(S, W, SH) do { if (sc.x_tri_only) GI_LAUNCH_XC2(S, W, SH, true); else GI_LAUNCH_XC2(S, W, SH, false); } while (0)
         // SH: the per-level masks in one 64-bit word when the tree has at most 8 levels
         const bool sh = sc.x_max_depth <= 7;
 #define GI_LAUNCH_X(S, L, W) do { if (sh) GI_LAUNCH_X1(S, L, W, true); else GI_LAUNCH_X1(S, L, W, false); } while (0)
@@ -2202,6 +2209,8 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
 #undef GI_LAUNCH_XC
 #undef GI_LAUNCH_X1
 #undef GI_LAUNCH_XC1
+#undef GI_LAUNCH_X2
+#undef GI_LAUNCH_XC2
         if (o.spp > 1) hipLaunchKernelGGL(k_x_reduce, sgrid, dim3(256), 0, stream, m, wk, o.spp, rgb, rgb8);
     }
     if (timed) kt->recorded++;

@@ -88,7 +88,10 @@ class RayTracer {
         o.depth = _integ.depth;
         o.seed = _integ.seed;
         o.shard_count = 1;
-        o.band_rows = 32;
+        // progressive bands: 32 rows for the reference's integrator (as cheap per row as the
+        // reference's own loop is slow); the path tracer's bands are an eighth of the frame, since
+        // each band is a launch that ends on its longest path (C4 in 32-row bands: 8x the frame)
+        o.band_rows = _integ.mode == GI_MODE_X ? std::max(32, (h + 63) / 64 * 8) : 32;
         Band band{_image.get(), w, _keep_radiance ? &_radiance : nullptr};
         if (_keep_radiance) _radiance.assign((size_t)w * h * 3, 0.0);
         const int rc = _gpu->multi ? gi_multi_render(_gpu->multi, &cam, light, w, h, &o, nullptr, nullptr, &_cancel,
