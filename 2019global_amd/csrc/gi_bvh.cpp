@@ -62,6 +62,9 @@ struct Builder {
     // the extra binary levels); 2 and 4 are 15-20% slower; the Cornell box and the 1k soup are
     // unchanged within noise.
     double kTraverse = 0.35;
+    // > 0: every binary node at this depth is a leaf (GI_XFLAT, tuning knob for tiny scenes: depth 3
+    // gives at most 8 leaves, i.e. one wide root whose children are all leaves)
+    int flat_depth = 0;
 
     int build(int first, int count, int depth) {
         const int ni = (int)nodes.size();
@@ -77,7 +80,7 @@ struct Builder {
         nodes[ni].box = box;
         nodes[ni].first = first;
         nodes[ni].count = count;
-        if (count <= 1 || depth > 60) return ni;
+        if (count <= 1 || depth > 60 || (flat_depth > 0 && depth >= flat_depth)) return ni;
         // binned SAH over the centroid bounds
         int best_axis = -1, best_split = -1;
         double best_cost = INFINITY;
@@ -191,6 +194,8 @@ void build_xbvh(const std::vector<XPrim>& prims, const std::vector<double>& boun
     b.leaf_max = std::max(1, leaf_max);
     if (const char* ct = std::getenv("GI_XSAH_CT")) b.kTraverse = std::atof(ct);   // tuning knobs
     if (const char* nb = std::getenv("GI_XSAH_BINS")) b.kBins = std::max(2, std::min(Builder::kMaxBins, std::atoi(nb)));
+    if (const char* fl = std::getenv("GI_XFLAT"))
+        if (np <= 64) b.flat_depth = std::max(0, std::min(6, std::atoi(fl)));
     b.order.resize(np);
     b.cen.resize(3 * np);
     for (size_t i = 0; i < np; ++i) {

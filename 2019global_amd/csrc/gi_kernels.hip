@@ -1041,6 +1041,9 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 #ifndef GI_X_TRI
 #define GI_X_TRI 1   // 4-wave LDS kernel: triangle-only primitive tests and texture mapping (TRI)
 #endif
+#ifndef GI_X_MERGE
+#define GI_X_MERGE 0   // LDS kernel: interior-node and restart root tests in one block per step
+#endif
 #ifndef GI_X_SPEC
 // speculative shadow rays (LDS scenes with path slots, i.e. the Cornell-class kernel): a closest
 // ray that finds a hit starts its shadow ray at once, inside the traversal step, instead of
@@ -1193,6 +1196,11 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     int poff = 0, pcnt = 0;   // LQ: the pending leaf (records H[poff .. poff + pcnt)), pcnt 0: none
     bool pdone = false;       // LQ: the ray ends once its pending leaf is tested
     bool rootp = false;       // RSPEND: the lane's next step is its restarted ray's root test
+    // MERGE (LDS kernel, no LQ): the step's interior-node test and a restarted ray's root test share
+    // one children_mask call at the end of the step
+    constexpr bool MERGE = GI_X_MERGE != 0 && PAIR && !LQ && !NST;
+    bool desc = false, rs = false;   // MERGE: this step descends into xch / restarts at the root
+    int xch = 0;
     const int leaf8 = ((xflags >> 12) & 15) ? ((xflags >> 12) & 15) : GI_X_LEAF8;
     uint64_t mlo = 0, mhi = 0;
     double tbest = INFINITY, tmax = INFINITY;
@@ -1351,12 +1359,14 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             const auto* nd = W + node;
             int c = 0, ch = 0;   // RSPEND root step: "child" 0 = the root wide node itself
             bool keep = true;
+            desc = false;
             if (!(GI_X_RSPEND && rootp)) {
                 const uint32_t msk = lvl_get<SH>(mlo, mhi, level);
                 const int kc = __builtin_ctz(msk);         // next child in front-to-back order
                 lvl_set<SH>(mlo, mhi, level, msk & (msk - 1));
                 c = kc ^ dmask;
                 ch = nd->child[c];
+                xch = ch;
                 // a closer hit may have arrived since the mask was computed: re-cull this child
                 if (phase == PH_CLOSEST && best >= 0) keep = child_hit(nd, c, of, ivf, tbest_f);
             }
@@ -1375,6 +1385,8 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     pcnt = nd->cnt[c];
                 } else if (ch < 0) {      // leaf: fp64 primitive tests (these decide the result)
                     leaf_test(H + ~ch, (int)nd->cnt[c]);
+                } else if (MERGE) {       // the node test runs below, shared with the restarts
+                    desc = true;
                 } else {                  // descend if any of the child's 8 children is hit (fp32)
                     if (!(GI_X_RSPEND && rootp)) ++nnode;   // (root tests are not node visits)
                     const uint32_t cm = children_mask<PAIR>(W + ch, of, ivf, tbest_f, dmask);
@@ -1393,7 +1405,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     }
                 }
             }
-            if (raying) {                 // climb to the nearest level with children left
+            if (raying && !desc) {        // climb to the nearest level with children left
                 uint32_t rest = lvl_get<SH>(mlo, mhi, level);
                 if constexpr (NST) {
                     if (rest == 0 && level > 0) {
@@ -1465,7 +1477,9 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 ivf = inv_dir(d);
                 dmask = (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
                 best = -1;
-                if (GI_X_RSPEND) {   // the root test waits for the next step's shared node test
+                if (MERGE) {         // the root test runs in the shared node test below
+                    rs = true;
+                } else if (GI_X_RSPEND) {   // the root test waits for the next step's shared node test
                     rootp = true;
                     raying = true;
                 } else {
@@ -1477,6 +1491,34 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     raying = rm != 0;
                 }
                 if (spec_start && no_shadow) raying = false;   // GI_FLAG_X_NO_SHADOW: always lit
+            }
+            // MERGE: one node test per step for the lanes that descend into an interior child and
+            // the lanes whose next bounce starts here (the root) -- one block instead of two
+            if (MERGE && (desc || rs)) {
+                if (desc) ++nnode;
+                const uint32_t cm = children_mask<PAIR>(W + (rs ? 0 : xch), of, ivf, tbest_f, dmask);
+                if (rs) {
+                    node = 0;
+                    level = 0;
+                    mlo = mhi = 0;
+                    lvl_set<SH>(mlo, mhi, 0, cm);
+                    raying = cm != 0;
+                } else if (cm) {
+                    node = xch;
+                    ++level;
+                    lvl_set<SH>(mlo, mhi, level, cm);
+                } else {   // the child's children all missed: climb as an unmerged step would have
+                    uint32_t rest = lvl_get<SH>(mlo, mhi, level);
+                    while (rest == 0 && level > 0) {
+                        --level;
+                        node = level == 0 ? 0 : W[node].parent;
+                        rest = lvl_get<SH>(mlo, mhi, level);
+                    }
+                    // a ray that ends here waits for the handler (which continues a shadow ray's path)
+                    if (rest == 0) raying = false;
+                }
+                rs = false;
+                desc = false;
             }
             }
         }
