@@ -1033,25 +1033,13 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 #ifndef GI_X_LEAFQ_LDS
 #define GI_X_LEAFQ_LDS 0   // LDS-resident scenes: leaf postponement as above (leaf tests two at a time)
 #endif
-#ifndef GI_X_RSPEND
-// inline bounce restart (short-traversal scenes): the new ray's root test runs as the next
-// traversal step, in the node-test code the descending lanes run, instead of in a block of its own
-#define GI_X_RSPEND 0
-#endif
 #ifndef GI_X_TRI
 #define GI_X_TRI 1   // 4-wave LDS kernel: triangle-only primitive tests and texture mapping (TRI)
 #endif
 #ifndef GI_X_MERGE
-#define GI_X_MERGE 0   // LDS kernel: interior-node and restart root tests in one block per step
-#endif
-#ifndef GI_X_SPEC
-// speculative shadow rays (LDS scenes with path slots, i.e. the Cornell-class kernel): a closest
-// ray that finds a hit starts its shadow ray at once, inside the traversal step, instead of
-// waiting idle for the wave's shading handler; the handler shades the hit whenever it next runs
-// (the shadow ray's origin, direction and length are the hit point, light direction and distance
-// the shading uses -- the same values) and the shadow answer is applied when both are known.
-// Lanes that used to wait for the handler trace their shadow ray meanwhile.
-#define GI_X_SPEC 0
+// 4-wave LDS kernel: a step's interior-node test and a restarted ray's root test in one block
+// (C3 6.08 -> 5.81 ms; the 3-wave LDS kernel of the every-entity scene is 2-4% slower with it)
+#define GI_X_MERGE 1
 #endif
 #ifndef GI_X_LEAF8
 #define GI_X_LEAF8 3   // LQ: leaf phase once 3/8 of the traversing lanes hold a leaf (C5 sweep 1-8)
@@ -1195,10 +1183,9 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     bool raying = false;
     int poff = 0, pcnt = 0;   // LQ: the pending leaf (records H[poff .. poff + pcnt)), pcnt 0: none
     bool pdone = false;       // LQ: the ray ends once its pending leaf is tested
-    bool rootp = false;       // RSPEND: the lane's next step is its restarted ray's root test
     // MERGE (LDS kernel, no LQ): the step's interior-node test and a restarted ray's root test share
     // one children_mask call at the end of the step
-    constexpr bool MERGE = GI_X_MERGE != 0 && PAIR && !LQ && !NST;
+    constexpr bool MERGE = GI_X_MERGE != 0 && PAIR && PSL && !LQ && !NST;
     bool desc = false, rs = false;   // MERGE: this step descends into xch / restarts at the root
     int xch = 0;
     const int leaf8 = ((xflags >> 12) & 15) ? ((xflags >> 12) & 15) : GI_X_LEAF8;
@@ -1212,11 +1199,6 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     V3 Lv = v3(0, 0, 0), Lo = v3(0, 0, 0), T = v3(1, 1, 1);
     V3 nextd = v3(0, 0, 0);   // carried across the shadow ray (its origin = the shadow ray's)
     bool has_next = false;
-    // SPEC: the lane's closest hit waits for shading while its shadow ray runs; the hit's primitive
-    // and incoming direction are kept in the path slot (pslot[0] as int, pslot[3..5]: free until the
-    // shading writes Lo and the next direction there)
-    constexpr bool SPEC = GI_X_SPEC != 0 && PSL && !HELP && !LQ;
-    bool need_shade = false;
 
     // fp64 primitive tests of one leaf's records hp[0 .. cntl) (these decide the result): global
     // records fetched one ahead of the test; LDS records (PAIR) two at a time, the two fp64
@@ -1299,13 +1281,8 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
         const bool trav = raying;
         const unsigned long long m_trav = __ballot(trav);
         const int n_wait = __popcll(m_live & ~m_trav);
-        // SPEC: a lane whose hit waits for shading is ready for the handler even while its shadow
-        // ray runs; the handler runs once the ready share of the live lanes reaches handle8 eighths,
-        // or when no lane traces anything else
-        const bool ready = phase != PH_DEAD && (!trav || (SPEC && need_shade));
-        const unsigned long long m_busy = SPEC ? __ballot(trav && !need_shade) : m_trav;
-        const int n_ready = SPEC ? __popcll(__ballot(ready)) : n_wait;
-        const bool handle = ready && (8 * n_ready >= handle8 * __popcll(m_live) || m_busy == 0);
+        const bool handle = phase != PH_DEAD && !trav &&
+                            (8 * n_wait >= handle8 * __popcll(m_live) || m_trav == 0);
         if (STATS) {   // ballots over the whole wave, accumulated by lane 0
             const unsigned long long m_h = __ballot(handle);
             const unsigned long long m_hc = __ballot(handle && phase == PH_CLOSEST);
@@ -1357,19 +1334,16 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             // the current level has a child left; the step pops it, then climbs past exhausted
             // levels, so a ray ends in the step that exhausts the root level (no empty iteration).
             const auto* nd = W + node;
-            int c = 0, ch = 0;   // RSPEND root step: "child" 0 = the root wide node itself
-            bool keep = true;
+            const uint32_t msk = lvl_get<SH>(mlo, mhi, level);
+            const int kc = __builtin_ctz(msk);         // next child in front-to-back order
+            lvl_set<SH>(mlo, mhi, level, msk & (msk - 1));
+            const int c = kc ^ dmask;
+            const int ch = nd->child[c];
+            xch = ch;
             desc = false;
-            if (!(GI_X_RSPEND && rootp)) {
-                const uint32_t msk = lvl_get<SH>(mlo, mhi, level);
-                const int kc = __builtin_ctz(msk);         // next child in front-to-back order
-                lvl_set<SH>(mlo, mhi, level, msk & (msk - 1));
-                c = kc ^ dmask;
-                ch = nd->child[c];
-                xch = ch;
-                // a closer hit may have arrived since the mask was computed: re-cull this child
-                if (phase == PH_CLOSEST && best >= 0) keep = child_hit(nd, c, of, ivf, tbest_f);
-            }
+            // a closer hit may have arrived since the mask was computed: re-cull this child
+            bool keep = true;
+            if (phase == PH_CLOSEST && best >= 0) keep = child_hit(nd, c, of, ivf, tbest_f);
             if (STATS) {
                 const unsigned long long mn = __ballot(keep && ch >= 0), ml = __ballot(keep && ch < 0);
                 if (lane == 0) {
@@ -1388,16 +1362,9 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 } else if (MERGE) {       // the node test runs below, shared with the restarts
                     desc = true;
                 } else {                  // descend if any of the child's 8 children is hit (fp32)
-                    if (!(GI_X_RSPEND && rootp)) ++nnode;   // (root tests are not node visits)
+                    ++nnode;
                     const uint32_t cm = children_mask<PAIR>(W + ch, of, ivf, tbest_f, dmask);
-                    if (GI_X_RSPEND && rootp) {   // the restarted ray's root mask: level 0
-                        rootp = false;
-                        node = 0;
-                        level = 0;
-                        mlo = mhi = 0;
-                        lvl_set<SH>(mlo, mhi, 0, cm);
-                        raying = cm != 0;         // no root child hit: finished
-                    } else if (cm) {
+                    if (cm) {
                         node = ch;
                         ++level;
                         lvl_set<SH>(mlo, mhi, level, cm);
@@ -1447,24 +1414,8 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     cnt.ln_rs += __popcll(mr);
                 }
             }
-            // SPEC: a closest ray that has just found its hit starts the hit's shadow ray here
-            const bool spec_start = SPEC && !raying && phase == PH_CLOSEST && best >= 0;
-            if ((inline_shadow && !raying && phase == PH_SHADOW && has_next && !(SPEC && need_shade)) || spec_start) {
+            if (inline_shadow && !raying && phase == PH_SHADOW && has_next) {
                 ++nrays;
-                if (spec_start) {   // the shading's own P, light direction and distance (pixel_mode_x)
-                    const V3 P = o + tbest * d;
-                    const V3 lv = light - P;
-                    const double ldist = gsqrt(dot(lv, lv));
-                    reinterpret_cast<int*>(pslot)[0] = best;   // free until the shading writes Lo there
-                    pslot[3] = d.x; pslot[4] = d.y; pslot[5] = d.z;
-                    need_shade = true;
-                    o = P;
-                    d = normalize(lv);
-                    phase = PH_SHADOW;
-                    tmax = ldist;
-                    tbest = ldist;
-                    tbest_f = up32(ldist);
-                } else {
                 if (best >= 0) Lv = PSL ? v3(pslot[0], pslot[1], pslot[2]) : Lo;   // occluded: ambient term only
                 d = PSL ? v3(pslot[3], pslot[4], pslot[5]) : nextd;                // o is still the hit point
                 ++b;
@@ -1472,16 +1423,12 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 tmax = INFINITY;
                 tbest = INFINITY;
                 tbest_f = INFINITY;
-                }
                 of = f3((float)o.x, (float)o.y, (float)o.z);
                 ivf = inv_dir(d);
                 dmask = (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
                 best = -1;
                 if (MERGE) {         // the root test runs in the shared node test below
                     rs = true;
-                } else if (GI_X_RSPEND) {   // the root test waits for the next step's shared node test
-                    rootp = true;
-                    raying = true;
                 } else {
                     const uint32_t rm = children_mask<PAIR>(W, of, ivf, tbest_f, dmask);
                     node = 0;
@@ -1490,7 +1437,6 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     lvl_set<SH>(mlo, mhi, 0, rm);
                     raying = rm != 0;
                 }
-                if (spec_start && no_shadow) raying = false;   // GI_FLAG_X_NO_SHADOW: always lit
             }
             // MERGE: one node test per step for the lanes that descend into an interior child and
             // the lanes whose next bounce starts here (the root) -- one block instead of two
@@ -1546,35 +1492,23 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
         if (handle && !hold && phase != PH_DEAD) {
             // ---- the lane's ray is finished: consume it, spawn the next one --------------------
             bool end_path = false;
-            bool keep_ray = false;   // SPEC: the lane's shadow ray is still in flight after its shading
-            const bool sh = SPEC && need_shade;   // SPEC: shade the hit whose shadow ray is under way
-            if (sh || phase == PH_CLOSEST) {
-                if (!sh) ++nrays;
-                if (!sh && best < 0) {
+            if (phase == PH_CLOSEST) {
+                ++nrays;
+                if (best < 0) {
                     end_path = true;
                 } else {
-                    // the hit: primitive, incoming direction, point -- for SPEC lanes kept from the
-                    // step that found it (the shadow ray's origin is the hit point o + tbest * d)
-                    const int hb = sh ? reinterpret_cast<const int*>(pslot)[0] : best;
-                    const V3 din = sh ? v3(pslot[3], pslot[4], pslot[5]) : d;
-                    const V3 P = sh ? o : o + tbest * d;
-                    const XPrim& p = XP[hb];   // by reference: only used fields are loaded
+                    const V3 din = d;   // the incoming direction
+                    const V3 P = o + tbest * d;
+                    const XPrim& p = XP[best];   // by reference: only used fields are loaded
                     const REnt& e = EN[p.ent];
                     V3 N = (TRI || p.kind == 0) ? ld3(p.n) : normalize(P - ld3(p.a));
                     if (!(dot(din, N) < 0)) N = -N;
                     int32_t tu, tv;
                     x_texcoord<TRI>(sc, e, P, tu, tv);
                     const V3 tc = texel(ld3(e.color), tu, tv);
-                    V3 Ld;
-                    double ldist;
-                    if (sh) {   // the shadow ray is (P, normalize(light - P), |light - P|)
-                        Ld = d;
-                        ldist = tmax;
-                    } else {
-                        const V3 lv = light - P;
-                        ldist = gsqrt(dot(lv, lv));
-                        Ld = normalize(lv);
-                    }
+                    const V3 lv = light - P;
+                    const double ldist = gsqrt(dot(lv, lv));
+                    const V3 Ld = normalize(lv);
                     const V3 la = tc * e.shader[0];
                     const V3 ldf = (smax(0.0, dot(N, Ld)) * (tc * 0.5)) * e.shader[1];
                     const V3 bis = normalize(normalize(-din) + Ld);
@@ -1616,26 +1550,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     // shadow ray toward the point light: handed to an idle lane of the wave when the
                     // path continues and one is free (the k-th giver takes the k-th idle lane), the
                     // lane then starts its next bounce at once; else traced here first
-                    if (sh) {   // the shadow answer: now, or when the ray ends (inline restart)
-                        need_shade = false;
-                        if (raying) {
-                            keep_ray = true;
-                        } else {
-                            ++nrays;
-                            if (best >= 0) Lv = v3(pslot[0], pslot[1], pslot[2]);   // occluded: ambient only
-                            if (!has_next) {
-                                end_path = true;
-                            } else {
-                                d = v3(pslot[3], pslot[4], pslot[5]);   // o is still the hit point
-                                ++b;
-                                phase = PH_CLOSEST;
-                                tmax = INFINITY;
-                                tbest = INFINITY;
-                                tbest_f = INFINITY;
-                            }
-                        }
-                    }
-                    bool give = !sh && handoff && has_next;
+                    bool give = handoff && has_next;
                     if (HELP) {
                         const unsigned long long m_give = __ballot(give);
                         if (give) {
@@ -1660,7 +1575,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                             }
                         }
                     }
-                    if (!give && !sh) {
+                    if (!give) {
                         phase = PH_SHADOW;
                         o = P;
                         d = Ld;
@@ -1708,7 +1623,6 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             // GI_X_START_BURST primary rays per lane per handler run.
             int burst = 0;
             for (;;) {
-                if (SPEC && keep_ray) break;   // still tracing its shadow ray: no new ray
                 if (STATS) {
                     const unsigned long long mb = __ballot(true);
                     if (lane == 0) {
