@@ -1036,6 +1036,9 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 #ifndef GI_X_TRI
 #define GI_X_TRI 1   // 4-wave LDS kernel: triangle-only primitive tests and texture mapping (TRI)
 #endif
+#ifndef GI_X_RECULL_INT_HBM
+#define GI_X_RECULL_INT_HBM 0   // HBM-resident scenes: re-cull popped interior children too
+#endif
 #ifndef GI_X_MERGE
 // 4-wave LDS kernel: a step's interior-node test and a restarted ray's root test in one block
 // (C3 6.08 -> 5.81 ms; the 3-wave LDS kernel of the every-entity scene is 2-4% slower with it)
@@ -1341,9 +1344,14 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             const int ch = nd->child[c];
             xch = ch;
             desc = false;
-            // a closer hit may have arrived since the mask was computed: re-cull this child
+            // a closer hit may have arrived since the mask was computed: re-cull this child -- in
+            // HBM-resident scenes only a leaf (GI_X_RECULL_INT_HBM 0): an interior child's own node
+            // test culls its children against the same t, and skipping its re-cull drops a node-
+            // record fetch and ~60 instructions from the step (C5 214 -> 208.7 ms; the LDS kernel,
+            // whose re-cull is cheaper than a node test, keeps it: C3 +0.9% without)
             bool keep = true;
-            if (phase == PH_CLOSEST && best >= 0) keep = child_hit(nd, c, of, ivf, tbest_f);
+            if (phase == PH_CLOSEST && best >= 0 && (PAIR || GI_X_RECULL_INT_HBM || ch < 0))
+                keep = child_hit(nd, c, of, ivf, tbest_f);
             if (STATS) {
                 const unsigned long long mn = __ballot(keep && ch >= 0), ml = __ballot(keep && ch < 0);
                 if (lane == 0) {
