@@ -1036,6 +1036,15 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 #ifndef GI_X_TRI
 #define GI_X_TRI 1   // 4-wave LDS kernel: triangle-only primitive tests and texture mapping (TRI)
 #endif
+#ifndef GI_X_PREFETCH
+#define GI_X_PREFETCH 1   // HBM-resident scenes: fetch the next pop's child reference a step ahead (PF)
+#endif
+#ifndef GI_X_RECULL_LEAF_HBM
+// HBM-resident scenes: re-cull popped leaves (0: a leaf's fp64 tests run against the best t as they
+// stand -- C5 208 -> 199 ms, C4 1.89 -> 1.82 ms: the re-cull's node-record fetch and ~60 instructions
+// cost more than the leaf tests it saves)
+#define GI_X_RECULL_LEAF_HBM 0
+#endif
 #ifndef GI_X_RECULL_INT_HBM
 #define GI_X_RECULL_INT_HBM 0   // HBM-resident scenes: re-cull popped interior children too
 #endif
@@ -1251,6 +1260,21 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
         }
     };
 
+    // PF (HBM-resident scenes): the next pop's child reference and leaf count are fetched at the
+    // end of the step that sets up the level (descend, climb or ray start), so the pop itself waits
+    // for no load: one dependent round trip per step (the child's node or leaf records) instead of
+    // two.  (lvl mask, node) do not change between that fetch and the pop.
+    constexpr bool PF = GI_X_PREFETCH != 0 && !PAIR;
+    int pf_ch = 0, pf_cnt = 0;
+    auto prefetch = [&]() {
+        const uint32_t m = lvl_get<SH>(mlo, mhi, level);
+        if (m) {
+            const int c = __builtin_ctz(m) ^ dmask;
+            pf_ch = W[node].child[c];
+            pf_cnt = W[node].cnt[c];
+        }
+    };
+
     const uint64_t t_begin = STATS ? clock64() : 0;
     for (;;) {
         if (HELP && any_gave && phase == PH_DEAD) {   // an idle lane given a shadow ray starts it
@@ -1275,6 +1299,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 mlo = mhi = 0;
                 lvl_set<SH>(mlo, mhi, 0, rm);
                 raying = rm != 0;
+                if (PF && raying) prefetch();
             }
         }
         const unsigned long long m_live = __ballot(phase != PH_DEAD);
@@ -1341,16 +1366,17 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             const int kc = __builtin_ctz(msk);         // next child in front-to-back order
             lvl_set<SH>(mlo, mhi, level, msk & (msk - 1));
             const int c = kc ^ dmask;
-            const int ch = nd->child[c];
+            const int ch = PF ? pf_ch : nd->child[c];
             xch = ch;
             desc = false;
             // a closer hit may have arrived since the mask was computed: re-cull this child -- in
-            // HBM-resident scenes only a leaf (GI_X_RECULL_INT_HBM 0): an interior child's own node
-            // test culls its children against the same t, and skipping its re-cull drops a node-
-            // record fetch and ~60 instructions from the step (C5 214 -> 208.7 ms; the LDS kernel,
-            // whose re-cull is cheaper than a node test, keeps it: C3 +0.9% without)
+            // the LDS kernel only (GI_X_RECULL_*_HBM 0): in HBM-resident scenes an interior child's
+            // own node test culls its children against the same t, and skipping the re-cull drops a
+            // node-record fetch and ~60 instructions from the step (C5 214 -> 199 ms, C4 1.96 ->
+            // 1.82; the LDS kernel, whose re-cull is cheaper than a node test, keeps it: C3 +0.9%
+            // without)
             bool keep = true;
-            if (phase == PH_CLOSEST && best >= 0 && (PAIR || GI_X_RECULL_INT_HBM || ch < 0))
+            if (phase == PH_CLOSEST && best >= 0 && (PAIR || GI_X_RECULL_INT_HBM || (ch < 0 && GI_X_RECULL_LEAF_HBM)))
                 keep = child_hit(nd, c, of, ivf, tbest_f);
             if (STATS) {
                 const unsigned long long mn = __ballot(keep && ch >= 0), ml = __ballot(keep && ch < 0);
@@ -1364,9 +1390,9 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             if (keep) {
                 if (LQ && ch < 0) {       // leaf: pending until the wave's next leaf phase
                     poff = ~ch;
-                    pcnt = nd->cnt[c];
+                    pcnt = PF ? pf_cnt : (int)nd->cnt[c];
                 } else if (ch < 0) {      // leaf: fp64 primitive tests (these decide the result)
-                    leaf_test(H + ~ch, (int)nd->cnt[c]);
+                    leaf_test(H + ~ch, PF ? pf_cnt : (int)nd->cnt[c]);
                 } else if (MERGE) {       // the node test runs below, shared with the restarts
                     desc = true;
                 } else {                  // descend if any of the child's 8 children is hit (fp32)
@@ -1410,6 +1436,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     else raying = false;
                 }
             }
+            if (PF && raying && !pdone) prefetch();
             }
             // a finished shadow ray whose path continues: resolve it and start the next bounce
             // right here (the bounce direction was drawn when the hit was shaded), so the lane
@@ -1444,6 +1471,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     mlo = mhi = 0;
                     lvl_set<SH>(mlo, mhi, 0, rm);
                     raying = rm != 0;
+                    if (PF && raying) prefetch();
                 }
             }
             // MERGE: one node test per step for the lanes that descend into an interior child and
@@ -1764,6 +1792,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 mlo = mhi = 0;
                 lvl_set<SH>(mlo, mhi, 0, rm);
                 raying = rm != 0;   // no root child hit: finished (consumed by the next handler run)
+                if (PF && raying) prefetch();
                 break;
             }
         }
