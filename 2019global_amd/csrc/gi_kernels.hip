@@ -1037,7 +1037,12 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 #define GI_X_TRI 1   // 4-wave LDS kernel: triangle-only primitive tests and texture mapping (TRI)
 #endif
 #ifndef GI_X_PREFETCH
-#define GI_X_PREFETCH 1   // HBM-resident scenes: fetch the next pop's child reference a step ahead (PF)
+// HBM-resident scenes: fetch the next pop's child reference a step ahead (PF): C4 1.94 -> 1.75-1.78 ms,
+// C5 199.7 -> 198.5 ms
+#define GI_X_PREFETCH 1
+#endif
+#ifndef GI_X_PREFETCH_LDS
+#define GI_X_PREFETCH_LDS 0   // the same for LDS-resident scenes
 #endif
 #ifndef GI_X_RECULL_LEAF_HBM
 // HBM-resident scenes: re-cull popped leaves (0: a leaf's fp64 tests run against the best t as they
@@ -1264,7 +1269,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     // end of the step that sets up the level (descend, climb or ray start), so the pop itself waits
     // for no load: one dependent round trip per step (the child's node or leaf records) instead of
     // two.  (lvl mask, node) do not change between that fetch and the pop.
-    constexpr bool PF = GI_X_PREFETCH != 0 && !PAIR;
+    constexpr bool PF = PAIR ? GI_X_PREFETCH_LDS != 0 : GI_X_PREFETCH != 0;
     int pf_ch = 0, pf_cnt = 0;
     auto prefetch = [&]() {
         const uint32_t m = lvl_get<SH>(mlo, mhi, level);
@@ -1436,7 +1441,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     else raying = false;
                 }
             }
-            if (PF && raying && !pdone) prefetch();
+            if (PF && raying && !pdone && !desc) prefetch();   // (MERGE: descending lanes below)
             }
             // a finished shadow ray whose path continues: resolve it and start the next bounce
             // right here (the bounce direction was drawn when the hit was shaded), so the lane
@@ -1499,6 +1504,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     // a ray that ends here waits for the handler (which continues a shadow ray's path)
                     if (rest == 0) raying = false;
                 }
+                if (PF && raying) prefetch();
                 rs = false;
                 desc = false;
             }
