@@ -574,7 +574,7 @@ bool build_host_scene(const gi_scene_desc& desc, HostScene& hs, std::string& err
             for (int k = 0; k < 3; ++k) { bounds[6 * i + k] = pb[i].mn[k]; bounds[6 * i + 3 + k] = pb[i].mx[k]; }
         int leaf_max = 4;
         if (const char* lm = std::getenv("GI_XLEAF_MAX")) leaf_max = std::max(1, std::atoi(lm));
-        build_xbvh(hs.xprims, bounds, leaf_max, hs);
+        build_xbvh(hs.xprims, bounds, leaf_max, hs, true);
         return true;
     }
     hs.xnodes.resize(1);

@@ -144,6 +144,7 @@ struct HostScene {
     int32_t x_handle8 = 6;   // Mode X handler threshold (eighths), chosen by the builder
     int32_t x_flags = 0;     // Mode X schedule flags (DevScene::x_flags), chosen by the builder
     double x_est_nodes = 0, x_est_prims = 0;   // SAH estimates per random ray through the root
+    bool x_spatial = false;  // the Mode X BVH was built with spatial splits (a primitive in several leaves)
 };
 
 // Sets XWNode::exists from the child references (both Mode X builders call it last).
@@ -156,7 +157,10 @@ inline void finalize_xwnodes(std::vector<XWNode>& w) {
 }
 
 // Mode X 8-wide BVH over the primitives (gi_bvh.cpp); bounds: 6 doubles (min xyz, max xyz) each.
-void build_xbvh(const std::vector<XPrim>& prims, const std::vector<double>& bounds, int leaf_max, HostScene& hs);
+// geometric: the prims hold their geometry (Mode X), so large scenes may use spatial splits; the
+// Mode R line BVH passes boxes only.
+void build_xbvh(const std::vector<XPrim>& prims, const std::vector<double>& bounds, int leaf_max, HostScene& hs,
+                bool geometric = false);
 // Mode R candidate reconstruction structures (HostScene app_* / rpath* / rc_* / r_always) from the
 // reference octree (rnodes, leaf_ents) and the entities' triangles.
 void build_rcand(HostScene& hs);

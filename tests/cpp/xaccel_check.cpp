@@ -1,8 +1,9 @@
 // xaccel_check.cpp — CPU check of the Mode X acceleration structure built by libgi's host code
 // (gi_build.cpp + gi_bvh.cpp, compiled here by g++ from the same sources).
 //
-//  * structure: every primitive in exactly one leaf (BVH) / at least one leaf (octree), every
-//    fp32 child box contains its subtree's fp64 primitive bounds, parent pointers consistent,
+//  * structure: every primitive in exactly one leaf (BVH) / at least one leaf (octree, and the
+//    spatial-split BVH of scenes over 8192 primitives: scene 2), every fp32 child box of a BVH
+//    without spatial splits contains its subtree's fp64 primitive bounds, parent pointers consistent,
 //    depth within the 16 mask levels of the traversal;
 //  * traversal: the kernel's stackless front-to-back walk (k_mode_x, restated here step for step:
 //    per-level 8-bit child masks, slot k ^ octant order, re-cull against the current best t)
@@ -317,7 +318,8 @@ int main(int argc, char** argv) {
         std::string err;
         if (!build_host_scene(sd, hs, err)) { std::printf("build failed: %s\n", err.c_str()); return 2; }
         const bool bvh = hs.xnodes.empty();
-        if (check_structure(hs, bvh)) return 1;
+        // the spatial-split build puts a primitive in several leaves, each boxing a part of it
+        if (check_structure(hs, bvh && !hs.x_spatial)) return 1;
         std::vector<XWNode> dec;
         if (check_quantised(hs, dec)) return 1;
         std::vector<XCNode> xc;
