@@ -743,6 +743,45 @@ void build_rcand(HostScene& hs) {
     hs.rc_nodes = std::move(tmp.xwnodes);
     hs.rc_ent.resize(tmp.xhot.size());
     for (size_t j = 0; j < tmp.xhot.size(); ++j) hs.rc_ent[j] = atom_ent[tmp.xhot[j].prim];
+    // Rank order: every slot carries the highest list rank of the entities below it (an entity's
+    // first appearance is its latest), and each node's slots are sorted by it, highest first.  The
+    // answer is the hitting candidate of highest reachable rank, so a walk in slot order meets the
+    // likely winners first, and once a popped slot's bound is <= the best rank found, neither it nor
+    // its later siblings can hold a better candidate (the kernels drop the rest of that level).
+    // Children follow their parent in rc_nodes (fill pushes them), so one backward pass suffices.
+    const int nw = (int)hs.rc_nodes.size();
+    hs.rc_maxkey.assign((size_t)nw * 8, -1);
+    for (int w = nw - 1; w >= 0; --w) {
+        XWNode& nd = hs.rc_nodes[w];
+        int64_t key[8];
+        for (int c = 0; c < 8; ++c) {
+            key[c] = -1;
+            if (nd.child[c] == XEMPTY) continue;
+            if (nd.child[c] >= 0) {
+                for (int k = 0; k < 8; ++k) key[c] = std::max(key[c], hs.rc_maxkey[(size_t)nd.child[c] * 8 + k]);
+            } else {
+                for (int j = 0; j < nd.cnt[c]; ++j) {
+                    const int e = hs.rc_ent[~nd.child[c] + j];
+                    key[c] = std::max(key[c], hs.app_rank[hs.app_off[e]]);
+                }
+            }
+        }
+        int perm[8] = {0, 1, 2, 3, 4, 5, 6, 7};
+        std::stable_sort(perm, perm + 8, [&](int a, int b) {
+            const bool ea = nd.child[a] == XEMPTY, eb = nd.child[b] == XEMPTY;
+            if (ea != eb) return eb;   // empty slots last
+            return key[a] > key[b];
+        });
+        const XWNode old = nd;
+        for (int i = 0; i < 8; ++i) {
+            const int c = perm[i];
+            for (int a = 0; a < 3; ++a) { nd.lo[a][i] = old.lo[a][c]; nd.hi[a][i] = old.hi[a][c]; }
+            nd.child[i] = old.child[c];
+            nd.cnt[i] = old.cnt[c];
+            hs.rc_maxkey[(size_t)w * 8 + i] = key[c];
+        }
+    }
+    finalize_xwnodes(hs.rc_nodes);
 }
 
 

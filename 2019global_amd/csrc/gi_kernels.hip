@@ -695,7 +695,9 @@ __device__ __forceinline__ void trace_mode_r_cand(const DevScene& sc, V3 o, V3 d
         lvl_set(mlo, mhi, level, msk & (msk - 1));
         const XWNode* nd = W + node;
         const int ch = nd->child[c];
-        if (ch < 0) {
+        if (sc.rc_maxkey[node * 8 + c] <= best) {   // rank order: no better candidate here or after
+            lvl_set(mlo, mhi, level, 0);
+        } else if (ch < 0) {
             const int cnt = nd->cnt[c];
             for (int j = 0; j < cnt; ++j) r_consider(sc, sc.rc_ent[~ch + j], o, d, best, r, nnode, nprim);
         } else {
@@ -765,7 +767,11 @@ __device__ __forceinline__ void trace_mode_r_split(const DevScene& sc, V3 o, V3 
         lvl_set(mlo, mhi, level, msk & (msk - 1));
         const XWNode* nd = W + node;
         const int ch = nd->child[c];
-        if (ch < 0) {
+        // rank order (gi_bvh.cpp build_rcand): a slot whose highest rank is <= the group's best --
+        // the same value in all NSUB lanes here -- and its later siblings hold no better candidate
+        if (sc.rc_maxkey[node * 8 + c] <= best) {
+            lvl_set(mlo, mhi, level, 0);
+        } else if (ch < 0) {
             const int cnt = nd->cnt[c];
             for (int j = 0; j < cnt; ++j) consider(sc.rc_ent[~ch + j]);
             best = group_max<NSUB>(best);
@@ -787,8 +793,11 @@ __device__ __forceinline__ void trace_mode_r_split(const DevScene& sc, V3 o, V3 
     }
 }
 
+#ifndef GI_R_MIN_WAVES
+#define GI_R_MIN_WAVES 1   // minimum waves per SIMD asked of the register allocator (k_mode_r_split)
+#endif
 template <bool STATS, int NSUB>
-__global__ __launch_bounds__(256) void k_mode_r_split(DevScene sc, CamDev cam, V3 light, TileMap m, double* rgb,
+__global__ __launch_bounds__(256, GI_R_MIN_WAVES) void k_mode_r_split(DevScene sc, CamDev cam, V3 light, TileMap m, double* rgb,
                                                        uint8_t* rgb8, unsigned long long* stats, float tau) {
     const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     const long long ps = g / NSUB;   // pixel slot (tile order)

@@ -139,6 +139,8 @@ struct HostScene {
     std::vector<int32_t> rpath;      //   (filled for leaves; the leaf itself is the last entry)
     std::vector<XWNode> rc_nodes;    // line BVH over the non-sphere entities that appear in a leaf
     std::vector<int32_t> rc_ent;     //   entity of each leaf record
+    std::vector<int64_t> rc_maxkey;  //   per node slot (8 per node): the highest app_rank under it;
+                                     //   a node's slots are in decreasing order of it
     std::vector<int32_t> r_always;   // ImpSpheres that appear in a leaf (tested by every ray)
     double rc_ext = 0;               // max |coordinate| of the line BVH's boxes
     int32_t x_handle8 = 6;   // Mode X handler threshold (eighths), chosen by the builder
@@ -195,6 +197,7 @@ struct DevScene {
     const int32_t* rpath;
     const XWNode* rc_nodes;
     const int32_t* rc_ent;
+    const int64_t* rc_maxkey;
     const int32_t* r_always;
     int32_t n_r_always;
     float rc_ext;

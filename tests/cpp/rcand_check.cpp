@@ -8,6 +8,7 @@
 //   rcand_check <n_rays> [scene.scn ...]
 #include <cfloat>
 #include <cmath>
+#include <functional>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -158,17 +159,19 @@ static Res candidates(const HostScene& s, V3 o, V3 d, long& considered) {
     // the kernel's inv_dir: reciprocal clamped to +-1e30
     auto inv = [](float v) { return std::fmin(std::fmax(1.0f / v, -1e30f), 1e30f); };
     const float iv[3] = {inv((float)d.x), inv((float)d.y), inv((float)d.z)};
-    std::vector<int> stack = {0};
-    while (!stack.empty()) {
-        const XWNode& nd = s.rc_nodes[stack.back()];
-        stack.pop_back();
+    // the kernels' walk: depth first in slot order, a level dropped once a popped slot's highest
+    // rank (rc_maxkey; slots sorted by it) is <= the best rank found
+    std::function<void(int)> visit = [&](int n) {
+        const XWNode& nd = s.rc_nodes[n];
         const uint32_t m = mask_line(nd, of, iv, tau);
         for (int c = 0; c < 8; ++c) {
             if (!((m >> c) & 1)) continue;
-            if (nd.child[c] >= 0) stack.push_back(nd.child[c]);
+            if (s.rc_maxkey[(size_t)n * 8 + c] <= best) return;
+            if (nd.child[c] >= 0) visit(nd.child[c]);
             else for (int j = 0; j < nd.cnt[c]; ++j) consider(s.rc_ent[~nd.child[c] + j]);
         }
-    }
+    };
+    if (!s.rc_nodes.empty()) visit(0);
     return r;
 }
 
