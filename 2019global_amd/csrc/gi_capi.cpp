@@ -380,6 +380,9 @@ int scene_create_on(const gi_scene_desc* desc, int device, gi_scene** out) {
             }
         for (const XPrim& xp : h.xprims)
             if (xp.kind != 0) d.x_tri_only = 0;
+        d.r_tri_only = 1;
+        for (const REnt& r : h.ents)
+            if (r.kind != K_IMP_TRIANGLE) d.r_tri_only = 0;
     }
     // HBM-resident scenes whose XWNode tree outgrows an XCD's L2 share (> 2 MB) traverse quantised
     // nodes (XCNode: one 128-byte line per node instead of two): C5 287 -> 270 ms; the 1k soup, whose

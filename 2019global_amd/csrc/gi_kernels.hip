@@ -46,7 +46,14 @@ constexpr int kWavesPerBlock = 4;
 // ---------------------------------------------------------------------------------------------
 // Mode R device pieces
 // ---------------------------------------------------------------------------------------------
+// TRI: every entity of the scene is an ImpTriangle (DevScene::r_tri_only; the other kinds' code and
+// registers drop out of the Mode R kernels)
+template <bool TRI = false>
 __device__ bool ent_hit(const DevScene& sc, const REnt& e, V3 o, V3 d, V3& P, V3& N, uint32_t& nprim) {
+    if (TRI) {
+        ++nprim;
+        return tri_hit(sc.tris[e.tri_first], o, d, P, N);
+    }
     if (e.kind == K_IMP_SPHERE) {
         ++nprim;
         return sphere_hit(ld3(e.pos), e.radius, o, d, P, N);
@@ -98,8 +105,9 @@ __device__ bool ent_hit(const DevScene& sc, const REnt& e, V3 o, V3 d, V3& P, V3
 }
 
 // getTextureCoord (entities.h:108-130, 277-303, 630-641) with the device's f64 acos/sin/cos
+template <bool TRI = false>
 __device__ void tex_coord(const DevScene& sc, const REnt& e, V3 ip, int32_t& x, int32_t& y) {
-    if (e.kind == K_IMP_SPHERE) {
+    if (!TRI && e.kind == K_IMP_SPHERE) {
         const double r = e.radius;
         const double unit_v = 2.0 * REF_PI * r / 320.0;
         const V3 to = ip - ld3(e.pos);
@@ -110,7 +118,7 @@ __device__ void tex_coord(const DevScene& sc, const REnt& e, V3 ip, int32_t& x, 
         const double cos_hori = dot(v3(to.x, to.y, 0), v3(0, small_r, 0)) / (small_r * small_r);
         const double unit_h = 2.0 * REF_PI * small_r / 320.0;
         x = x86_trunc(small_r * acos(cos_hori) / unit_h);
-    } else if (e.kind == K_IMP_TRIANGLE) {   // per-triangle constants precomputed by the builder
+    } else if (TRI || e.kind == K_IMP_TRIANGLE) {   // per-triangle constants precomputed by the builder
         const V3 p1 = ld3(e.qv0), p21 = ld3(e.qv1), i1 = ip - p1;
         const double i1l = gsqrt(sq3(i1));
         const double theta = acos(dot(p21, i1) / (e.qv2[0] * i1l));
@@ -591,6 +599,7 @@ __device__ __forceinline__ uint32_t children_mask_line(const XWNode* nd, F3 of, 
     // distance ((b -+ tau) - o) * iv is monotone in b, so no per-child min / max; the planes' quads
     // are addressed directly (lo of axis a at quad 2a, hi at 6 + 2a)
     const int sm = iv_signs(ivf);
+    const int ex = nd->exists;
     float4 q[12];   // near[3][8] then far[3][8]
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
@@ -600,7 +609,6 @@ __device__ __forceinline__ uint32_t children_mask_line(const XWNode* nd, F3 of, 
         q[6 + 2 * a] = b[fq];
         q[6 + 2 * a + 1] = b[fq + 1];
     }
-    const int ex = nd->exists;
     const float* v = reinterpret_cast<const float*>(q);
     const float sx = (sm & 1) ? tau : -tau, sy = (sm & 2) ? tau : -tau, sz = (sm & 4) ? tau : -tau;
     uint32_t m = 0;
@@ -657,12 +665,13 @@ __device__ __forceinline__ bool r_leaf_reachable(const DevScene& sc, int leaf, V
 }
 
 // entity e as a candidate: exact test, then its latest reachable appearance against the best so far
+template <bool TRI = false>
 __device__ __forceinline__ void r_consider(const DevScene& sc, int e, V3 o, V3 d, long long& best, RResult& r,
                                            uint32_t& nnode, uint32_t& nprim, RMemo memo = RMemo{nullptr}) {
     const int a0 = sc.app_off[e], a1 = sc.app_off[e + 1];
     if (a0 == a1 || sc.app_rank[a0] <= best) return;
     V3 P, N;
-    if (!ent_hit(sc, sc.ents[e], o, d, P, N, nprim) || !(sq3(P - o) < DBL_MAX)) return;   // raytracer.h:58-65
+    if (!ent_hit<TRI>(sc, sc.ents[e], o, d, P, N, nprim) || !(sq3(P - o) < DBL_MAX)) return;   // raytracer.h:58-65
     for (int i = a0; i < a1; ++i) {
         const long long rk = sc.app_rank[i];
         if (rk <= best) return;
@@ -738,7 +747,7 @@ __device__ __forceinline__ long long group_max(long long v) {
     }
     return v;
 }
-template <int NSUB>
+template <int NSUB, bool TRI>
 __device__ __forceinline__ void trace_mode_r_split(const DevScene& sc, V3 o, V3 d, float tau, int sub, RResult& r,
                                                    long long& mine, uint32_t& nnode, uint32_t& nprim, RMemo memo) {
     r.ent = -1;
@@ -748,7 +757,7 @@ __device__ __forceinline__ void trace_mode_r_split(const DevScene& sc, V3 o, V3 
     auto consider = [&](int e) {
         if ((int)(k++ % NSUB) != sub) return;
         const long long before = best;
-        r_consider(sc, e, o, d, best, r, nnode, nprim, memo);
+        r_consider<TRI>(sc, e, o, d, best, r, nnode, nprim, memo);
         if (best != before) mine = best;
     };
     for (int i = 0; i < sc.n_r_always; ++i) consider(sc.r_always[i]);
@@ -793,10 +802,13 @@ __device__ __forceinline__ void trace_mode_r_split(const DevScene& sc, V3 o, V3 
     }
 }
 
+#ifndef GI_R_TRI
+#define GI_R_TRI 1   // k_mode_r_split specialised for scenes of ImpTriangles only (DevScene::r_tri_only)
+#endif
 #ifndef GI_R_MIN_WAVES
 #define GI_R_MIN_WAVES 1   // minimum waves per SIMD asked of the register allocator (k_mode_r_split)
 #endif
-template <bool STATS, int NSUB>
+template <bool STATS, int NSUB, bool TRI>
 __global__ __launch_bounds__(256, GI_R_MIN_WAVES) void k_mode_r_split(DevScene sc, CamDev cam, V3 light, TileMap m, double* rgb,
                                                        uint8_t* rgb8, unsigned long long* stats, float tau) {
     const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -820,7 +832,7 @@ __global__ __launch_bounds__(256, GI_R_MIN_WAVES) void k_mode_r_split(DevScene s
         const V3 d = normalize(primary_dir(cam, (double)x, (double)y));   // Ray ctor (ray.h:6)
         RResult r;
         long long mine;
-        trace_mode_r_split<NSUB>(sc, o, d, tau, sub, r, mine, nnode, nprim, memo);
+        trace_mode_r_split<NSUB, TRI>(sc, o, d, tau, sub, r, mine, nnode, nprim, memo);
         const long long gmax = group_max<NSUB>(mine);
         // the lowest sub-lane holding the maximum shades (ranks are unique: one lane at most)
         const unsigned long long m_win = __ballot(mine == gmax);
@@ -830,9 +842,9 @@ __global__ __launch_bounds__(256, GI_R_MIN_WAVES) void k_mode_r_split(DevScene s
         if (writer) {
             double c0 = 0, c1 = 0, c2 = 0;
             if (gmax >= 0) {
-                const REnt e = sc.ents[r.ent];
+                const REnt& e = sc.ents[r.ent];
                 int32_t u, v;
-                tex_coord(sc, e, r.P, u, v);
+                tex_coord<TRI>(sc, e, r.P, u, v);
                 const V3 col = shade_ref(e, d, light, r.P, r.N, u, v);
                 c0 = col.x; c1 = col.y; c2 = col.z;
             }
@@ -2145,8 +2157,13 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
         mark(ev_begin);
         if (split) {
             const dim3 sgrid((unsigned)((m.n_local * (kTile * kTile) * GI_R_NSUB + 255) / 256));
-            if (stats) hipLaunchKernelGGL((k_mode_r_split<true, GI_R_NSUB>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
-            else hipLaunchKernelGGL((k_mode_r_split<false, GI_R_NSUB>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
+            if (sc.r_tri_only && GI_R_TRI) {
+                if (stats) hipLaunchKernelGGL((k_mode_r_split<true, GI_R_NSUB, true>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
+                else hipLaunchKernelGGL((k_mode_r_split<false, GI_R_NSUB, true>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
+            } else {
+                if (stats) hipLaunchKernelGGL((k_mode_r_split<true, GI_R_NSUB, false>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
+                else hipLaunchKernelGGL((k_mode_r_split<false, GI_R_NSUB, false>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
+            }
         } else if (stats) {
             hipLaunchKernelGGL(k_mode_r<true>, grid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, dfs);
         } else {

@@ -188,6 +188,7 @@ struct DevScene {
     int32_t x_waves4;      // LDS-resident scene with light shading: k_mode_x at 4 waves per SIMD
     int32_t x_tri_only;    // every primitive a triangle, every entity ImpTriangle / ExpQuad / ExpCube /
                            // ExpBox (the 4-wave kinds): HBM-resident k_mode_x's TRI specialisation
+    int32_t r_tri_only;    // every entity an ImpTriangle: k_mode_r_split's TRI specialisation
     float root_lo[3], root_hi[3];   // Mode X: union of the root's fp32 child boxes (conservative)
     // Mode R candidate reconstruction (HostScene fields of the same names)
     const int32_t* app_off;

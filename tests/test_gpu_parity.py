@@ -955,12 +955,13 @@ def test_mode_r_split_candidates_frame_identical(torch_cuda, tmp_path):
             assert U.bits_equal(p.cpu().numpy(), ref[name + "_packed"]).all(), name + " packed"
 
 
-@pytest.mark.parametrize("accel", [{"GI_XACCEL": "octree"}, {"GI_XLEAF_MAX": "1"}])
+@pytest.mark.parametrize("accel", [{"GI_XACCEL": "octree"}, {"GI_XLEAF_MAX": "1"}, {"GI_XSBVH": "1"}])
 def test_mode_x_other_acceleration_structures_bit_exact(torch_cuda, accel):
     """Mode X over the SAT octree (GI_XACCEL=octree: up to 12 levels, so the kernel keeps its two-word
-    level masks) and over a BVH of single-primitive leaves (GI_XLEAF_MAX=1), both read when the
-    scene is built: frames equal the oracle's bit for bit -- the result does not depend on the
-    acceleration structure."""
+    level masks), over a BVH of single-primitive leaves (GI_XLEAF_MAX=1) and over the spatial-split
+    BVH forced onto these small scenes (GI_XSBVH=1: triangles cut by planes, a primitive in several
+    leaves; the 100k soup uses it by default), all read when the scene is built: frames equal the
+    oracle's bit for bit -- the result does not depend on the acceleration structure."""
     old = {k: os.environ.get(k) for k in accel}
     os.environ.update(accel)
     try:
