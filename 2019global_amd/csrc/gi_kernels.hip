@@ -509,6 +509,9 @@ __device__ __forceinline__ uint32_t children_mask(const XWNode* nd, F3 of, F3 iv
 // difference from decoding first is a few fp32 ulps of t, inside the 1e-5 * extent padding that
 // the host-checked decoded box already exceeds (the CPU checker runs this form).  Near / far
 // planes per axis as for XWNode.
+#ifndef GI_XC_PK
+#define GI_XC_PK 0   // quantised node test: two children per v_pk_fma_f32
+#endif
 __device__ __forceinline__ float xc_scale(int w, int a) {   // 2^e of axis a (e: signed byte a of w)
     const int e = (int)(int8_t)((w >> (8 * a)) & 0xFF);
     return __int_as_float((e + 127) << 23);
@@ -516,10 +519,9 @@ __device__ __forceinline__ float xc_scale(int w, int a) {   // 2^e of axis a (e:
 __device__ __forceinline__ float xc_q(int lo4, int hi4, int c) {   // byte c of the 8-byte pair
     return (float)(((c < 4 ? lo4 : hi4) >> (8 * (c & 3))) & 0xFF);
 }
-template <bool AXIS>
-__device__ __forceinline__ uint32_t children_mask(const XCNode* nd, F3 of, F3 ivf, float tmax, int dmask) {
-    const int4* b = reinterpret_cast<const int4*>(nd);
-    const int4 h = b[0], q1 = b[1], q2 = b[2], q3 = b[3];
+// the slab tests of a quantised node whose first 64 bytes (h, q1..q3) are already in registers
+__device__ __forceinline__ uint32_t children_mask_q(int4 h, int4 q1, int4 q2, int4 q3, F3 of, F3 ivf, float tmax,
+                                                    int dmask) {
     const F3 no = neg_oiv(of, ivf);
     const int sm = iv_signs(ivf);
     const float iv3[3] = {ivf.x, ivf.y, ivf.z}, no3[3] = {no.x, no.y, no.z};
@@ -539,6 +541,26 @@ __device__ __forceinline__ uint32_t children_mask(const XCNode* nd, F3 of, F3 iv
         fw[a][1] = neg ? lw[a][1] : hw[a][1];
     }
     uint32_t m = 0;
+#if GI_XC_PK
+    // children in pairs: one v_pk_fma_f32 gives two children's plane distances (the same fma per
+    // element, so the same mask)
+#pragma unroll
+    for (int c = 0; c < 8; c += 2) {
+        f32x2 tn = {0.0f, 0.0f}, tf = {tmax, tmax};
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const f32x2 s2 = {siv[a], siv[a]}, b2 = {base[a], base[a]};
+            const f32x2 qn = {xc_q(nw[a][0], nw[a][1], c), xc_q(nw[a][0], nw[a][1], c + 1)};
+            const f32x2 qf = {xc_q(fw[a][0], fw[a][1], c), xc_q(fw[a][0], fw[a][1], c + 1)};
+            const f32x2 t0 = __builtin_elementwise_fma(qn, s2, b2), t1 = __builtin_elementwise_fma(qf, s2, b2);
+            tn.x = fmaxf(tn.x, t0.x);
+            tn.y = fmaxf(tn.y, t0.y);
+            tf.x = fminf(tf.x, t1.x);
+            tf.y = fminf(tf.y, t1.y);
+        }
+        m |= (tn.x <= tf.x ? 1u << c : 0u) | (tn.y <= tf.y ? 2u << c : 0u);
+    }
+#else
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
         float tn = 0.0f, tf = tmax;
@@ -549,7 +571,13 @@ __device__ __forceinline__ uint32_t children_mask(const XCNode* nd, F3 of, F3 iv
         }
         m |= tn <= tf ? 1u << c : 0u;
     }
+#endif
     return xor_permute8(m & (uint32_t)((h.w >> 24) & 0xFF), dmask);
+}
+template <bool AXIS>
+__device__ __forceinline__ uint32_t children_mask(const XCNode* nd, F3 of, F3 ivf, float tmax, int dmask) {
+    const int4* b = reinterpret_cast<const int4*>(nd);
+    return children_mask_q(b[0], b[1], b[2], b[3], of, ivf, tmax, dmask);
 }
 __device__ __forceinline__ bool child_hit(const XCNode* nd, int c, F3 of, F3 ivf, float tmax) {
     const int4* b = reinterpret_cast<const int4*>(nd);
@@ -1048,8 +1076,9 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 #endif
 #ifndef GI_X_LEAFQ
 // quantised-node scenes, long launches: leaf tests postponed into leaf phases (LQ, mode_x_wave):
-// C5 245 -> 229 ms; the 1k soup (XWNode) +4% and C4 (short launches) +7% keep the plain step
-#define GI_X_LEAFQ 1
+// C5 245 -> 229 ms in round 2; with UL (one load round trip per step for node and leaf lanes) the
+// plain step is faster again (C5 182.5 ms without LQ against 196.5 ms with it), so LQ is off
+#define GI_X_LEAFQ 0
 #endif
 #ifndef GI_X_LEAFQ_LDS
 #define GI_X_LEAFQ_LDS 0   // LDS-resident scenes: leaf postponement as above (leaf tests two at a time)
@@ -1078,6 +1107,11 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 // 4-wave LDS kernel: a step's interior-node test and a restarted ray's root test in one block
 // (C3 6.08 -> 5.81 ms; the 3-wave LDS kernel of the every-entity scene is 2-4% slower with it)
 #define GI_X_MERGE 1
+#endif
+#ifndef GI_X_UNILOAD
+// UL (mode_x_wave, quantised-node HBM scenes): a step's node-test and leaf-test lanes share one load
+// round trip -- C5 196.5 -> 182.5 ms (without leaf postponement), C4 ~-1% (noise band)
+#define GI_X_UNILOAD 1
 #endif
 #ifndef GI_X_LEAF8
 #define GI_X_LEAF8 3   // LQ: leaf phase once 3/8 of the traversing lanes hold a leaf (C5 sweep 1-8)
@@ -1224,6 +1258,10 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     // MERGE (LDS kernel, no LQ): the step's interior-node test and a restarted ray's root test share
     // one children_mask call at the end of the step
     constexpr bool MERGE = GI_X_MERGE != 0 && PAIR && PSL && !LQ && !NST;
+    // UL (quantised-node HBM scenes without leaf postponement): one load round trip per step for
+    // the node-test and leaf-test lanes together
+    constexpr bool UL = GI_X_UNILOAD != 0 && !PAIR && !LQ &&
+                        std::is_same<std::remove_cv_t<std::remove_pointer_t<NodeP>>, XCNode>::value;
     bool desc = false, rs = false;   // MERGE: this step descends into xch / restarts at the root
     int xch = 0;
     const int leaf8 = ((xflags >> 12) & 15) ? ((xflags >> 12) & 15) : GI_X_LEAF8;
@@ -1241,23 +1279,26 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     // fp64 primitive tests of one leaf's records hp[0 .. cntl) (these decide the result): global
     // records fetched one ahead of the test; LDS records (PAIR) two at a time, the two fp64
     // dependency chains interleaved.  A shadow ray (own or a helper's) stops at any hit.
+    // leaf_test_from: global records, the first one already in registers (cur; UL below)
+    auto leaf_test_from = [&](XHotR cur, const auto* hp, int cntl) {
+        for (int j = 0; j < cntl; ++j) {
+            const XHotR rec = cur;
+            cur = load_hot(hp + min(j + 1, cntl - 1));
+            ++nprim;
+            const double t = x_prim_t<TRI>(rec.h, o, d, MX_TMIN);
+            const int pi = rec.h.prim;
+            if (phase != PH_CLOSEST) {
+                if (t < tmax) { best = pi; raying = false; return; }   // any hit occludes
+            } else if (t < tbest || (t == tbest && pi < best)) {
+                tbest = t;
+                best = pi;
+                tbest_f = up32(t);
+            }
+        }
+    };
     auto leaf_test = [&](const auto* hp, int cntl) {
         if constexpr (!PAIR) {
-            XHotR cur = load_hot(hp);
-            for (int j = 0; j < cntl; ++j) {
-                const XHotR rec = cur;
-                cur = load_hot(hp + min(j + 1, cntl - 1));
-                ++nprim;
-                const double t = x_prim_t<TRI>(rec.h, o, d, MX_TMIN);
-                const int pi = rec.h.prim;
-                if (phase != PH_CLOSEST) {
-                    if (t < tmax) { best = pi; raying = false; return; }   // any hit occludes
-                } else if (t < tbest || (t == tbest && pi < best)) {
-                    tbest = t;
-                    best = pi;
-                    tbest_f = up32(t);
-                }
-            }
+            leaf_test_from(load_hot(hp), hp, cntl);
         } else {
             for (int j = 0; j < cntl; j += 2) {
                 const bool two = j + 1 < cntl;
@@ -1413,7 +1454,34 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     cnt.ln_leaf += __popcll(ml);
                 }
             }
-            if (keep) {
+            if (UL) {
+                // one memory round trip for the wave's node-test AND leaf-test lanes: each lane's
+                // load (the child's 64 slab bytes, or its leaf's first record) is issued before
+                // either test waits, instead of a node-test block and a leaf-test block each
+                // waiting on its own load
+                XHotR ur;
+                if (ch < 0) {
+                    ur = load_hot(H + ~ch);
+                } else {
+                    const int4* qb = reinterpret_cast<const int4*>(W + ch);
+                    ur.q[0] = qb[0];
+                    ur.q[1] = qb[1];
+                    ur.q[2] = qb[2];
+                    ur.q[3] = qb[3];
+                }
+                if (ch < 0) {
+                    leaf_test_from(ur, H + ~ch, PF ? pf_cnt : (int)nd->cnt[c]);
+                } else {
+                    ++nnode;
+                    const uint32_t cm = children_mask_q(ur.q[0], ur.q[1], ur.q[2], ur.q[3], of, ivf, tbest_f, dmask);
+                    if (cm) {
+                        node = ch;
+                        ++level;
+                        lvl_set<SH>(mlo, mhi, level, cm);
+                        if (NST) nst[level * 256] = ch;
+                    }
+                }
+            } else if (keep) {
                 if (LQ && ch < 0) {       // leaf: pending until the wave's next leaf phase
                     poff = ~ch;
                     pcnt = PF ? pf_cnt : (int)nd->cnt[c];
