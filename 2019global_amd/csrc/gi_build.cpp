@@ -641,7 +641,7 @@ bool build_host_scene(const gi_scene_desc& desc, HostScene& hs, std::string& err
                 memcpy(h.b, p.b, sizeof h.b);
                 memcpy(h.c, p.c, sizeof h.c);
                 h.prim = pi;
-                h.kind = xhot_kind(p);
+                h.kind = p.kind;
                 hs.xhot.push_back(h);
                 XBox bx;
                 for (int a = 0; a < 3; ++a) { bx.lo[a] = lo32(pb[pi].mn[a]); bx.hi[a] = hi32(pb[pi].mx[a]); }

@@ -463,7 +463,7 @@ void build_xbvh(const std::vector<XPrim>& prims, const std::vector<double>& boun
             memcpy(h.b, p.b, sizeof h.b);
             memcpy(h.c, p.c, sizeof h.c);
             h.prim = pi;
-            h.kind = xhot_kind(p);
+            h.kind = p.kind;
             hs.xhot.push_back(h);
             XBox bx;
             for (int a = 0; a < 3; ++a) { bx.lo[a] = lo32(pb[pi].mn[a]); bx.hi[a] = hi32(pb[pi].mx[a]); }
@@ -585,7 +585,7 @@ void build_xbvh(const std::vector<XPrim>& prims, const std::vector<double>& boun
                     memcpy(h.b, p.b, sizeof h.b);
                     memcpy(h.c, p.c, sizeof h.c);
                     h.prim = pi;
-                    h.kind = xhot_kind(p);
+                    h.kind = p.kind;
                     hs.xhot.push_back(h);
                     XBox bx;
                     for (int a = 0; a < 3; ++a) { bx.lo[a] = lo32(pb[pi].mn[a]); bx.hi[a] = hi32(pb[pi].mx[a]); }

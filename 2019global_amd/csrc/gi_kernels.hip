@@ -359,7 +359,7 @@ __device__ __forceinline__ XHotR load_hot(const XHot* p) {
 // kind test vanish, so a leaf test is one straight block the compiler schedules as a whole
 template <bool TRI = false>
 __device__ __forceinline__ double x_prim_t(const XHot& p, V3 o, V3 d, double tmin) {
-    if (TRI || (p.kind & 1) == 0) {
+    if (TRI || p.kind == 0) {
         const V3 e1 = ld3(p.b), e2 = ld3(p.c), v0 = ld3(p.a);
         const V3 pv = fcross(d, e2);
         const double det = fdot(e1, pv);
@@ -1113,9 +1113,6 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 // round trip -- C5 196.5 -> 182.5 ms (without leaf postponement), C4 ~-1% (noise band)
 #define GI_X_UNILOAD 1
 #endif
-#ifndef GI_X_HENT
-#define GI_X_HENT 0   // the closest hit's entity index taken from its XHot record (XHot::kind >> 1)
-#endif
 #ifndef GI_X_LEAF8
 #define GI_X_LEAF8 3   // LQ: leaf phase once 3/8 of the traversing lanes hold a leaf (C5 sweep 1-8)
 #endif
@@ -1255,7 +1252,6 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     // current ray
     V3 o = cam.pos, d = v3(1, 0, 0);
     int dmask = 0, best = -1, node = 0, level = 0;
-    int bent = 0;   // HENT: the entity of the closest hit so far (from its XHot record)
     bool raying = false;
     int poff = 0, pcnt = 0;   // LQ: the pending leaf (records H[poff .. poff + pcnt)), pcnt 0: none
     bool pdone = false;       // LQ: the ray ends once its pending leaf is tested
@@ -1296,7 +1292,6 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             } else if (t < tbest || (t == tbest && pi < best)) {
                 tbest = t;
                 best = pi;
-                if (GI_X_HENT) bent = rec.h.kind >> 1;
                 tbest_f = up32(t);
             }
         }
@@ -1321,12 +1316,10 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     if (ta < tbest || (ta == tbest && r0.h.prim < best)) {
                         tbest = ta;
                         best = r0.h.prim;
-                        if (GI_X_HENT) bent = r0.h.kind >> 1;
                     }
                     if (tb < tbest || (tb == tbest && r1.h.prim < best)) {
                         tbest = tb;
                         best = r1.h.prim;
-                        if (GI_X_HENT) bent = r1.h.kind >> 1;
                     }
                     tbest_f = up32(tbest);
                 }
@@ -1638,7 +1631,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     const V3 din = d;   // the incoming direction
                     const V3 P = o + tbest * d;
                     const XPrim& p = XP[best];   // by reference: only used fields are loaded
-                    const REnt& e = EN[GI_X_HENT ? bent : p.ent];   // HENT: no wait on XP[best]
+                    const REnt& e = EN[p.ent];
                     V3 N = (TRI || p.kind == 0) ? ld3(p.n) : normalize(P - ld3(p.a));
                     if (!(dot(din, N) < 0)) N = -N;
                     int32_t tu, tv;

@@ -100,11 +100,9 @@ bool encode_xcnodes(const std::vector<XWNode>& w, std::vector<XCNode>& out);
 struct XHot {              // 80 bytes
     double a[3], b[3], c[3];   // triangle v0, e1, e2 | sphere centre, (r, 0, 0)
     int32_t prim;          // global primitive index (tie-break, shading record)
-    int32_t kind;          // bit 0: 0 triangle, 1 sphere; bits 1..31: the primitive's entity (XPrim::ent),
-                           // so the shading handler's entity load need not wait for the XPrim record
+    int32_t kind;          // 0 triangle, 1 sphere
 };
 static_assert(sizeof(XHot) == 80, "XHot layout");
-inline int32_t xhot_kind(const XPrim& p) { return (p.kind & 1) | (int32_t)((uint32_t)p.ent << 1); }
 // fp32 prefilter record parallel to xhot[]: the primitive's AABB rounded outward and padded, so a
 // ray that misses it cannot hit the primitive; the 80-B fp64 record is fetched only otherwise.
 struct XBox {              // 32 bytes

@@ -38,7 +38,7 @@ static double urand() {
 }
 
 static double prim_t(const XHot& p, V3 o, V3 d, double tmin) {   // the kernel's x_prim_t
-    if ((p.kind & 1) == 0) {   // bit 0: triangle / sphere (the entity rides above it)
+    if (p.kind == 0) {
         const V3 e1 = ld3(p.b), e2 = ld3(p.c);
         const V3 pv = fcross(d, e2);
         const double det = fdot(e1, pv);
@@ -70,7 +70,7 @@ static XHot hot_of(const XPrim& p, int i) {
     XHot h;
     for (int k = 0; k < 3; ++k) { h.a[k] = p.a[k]; h.b[k] = p.b[k]; h.c[k] = p.c[k]; }
     h.prim = i;
-    h.kind = xhot_kind(p);
+    h.kind = p.kind;
     return h;
 }
 
