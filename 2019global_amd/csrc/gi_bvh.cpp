@@ -628,9 +628,10 @@ void build_xbvh(const std::vector<XPrim>& prims, const std::vector<double>& boun
     // k_mode_x's shading handler runs once this many eighths of a wave's live lanes wait.  Short
     // traversals (few node visits per ray) gain from shading whole waves at once; long ones lose
     // more to lanes idling at the threshold (measured: Cornell / main / 1k soup best at 8/8, the
-    // 100k soup at 3/8).  One node visit costs ~4 primitive tests.
+    // 100k soup at 3/8 in round 2 and 4/8 with UL: C4 1.72 -> 1.67-1.69 ms, C5 equal).  One node
+    // visit costs ~4 primitive tests.
     const bool long_traversal = est_nodes + 0.25 * est_prims > 16.0;
-    hs.x_handle8 = long_traversal ? 3 : 8;
+    hs.x_handle8 = long_traversal ? 4 : 8;
     // short traversals also continue a path from its finished shadow ray inside the traversal
     // branch (measured +14% on the Cornell box, -5% on the 100k soup)
     hs.x_flags = long_traversal ? 0 : 1;
