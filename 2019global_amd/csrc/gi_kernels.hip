@@ -1283,7 +1283,9 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     auto leaf_test_from = [&](XHotR cur, const auto* hp, int cntl) {
         for (int j = 0; j < cntl; ++j) {
             const XHotR rec = cur;
-            cur = load_hot(hp + min(j + 1, cntl - 1));
+            // long launches (no handoff build): no load after the leaf's last record (C5 182.3 ->
+            // 180.2 ms); the handoff build keeps the unconditional one-ahead load (C4 +3% without)
+            if (HELP || j + 1 < cntl) cur = load_hot(hp + min(j + 1, cntl - 1));
             ++nprim;
             const double t = x_prim_t<TRI>(rec.h, o, d, MX_TMIN);
             const int pi = rec.h.prim;
