@@ -47,6 +47,8 @@ FLAG_STATS = 1
 FLAG_R_DFS = 2   # Mode R: reverse-DFS over the whole reference octree (A/B against the default)
 FLAG_TIME = 4    # HIP events around the dominant kernel; read with DeviceScene.kernel_ms()
 FLAG_X_NO_SHADOW = 8   # Mode X, tests only: no shadow rays (reduces depth-1 Mode X to the reference's shading)
+FLAG_X_WF = 16   # Mode X: the wavefront form (one launch per bounce over compacted path queues, gi_wf.hip)
+FLAG_X_MEGA = 32   # Mode X: the persistent path-state kernel k_mode_x (neither flag: chosen per launch)
 STAT_RAYS, STAT_NODES, STAT_PRIMS, STAT_PIXELS, STAT_X_PATH_MAX = 0, 1, 2, 3, 4
 STAT_X_ITERS, STAT_X_TRAV, STAT_X_HANDLE, STAT_X_HLANES, STAT_X_HCLOSE, STAT_X_HSHADOW = 5, 6, 7, 8, 9, 10
 STAT_X_CYC_TRAV, STAT_X_CYC_HIT, STAT_X_CYC_NEXT, STAT_X_CYC_ALL = 11, 12, 13, 14
@@ -55,7 +57,7 @@ STAT_X_IT_NODE, STAT_X_LN_NODE, STAT_X_IT_LEAF, STAT_X_LN_LEAF = 16, 17, 18, 19
 STAT_X_IT_RS, STAT_X_LN_RS, STAT_X_IT_ST, STAT_X_LN_ST = 20, 21, 22, 23
 STATS_N = 24
 TILE = 8
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 
 class GIError(RuntimeError):

@@ -22,8 +22,8 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = "gfx950"
 
 HOST_SRCS = ["gi_build.cpp", "gi_bvh.cpp", "gi_capi.cpp", "gi_multi.cpp", "gi_obj.cpp"]
-DEV_SRCS = ["gi_kernels.hip"]
-HEADERS = ["gi_math.h", "gi_scene.h", "gi_internal.h"]
+DEV_SRCS = ["gi_kernels.hip", "gi_wf.hip"]
+HEADERS = ["gi_math.h", "gi_scene.h", "gi_internal.h", "gi_dev.h"]
 
 COMMON = ["-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", f"-I{INCLUDE}", f"-I{CSRC}"]
 
@@ -77,17 +77,25 @@ def build(verbose: bool = False, force: bool = False, variant: str = "", hip_def
         objs.append(obj)
     with open(bid_file, "w") as f:
         f.write(bid + "\n")
+    jobs = []   # the kernel translation units compile in parallel
     for s in DEV_SRCS:
         src = os.path.join(CSRC, s)
         obj = os.path.join(objdir, s + (f".{variant}" if variant else "") + ".o")
         if force or _stale(obj, [src] + hdrs):
-            _run([hipcc, f"--offload-arch={ARCH}", "-O3", "-Wshadow", *COMMON, *[f"-D{d}" for d in hip_defines],
-                  "-munsafe-fp-atomics", "-c", src, "-o", obj], verbose)
+            cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-Wshadow", *COMMON, *[f"-D{d}" for d in hip_defines],
+                   "-munsafe-fp-atomics", "-c", src, "-o", obj]
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            jobs.append((cmd, subprocess.Popen(cmd)))
         objs.append(obj)
+    for cmd, p in jobs:
+        if p.wait() != 0:
+            raise subprocess.CalledProcessError(p.returncode, cmd)
     if force or _stale(out, objs):
         _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-o", out, *objs, f"-L{ROCM}/lib", "-lamdhip64", "-ldl"], verbose)
-        for leftover in glob.glob(out + ".0.*"):   # hipcc's unbundling temporaries
-            os.remove(leftover)
+    # hipcc's unbundling temporaries (libgi.so.<n>.hipv4-..., .host-...): removed on every build
+    for leftover in glob.glob(out + ".[0-9]*.hipv4-*") + glob.glob(out + ".[0-9]*.host-*"):
+        os.remove(leftover)
     return out
 
 

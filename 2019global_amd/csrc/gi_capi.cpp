@@ -22,6 +22,8 @@ namespace gi {
 bool build_host_scene(const gi_scene_desc& desc, HostScene& hs, std::string& err);
 long long shard_tiles(int w, int h, int shard_count);
 hipError_t x_launch_config(const DevScene& sc, int device, XLaunchCfg& cfg);
+bool x_wf_choice(const DevScene& sc, const XLaunchCfg& xc, const gi_opts& o);
+long long x_wf_chunk();
 hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev& cam, V3 light, int w, int h, int y0,
                          const gi_opts& o, double* rgb, uint8_t* rgb8, const XScratch& xs, KTimer* kt,
                          hipStream_t stream);
@@ -119,7 +121,10 @@ int ensure_xscratch(gi_scene* s, int w, int h, const gi_opts* o) {
     if (x.cap < need) {
         (void)hipFree(x.list);
         (void)hipFree(x.part);
-        x = XScratch();
+        x.list = nullptr;
+        x.part = nullptr;
+        x.cap = 0;
+        x.spp = 0;
         if ((e = hipMalloc((void**)&x.list, (size_t)need * sizeof(unsigned))) != hipSuccess) return hip_fail(e, "hipMalloc (work list)");
         x.cap = need;
     }
@@ -130,6 +135,29 @@ int ensure_xscratch(gi_scene* s, int w, int h, const gi_opts* o) {
         if ((e = hipMalloc((void**)&x.part, (size_t)o->spp * (size_t)x.cap * 3 * sizeof(double))) != hipSuccess)
             return hip_fail(e, "hipMalloc (per-sample radiance)");
         x.spp = o->spp;
+    }
+    if (x_wf_choice(s->dev, s->xcfg, *o)) {   // wavefront form: path queues sized to a chunk of units
+        const long long want = std::max(64ll, std::min(x_wf_chunk(), need * (long long)o->spp));
+        if (!x.wcnt) {
+            if ((e = hipMalloc((void**)&x.wcnt, 2 * 64 * sizeof(unsigned))) != hipSuccess) return hip_fail(e, "hipMalloc (wavefront counters)");
+            if ((e = hipHostMalloc((void**)&x.h_nlist, sizeof(unsigned), hipHostMallocDefault)) != hipSuccess)
+                return hip_fail(e, "hipHostMalloc (wavefront)");
+        }
+        if (x.wcap < want) {
+            for (int q = 0; q < 2; ++q) {
+                (void)hipFree(x.wq[q]);
+                (void)hipFree(x.wid[q]);
+                x.wq[q] = nullptr;
+                x.wid[q] = nullptr;
+            }
+            x.wcap = 0;
+            for (int q = 0; q < 2; ++q) {
+                if ((e = hipMalloc((void**)&x.wq[q], (size_t)want * 12 * sizeof(double))) != hipSuccess ||
+                    (e = hipMalloc((void**)&x.wid[q], (size_t)want * 2 * sizeof(unsigned))) != hipSuccess)
+                    return hip_fail(e, "hipMalloc (wavefront path queues)");
+            }
+            x.wcap = want;
+        }
     }
     return GI_OK;
 }
@@ -238,6 +266,12 @@ void destroy_scene(gi_scene* s) noexcept {
     for (void* p : s->allocs) (void)hipFree(p);
     (void)hipFree(s->xs.list);
     (void)hipFree(s->xs.part);
+    for (int q = 0; q < 2; ++q) {
+        (void)hipFree(s->xs.wq[q]);
+        (void)hipFree(s->xs.wid[q]);
+    }
+    (void)hipFree(s->xs.wcnt);
+    (void)hipHostFree(s->xs.h_nlist);
     for (int i = 0; i < KTimer::kRing; i++) {
         if (s->kt.ev0[i]) (void)hipEventDestroy(static_cast<hipEvent_t>(s->kt.ev0[i]));
         if (s->kt.ev1[i]) (void)hipEventDestroy(static_cast<hipEvent_t>(s->kt.ev1[i]));

@@ -61,10 +61,45 @@ bool is_real(const char* p, size_t n) {
 // std::from_chars: correctly rounded like Python's float(), and independent of the C locale (the
 // reference host is a Qt app: QApplication calls setlocale(LC_ALL, ""), so strtod would stop at
 // the '.' of "1.5" under a comma-decimal locale such as de_DE)
+// decimal exponent of the leading non-zero digit of a real token accepted by is_real (the value is
+// in [10^e, 10^(e+1))); a large sentinel when every digit is zero
+long long decimal_magnitude(const char* p, size_t n) {
+    size_t i = (n > 0 && (p[0] == '+' || p[0] == '-')) ? 1 : 0;
+    long long pos = 0;   // position of the leading non-zero digit relative to the point (0: units)
+    bool found = false;
+    long long int_digits = 0;
+    for (; i < n && p[i] >= '0' && p[i] <= '9'; ++i) {
+        if (!found && p[i] != '0') found = true;
+        if (found) ++int_digits;
+    }
+    if (found) pos = int_digits - 1;
+    if (i < n && p[i] == '.') {
+        ++i;
+        for (long long k = 1; i < n && p[i] >= '0' && p[i] <= '9'; ++i, ++k)
+            if (!found && p[i] != '0') { found = true; pos = -k; }
+    }
+    if (!found) return 1ll << 40;
+    long long e = 0;
+    if (i < n && (p[i] == 'e' || p[i] == 'E')) {
+        ++i;
+        const bool neg = i < n && p[i] == '-';
+        if (i < n && (p[i] == '+' || p[i] == '-')) ++i;
+        for (; i < n && p[i] >= '0' && p[i] <= '9'; ++i) e = std::min(e * 10 + (p[i] - '0'), 1ll << 40);
+        if (neg) e = -e;
+    }
+    return pos + e;
+}
+
 bool parse_double(const Tok& t, double& v) {
     if (!is_real(t.p, t.n)) return false;
     const char* b = t.p + (t.p[0] == '+' ? 1 : 0);   // from_chars takes no leading '+'
     const std::from_chars_result r = std::from_chars(b, t.p + t.n, v);
+    if (r.ec == std::errc::result_out_of_range && r.ptr == t.p + t.n && decimal_magnitude(t.p, t.n) < 0) {
+        // underflow: the value rounds to a signed zero (from_chars reports it as out of range and
+        // leaves v alone; Python's float() -- scenes.load_obj -- returns the zero)
+        v = t.p[0] == '-' ? -0.0 : 0.0;
+        return true;
+    }
     return r.ec == std::errc() && r.ptr == t.p + t.n && std::isfinite(v);
 }
 

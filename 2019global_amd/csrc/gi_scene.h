@@ -224,6 +224,14 @@ struct XScratch {
     double* part = nullptr;     // cap * spp * 3 doubles
     long long cap = 0;          // pixel slots the buffers hold
     int spp = 0;                // samples per pixel the part buffer was sized for
+    // wavefront Mode X (gi_wf.hip): two path queues of wcap entries (SoA: 12 fp64 fields + a
+    // (list index, sample) pair = 104 B per entry), 2 device counters per bounce, and a pinned word
+    // for the work list's length
+    double* wq[2] = {nullptr, nullptr};
+    unsigned* wid[2] = {nullptr, nullptr};
+    unsigned* wcnt = nullptr;
+    unsigned* h_nlist = nullptr;
+    long long wcap = 0;
 };
 
 // Mode X launch configuration, computed once per scene when it is created (gi_capi.cpp, on the
@@ -232,6 +240,8 @@ struct XLaunchCfg {
     int kv = 0;              // kernel variant: 2 * (LDS-resident scene) + (4 waves per SIMD)
     size_t lds_bytes = 0;    // dynamic LDS per workgroup
     int resident = 1;        // resident 256-thread workgroups on the device (occupancy x CUs)
+    size_t wf_lds_bytes = 0; // wavefront Mode X (k_wf_bounce): dynamic LDS per workgroup
+    int wf_resident = 1;     //   and its resident workgroups
 };
 
 }  // namespace gi

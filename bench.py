@@ -171,38 +171,54 @@ def cpu_threads():
 
 
 def cpu_baseline(scn_text, w, h, mode, spp, depth, seed, target_s=20.0):
-    """The oracle (this repo's CPU port, OpenMP) on a bounded, centred window of the same frame:
-    a 256x96 probe sets the rate, then a window sized for about `target_s` seconds is timed."""
+    """The oracle (this repo's CPU port, OpenMP) on a frame-representative sample of the same workload:
+    full-width rows spread evenly over the frame (y = row0 + k * stride).  A probe of 8 rows sets the
+    rate, then about `target_s` seconds of rows are timed.  Mode X `value` basis: rays that reach the
+    scene -- primary samples whose ray misses the scene's bounding box add exactly +0 and are counted
+    apart (the GPU's classify pass and root-box pretest resolve the same kind of sample apart from its
+    `value`), so `value` here is traced rays per second like the GPU line's; `value_all_rays` counts
+    them too.  Mode R: one ray per pixel over a centred window (the reference's only depth)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_util as U
     threads = cpu_threads()
-
-    def window(ww, wh):
-        cx, cy = w // 2, (int(h * 0.8) if mode == 1 else h // 2)
-        x0, y0 = max(0, min(w - ww, cx - ww // 2)), max(0, min(h - wh, cy - wh // 2))
-        return (x0, y0, min(w, x0 + ww), min(h, y0 + wh))
-
-    def run(win):
-        t = time.perf_counter()
-        o = U.oracle_render(scn_text, w, h, mode=mode, spp=spp, depth=depth, seed=seed, window=win, threads=threads)
-        dt = time.perf_counter() - t
-        rays = int(o["ncand"].sum()) if mode == 1 else (win[2] - win[0]) * (win[3] - win[1])
-        return rays, dt
-
-    win = window(min(w, 256), min(h, 96))
-    rays, dt = run(win)
-    scale = target_s / max(dt, 1e-3)
-    if scale > 1.5:
-        f = min(scale ** 0.5, max(w / (win[2] - win[0]), h / (win[3] - win[1])))
-        win = window(min(w, int((win[2] - win[0]) * f)), min(h, int((win[3] - win[1]) * f)))
-        rays, dt = run(win)
     model, host_cores = cpu_info()
-    return {"value": round(rays / dt / 1e6, 4), "unit": "Mray/s", "cores": threads, "kind": "port",
+    if mode == 0:
+        cx, cy, ww, wh = w // 2, h // 2, min(w, 512), min(h, 256)
+        win = (max(0, cx - ww // 2), max(0, cy - wh // 2), min(w, cx - ww // 2 + ww), min(h, cy - wh // 2 + wh))
+        t = time.perf_counter()
+        U.oracle_render(scn_text, w, h, mode=0, window=win, threads=threads)
+        dt = time.perf_counter() - t
+        rays = (win[2] - win[0]) * (win[3] - win[1])
+        return {"value": round(rays / dt / 1e6, 4), "unit": "Mray/s", "cores": threads, "kind": "port",
+                "cpu_model": model, "host_cores": host_cores,
+                "sample": f"Mode R window x[{win[0]},{win[2]}) y[{win[1]},{win[3]}), {rays} rays, {dt:.2f} s wall, "
+                          f"OpenMP over {threads} threads"}
+
+    def run(row0, stride, n_rows):
+        t = time.perf_counter()
+        r = U.oracle_time_rows(scn_text, w, h, spp, depth, seed, row0, stride, n_rows, threads)
+        return r, time.perf_counter() - t
+
+    n, stride = min(8, h), max(1, h // min(8, h))
+    r, dt = run(stride // 2, stride, n)
+    for _ in range(3):   # rescale until the sample takes about target_s (whole frame at most)
+        if dt >= 0.5 * target_s or n >= h:
+            break
+        n = int(max(1, min(h, n * target_s / max(dt, 1e-3))))
+        stride = max(1, h // n)
+        n = min(n, (h + stride - 1) // stride)
+        r, dt = run(stride // 2, stride, n)
+    traced = r["rays"] - r["resolved"]
+    return {"value": round(traced / dt / 1e6, 4), "unit": "Mray/s", "cores": threads, "kind": "port",
+            "value_all_rays": round(r["rays"] / dt / 1e6, 4),
             "cpu_model": model, "host_cores": host_cores,
-            "sample": f"window x[{win[0]},{win[2]}) y[{win[1]},{win[3]}) of the same frame, {rays} rays, "
-                      f"{dt:.2f} s wall, OpenMP over {threads} threads (OMP_NUM_THREADS; the host has "
-                      f"{host_cores} logical CPUs); closest-hit queries by the oracle's own BVH for scenes "
-                      f"above 256 primitives, brute force below"}
+            "value_basis": "rays that reach the scene (primary samples missing the scene's bounding box counted "
+                           "apart, as the GPU's value does); value_all_rays includes them",
+            "sample": f"{r['pixels'] // w} full-width rows y = {stride // 2} + k*{stride} spread over the frame "
+                      f"({r['pixels']} pixels x {spp} spp), {traced} traced rays + {r['resolved']} resolved samples, "
+                      f"{dt:.2f} s wall, OpenMP over {threads} threads (OMP_NUM_THREADS; the host has {host_cores} "
+                      f"logical CPUs); closest-hit queries by the oracle's own BVH above 256 primitives, brute force "
+                      f"below"}
 
 
 def reference_cpu(scn_text, w, h):
@@ -254,8 +270,10 @@ def host_path(gi, sc, dev, cam, light, w, h, mode, spp, depth, seed, reps=3):
         timed("multi_2shards_1dev_rgb8+fp64_bands32", m2.render, (rgb, rgb8), 32)
         m2.close()
         os.environ["GI_MULTI_RCCL"] = "1"   # read by gi_multi_create
-        m1 = gi.MultiScene.from_scene(sc, [0])
-        del os.environ["GI_MULTI_RCCL"]
+        try:
+            m1 = gi.MultiScene.from_scene(sc, [0])
+        finally:
+            del os.environ["GI_MULTI_RCCL"]
         if m1.info()["rccl"]:
             timed("multi_rccl_self_rgb8+fp64_bands32", m1.render, (rgb, rgb8), 32)
             timed("multi_rccl_self_rgb8+fp64", m1.render, (rgb, rgb8), 0)

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define GI_ABI_VERSION 8
+#define GI_ABI_VERSION 9
 
 typedef enum gi_status {
     GI_OK = 0,
@@ -109,6 +109,10 @@ typedef enum gi_mode {
                                     depth 1 and spp 1 this reduces Mode X to the reference's own
                                     shading (raytracer.h:41-84, material.h:48-62), so its stages can
                                     be checked against the reference's frames (tests) */
+#define GI_FLAG_X_WF 16u         /* Mode X: the wavefront form (one launch per bounce over a compacted queue of
+                                    live paths, gi_wf.hip) whatever the scene; same frame bit for bit */
+#define GI_FLAG_X_MEGA 32u       /* Mode X: the persistent path-state kernel (k_mode_x) whatever the scene.
+                                    Neither flag: chosen per launch (GI_X_WF=0/1 overrides) */
 
 typedef struct gi_opts {
     int32_t mode;          /* gi_mode */

@@ -1306,6 +1306,67 @@ int gio_render(const char* scn, int w, int h, int mode, int spp, int depth, uint
     return 0;
 }
 
+// bench.py's cpu_baseline leg: Mode X over the full-width rows y = row0 + k * stride (k < n_rows),
+// timed by the caller.  A primary sample whose ray misses the scene's bounding box (the union of the
+// primitives' padded boxes, prim_bounds) adds exactly +0 and reaches no geometry: it is counted apart
+// (out[1]) and not traced, as the GPU's classify pass / root-box pretest resolve such samples apart
+// from its `value`.  out: [0] rays (primary + bounce + shadow, resolved ones included), [1] resolved
+// primary samples, [2] pixels, [3] the sum of the pixels' radiance (keeps the work observable).
+int gio_time_rows(const char* scn, int w, int h, int spp, int depth, uint64_t seed, int row0, int stride, int n_rows,
+                  int threads, double* out) {
+    Scene s;
+    if (!parse(scn, s, false)) return -1;
+    if (w <= 0 || h <= 0 || spp < 1 || depth < 1 || stride < 1 || n_rows < 0 || row0 < 0) { g_err = "bad arguments"; return -2; }
+    std::vector<Prim> prims;
+    OAccel A;
+    build_prims(s, prims);
+    build_accel(prims, A);
+    double blo[3] = {INFINITY, INFINITY, INFINITY}, bhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (const Prim& p : prims) {
+        double lo[3], hi[3];
+        prim_bounds(p, lo, hi);
+        for (int k = 0; k < 3; ++k) { blo[k] = std::fmin(blo[k], lo[k]); bhi[k] = std::fmax(bhi[k], hi[k]); }
+    }
+    const Cam c = make_cam(s, w);
+    std::vector<int> rows;
+    for (int k = 0; k < n_rows && row0 + (long)k * stride < h; ++k) rows.push_back(row0 + k * stride);
+    const long npx = (long)rows.size() * w;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#endif
+    long rays = 0, res = 0;
+    double sum = 0.0;
+#pragma omp parallel for schedule(dynamic, 64) reduction(+ : rays, res, sum)
+    for (long i = 0; i < npx; ++i) {
+        const int x = (int)(i % w), y = rows[(size_t)(i / w)];
+        const uint64_t pix = (uint64_t)y * (uint64_t)w + (uint64_t)x;
+        double acc[3] = {0, 0, 0};
+        for (int smp = 0; smp < spp; ++smp) {
+            double jx = 0.0, jy = 0.0;
+            if (spp > 1) { jx = mx_u01(seed, pix, smp, 0xFFFF, 0); jy = mx_u01(seed, pix, smp, 0xFFFF, 1); }
+            const V3 d0 = normalize((c.top_left - (c.left * ((double)x + jx)) * c.rx) - (c.up * ((double)y + jy)) * c.ry);
+            const double o3[3] = {c.pos.x, c.pos.y, c.pos.z}, d3[3] = {d0.x, d0.y, d0.z};
+            double tn = 0.0, tf = INFINITY;
+            for (int k = 0; k < 3; ++k) {
+                const double t0 = (blo[k] - o3[k]) / d3[k], t1 = (bhi[k] - o3[k]) / d3[k];
+                tn = std::fmax(tn, std::fmin(t0, t1));
+                tf = std::fmin(tf, std::fmax(t0, t1));
+            }
+            if (prims.empty() || !(tn <= tf)) { ++rays; ++res; continue; }   // L = 0
+            V3 L;
+            int32_t h0 = -1, u0 = 0, v0 = 0;
+            sample_mode_x(s, prims, A, c, w, x, y, smp, spp, depth, seed, L, h0, u0, v0, rays);
+            acc[0] = acc[0] + L.x; acc[1] = acc[1] + L.y; acc[2] = acc[2] + L.z;
+        }
+        sum += acc[0] + acc[1] + acc[2];
+    }
+    out[0] = (double)rays;
+    out[1] = (double)res;
+    out[2] = (double)npx;
+    out[3] = sum;
+    return 0;
+}
+
 long gio_tree(const char* scn, char* buf, long cap) {
     Scene s;
     if (!parse(scn, s)) return -1;

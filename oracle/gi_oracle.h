@@ -29,6 +29,12 @@ int gio_render(const char* scn, int w, int h, int mode, int spp, int depth, uint
                int x0, int y0, int x1, int y1, int threads,
                double* rgb, int32_t* hit, int32_t* uv, int32_t* ncand, int32_t* nnode, uint8_t* q);
 
+// bench.py's cpu_baseline: Mode X over full-width rows y = row0 + k*stride (k < n_rows); primary
+// samples whose ray misses the scene's bounding box are counted apart and not traced.  out[4]: rays,
+// resolved primary samples, pixels, radiance sum.
+int gio_time_rows(const char* scn, int w, int h, int spp, int depth, uint64_t seed, int row0, int stride, int n_rows,
+                  int threads, double* out);
+
 // Octree dump in the same text format as `ref_harness tree` (bbox lines, then DFS node lines).
 // Returns the number of bytes needed (excluding NUL); writes at most cap bytes.
 long gio_tree(const char* scn, char* buf, long cap);

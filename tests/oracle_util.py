@@ -51,6 +51,8 @@ def oracle():
         lib.gio_last_error.restype = ctypes.c_char_p
         lib.gio_set_accel.argtypes = [ctypes.c_int]
         lib.gio_set_no_shadow.argtypes = [ctypes.c_int]
+        lib.gio_time_rows.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, f64p]
         _oracle = lib
     return _oracle
 
@@ -73,6 +75,18 @@ def oracle_render(scn: str, w: int, h: int, mode: int = 0, spp: int = 1, depth: 
     if rc != 0:
         raise RuntimeError(f"gio_render failed ({rc}): {lib.gio_last_error().decode()}")
     return out
+
+
+def oracle_time_rows(scn: str, w: int, h: int, spp: int, depth: int, seed: int, row0: int, stride: int, n_rows: int,
+                     threads: int = 0) -> dict:
+    """Mode X over the full-width rows row0 + k*stride (bench.py's cpu_baseline): rays traced,
+    primary samples resolved by the scene-box test (not traced), pixels, radiance sum."""
+    out = np.zeros(4)
+    lib = oracle()
+    rc = lib.gio_time_rows(scn.encode(), w, h, spp, depth, seed, row0, stride, n_rows, threads, _p(out, ctypes.c_double))
+    if rc != 0:
+        raise RuntimeError(f"gio_time_rows failed ({rc}): {lib.gio_last_error().decode()}")
+    return {"rays": int(out[0]), "resolved": int(out[1]), "pixels": int(out[2]), "sum": float(out[3])}
 
 
 def oracle_no_shadow(on: bool) -> None:

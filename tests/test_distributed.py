@@ -1,5 +1,5 @@
-"""CPU, multi-process (gloo, world size 2 and 3): the N>1 frame path of bench.py — round-robin 8x8
-tile shards, per-rank packed buffers, FrameGather's gather to rank 0, and reassembly — gives the
+"""CPU, multi-process (gloo, world size 2, 3 and 8 -- the 8-GPU config's rank count): the N>1 frame
+path of bench.py — round-robin 8x8 tile shards, per-rank packed buffers, FrameGather's gather to rank 0, and reassembly — gives the
 exact single-process frame.  Rendering here is the CPU oracle (the GPU is not available); the
 GPU-side tests check gi_render_device's packed output and gi_unshard_device against the same
 layout (test_gpu_parity.py::test_sharded_render_equals_single, test_unshard_matches_host_layout)."""
@@ -45,7 +45,7 @@ def _worker(rank, world, port, w, h, scn, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_sharded_gather_reassembles_frame(world):
     S = U.scenes()
     w, h = 61, 43   # ragged: partial tiles on both edges

@@ -135,10 +135,13 @@ def test_malformed_input_rejected(bad):
 def test_number_forms_agree():
     """Every accepted number form parses to the same double on both sides."""
     text = ("v +1. .5 -0\nv 1E+2 -2.5e-3 007\nv 1e308 -4.9e-324 123456789012345678901234567890\n"
-            "f +1 2/7 -1//3\n")
+            "f +1 2/7 -1//3\n"
+            "v 1e-400 -2e-324 0.000001e-330\nf 1 2 4\n")   # ADVICE r03: underflow to a signed zero on both sides
     c, p = c_parse(text), py_parse(text)
     assert c == p
     assert c[0][2] == (1.0, 0.5, -0.0, 100.0, -0.0025, 7.0, 1e308, -5e-324, 1.2345678901234568e29)
+    v = c[1][2][6:9]
+    assert v == (0.0, -0.0, 0.0) and [str(x) for x in v] == ["0.0", "-0.0", "0.0"]
 
 
 def test_parse_ignores_c_locale(tmp_path):
