@@ -113,11 +113,24 @@ hipError_t upload(gi_scene* s, const std::vector<T>& v, const T** out) {
 // k_mode_x's per-sample radiance for spp > 1); grown, never shrunk.  hipFree synchronises with
 // work still using them.
 int ensure_xscratch(gi_scene* s, int w, int h, const gi_opts* o) {
-    if (o->mode != GI_MODE_X) return GI_OK;
     const long long need = shard_tiles(w, h, o->shard_count) * GI_TILE * GI_TILE;
+    hipError_t e;
+    if (o->mode == GI_MODE_R) {   // the heavy-pixel list of k_mode_r_split (every pixel slot at most;
+                                  // large scenes only: without the list the split kernel has no budget)
+        XScratch& x = s->xs;
+        if (s->dev.n_ents > 4096 && x.rcap < need) {
+            (void)hipFree(x.rheavy);
+            x.rheavy = nullptr;
+            x.rcap = 0;
+            if ((e = hipMalloc((void**)&x.rheavy, (size_t)need * 2 * sizeof(long long))) != hipSuccess)
+                return hip_fail(e, "hipMalloc (heavy-pixel list)");
+            x.rcap = need;
+        }
+        return GI_OK;
+    }
+    if (o->mode != GI_MODE_X) return GI_OK;
     if ((unsigned long long)need >= 0xFFFFFFFFull) return fail(GI_ERR_ARG, "mode X frame too large: 2^32 pixel slots");
     XScratch& x = s->xs;
-    hipError_t e;
     if (x.cap < need) {
         (void)hipFree(x.list);
         (void)hipFree(x.part);
@@ -271,6 +284,7 @@ void destroy_scene(gi_scene* s) noexcept {
         (void)hipFree(s->xs.wid[q]);
     }
     (void)hipFree(s->xs.wcnt);
+    (void)hipFree(s->xs.rheavy);
     (void)hipHostFree(s->xs.h_nlist);
     for (int i = 0; i < KTimer::kRing; i++) {
         if (s->kt.ev0[i]) (void)hipEventDestroy(static_cast<hipEvent_t>(s->kt.ev0[i]));

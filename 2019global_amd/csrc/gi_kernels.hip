@@ -410,12 +410,17 @@ __device__ __forceinline__ long long group_max(long long v) {
     }
     return v;
 }
+// best0: the pruning bound to start from (-1: none; the heavy-pixel pass restarts a pixel from the
+// rank its first pass had found, minus one, so that candidate is met again).  budget > 0: the walk
+// gives up (returns true, with best = the group's best so far) once the group has met more than
+// `budget` candidates -- decided after a leaf, where every lane holds the same count and best.
 template <int NSUB, bool TRI>
-__device__ __forceinline__ void trace_mode_r_split(const DevScene& sc, V3 o, V3 d, float tau, int sub, RResult& r,
-                                                   long long& mine, uint32_t& nnode, uint32_t& nprim, RMemo memo) {
+__device__ __forceinline__ bool trace_mode_r_split(const DevScene& sc, V3 o, V3 d, float tau, int sub, RResult& r,
+                                                   long long& mine, uint32_t& nnode, uint32_t& nprim, RMemo memo,
+                                                   long long& best, unsigned budget) {
     r.ent = -1;
     mine = -1;
-    long long best = -1;   // the group's best rank so far (pruning bound)
+    // best: the group's best rank so far (pruning bound)
     unsigned k = 0;        // candidates met so far (the same count in every lane of the group)
     auto consider = [&](int e) {
         if ((int)(k++ % NSUB) != sub) return;
@@ -447,6 +452,7 @@ __device__ __forceinline__ void trace_mode_r_split(const DevScene& sc, V3 o, V3 
             const int cnt = nd->cnt[c];
             for (int j = 0; j < cnt; ++j) consider(sc.rc_ent[~ch + j]);
             best = group_max<NSUB>(best);
+            if (budget && k > budget) return true;
         } else {
             const uint32_t cm = children_mask_line(W + ch, of, ivf, tau);
             if (cm) {
@@ -463,8 +469,45 @@ __device__ __forceinline__ void trace_mode_r_split(const DevScene& sc, V3 o, V3 
         }
         going = rest != 0;
     }
+    return false;
 }
 
+// the pixel from a group's walk: the lowest sub-lane holding the group's highest rank (ranks are
+// unique: one lane at most) shades it; none: black
+template <int NSUB, bool TRI>
+__device__ __forceinline__ void r_split_write(const DevScene& sc, V3 d, V3 light, const RResult& r, long long mine,
+                                              int sub, long long idx, double* rgb, uint8_t* rgb8) {
+    const long long gmax = group_max<NSUB>(mine);
+    const unsigned long long m_win = __ballot(mine == gmax);
+    const int base = (int)(threadIdx.x & 63) & ~(NSUB - 1);
+    const unsigned long long gm = NSUB >= 64 ? ~0ull : ((1ull << (NSUB & 63)) - 1);
+    const bool writer = gmax < 0 ? sub == 0 : (int)(threadIdx.x & 63) == base + __builtin_ctzll((m_win >> base) & gm);
+    if (writer) {
+        double c0 = 0, c1 = 0, c2 = 0;
+        if (gmax >= 0) {
+            const REnt& e = sc.ents[r.ent];
+            int32_t u, v;
+            tex_coord<TRI>(sc, e, r.P, u, v);
+            const V3 col = shade_ref(e, d, light, r.P, r.N, u, v);
+            c0 = col.x; c1 = col.y; c2 = col.z;
+        }
+        if (rgb) { rgb[3 * idx] = c0; rgb[3 * idx + 1] = c1; rgb[3 * idx + 2] = c2; }
+        if (rgb8) quantize(c0, c1, c2, rgb8 + 3 * idx);
+    }
+}
+
+// pixels whose first pass gave up (k_mode_r_split with a budget): (pixel slot, rank found) pairs
+struct RHeavy {
+    long long* list;   // 2 per entry
+    unsigned* n;
+    unsigned budget;   // 0: no budget (the first pass finishes every pixel)
+};
+
+#ifndef GI_R_BUDGET
+// candidates a pixel's 8 lanes may meet in k_mode_r_split before the pixel is handed to
+// k_mode_r_heavy (a whole wave per pixel); 0: never
+#define GI_R_BUDGET 0
+#endif
 #ifndef GI_R_TRI
 #define GI_R_TRI 1   // k_mode_r_split specialised for scenes of ImpTriangles only (DevScene::r_tri_only)
 #endif
@@ -473,7 +516,7 @@ __device__ __forceinline__ void trace_mode_r_split(const DevScene& sc, V3 o, V3 
 #endif
 template <bool STATS, int NSUB, bool TRI>
 __global__ __launch_bounds__(256, GI_R_MIN_WAVES) void k_mode_r_split(DevScene sc, CamDev cam, V3 light, TileMap m, double* rgb,
-                                                       uint8_t* rgb8, unsigned long long* stats, float tau) {
+                                                       uint8_t* rgb8, unsigned long long* stats, float tau, RHeavy hv) {
     const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     const long long ps = g / NSUB;   // pixel slot (tile order)
     const int sub = (int)(g % NSUB);
@@ -494,25 +537,16 @@ __global__ __launch_bounds__(256, GI_R_MIN_WAVES) void k_mode_r_split(DevScene s
         const V3 o = cam.pos;
         const V3 d = normalize(primary_dir(cam, (double)x, (double)y));   // Ray ctor (ray.h:6)
         RResult r;
-        long long mine;
-        trace_mode_r_split<NSUB, TRI>(sc, o, d, tau, sub, r, mine, nnode, nprim, memo);
-        const long long gmax = group_max<NSUB>(mine);
-        // the lowest sub-lane holding the maximum shades (ranks are unique: one lane at most)
-        const unsigned long long m_win = __ballot(mine == gmax);
-        const int base = (int)(threadIdx.x & 63) & ~(NSUB - 1);
-        const bool writer = gmax < 0 ? sub == 0
-                                     : (int)(threadIdx.x & 63) == base + __builtin_ctz((uint32_t)((m_win >> base) & ((1ull << NSUB) - 1)));
-        if (writer) {
-            double c0 = 0, c1 = 0, c2 = 0;
-            if (gmax >= 0) {
-                const REnt& e = sc.ents[r.ent];
-                int32_t u, v;
-                tex_coord<TRI>(sc, e, r.P, u, v);
-                const V3 col = shade_ref(e, d, light, r.P, r.N, u, v);
-                c0 = col.x; c1 = col.y; c2 = col.z;
+        long long mine, best = -1;
+        const bool gave_up = trace_mode_r_split<NSUB, TRI>(sc, o, d, tau, sub, r, mine, nnode, nprim, memo, best, hv.budget);
+        if (gave_up) {   // a heavy pixel: k_mode_r_heavy finishes it with a whole wave
+            if (sub == 0) {
+                const unsigned i = atomicAdd(hv.n, 1u);
+                hv.list[2 * i] = ps;
+                hv.list[2 * i + 1] = best;
             }
-            if (rgb) { rgb[3 * idx] = c0; rgb[3 * idx + 1] = c1; rgb[3 * idx + 2] = c2; }
-            if (rgb8) quantize(c0, c1, c2, rgb8 + 3 * idx);
+        } else {
+            r_split_write<NSUB, TRI>(sc, d, light, r, mine, sub, idx, rgb, rgb8);
         }
     } else if (sub == 0 && idx >= 0 && m.shard_count > 1) {   // padding slot of a packed tile
         if (rgb) { rgb[3 * idx] = 0; rgb[3 * idx + 1] = 0; rgb[3 * idx + 2] = 0; }
@@ -522,6 +556,39 @@ __global__ __launch_bounds__(256, GI_R_MIN_WAVES) void k_mode_r_split(DevScene s
         const bool px = ok && sub == 0;
         wave_add_stats(stats, px ? 1 : 0, nnode, nprim, px ? 1 : 0);
     }
+}
+
+// Heavy pixels of the budgeted first pass: one wave (64 lanes) per pixel, candidates dealt over its
+// 64 lanes, the walk restarted with the first pass's rank minus one as the pruning bound (its
+// candidate is met again; nothing of lower rank can win).  Waves loop over the list.
+template <bool STATS, bool TRI>
+__global__ __launch_bounds__(256, GI_R_MIN_WAVES) void k_mode_r_heavy(DevScene sc, CamDev cam, V3 light, TileMap m, double* rgb,
+                                                       uint8_t* rgb8, unsigned long long* stats, float tau, RHeavy hv) {
+    __shared__ int s_memo[GI_R_MEMO > 0 ? 4 * GI_R_MEMO : 1];
+    RMemo memo{GI_R_MEMO > 0 ? s_memo + (threadIdx.x >> 6) * GI_R_MEMO : nullptr};
+    const int sub = (int)(threadIdx.x & 63);
+    const unsigned n = *hv.n;
+    uint32_t nnode = 0, nprim = 0;
+    for (unsigned i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < n; i += (gridDim.x * blockDim.x) >> 6) {
+        const long long ps = hv.list[2 * i];
+        long long best = hv.list[2 * i + 1] - 1;
+        if (GI_R_MEMO > 0) {
+            for (int k = sub; k < GI_R_MEMO; k += 64) memo.e[k] = -1;
+            __builtin_amdgcn_wave_barrier();
+        }
+        long long idx = -1;
+        int x = 0, y = 0;
+        slot_pixel(m, ps >> 6, (int)(ps & 63), idx, x, y);
+        y += m.y0;
+        const V3 o = cam.pos;
+        const V3 d = normalize(primary_dir(cam, (double)x, (double)y));
+        RResult r;
+        long long mine;
+        trace_mode_r_split<64, TRI>(sc, o, d, tau, sub, r, mine, nnode, nprim, memo, best, 0);
+        r_split_write<64, TRI>(sc, d, light, r, mine, sub, idx, rgb, rgb8);
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (STATS) wave_add_stats(stats, 0, nnode, nprim, 0);
 }
 
 template <bool STATS>
@@ -1653,6 +1720,7 @@ long long shard_tiles(int w, int h, int shard_count) { return make_map(w, h, sha
 // work-unit run length (scenes of cheap background samples such as the main.cpp scene prefer 8).
 struct XEnv {
     int lds = 1, h8 = 0, xf = -1, run_log2 = 0, help = 1, spread = -1, r_split = -1, leaf8 = 0, wf = -1;
+    int r_budget = GI_R_BUDGET;       // Mode R heavy-pixel hand-off (GI_R_BUDGET, candidates; 0: off)
     long long wf_chunk = 8ll << 20;   // wavefront Mode X: units (pixel samples) per chunk = queue capacity
 };
 const XEnv& x_env() {
@@ -1665,6 +1733,7 @@ const XEnv& x_env() {
         if (const char* v = std::getenv("GI_X_HELP")) env.help = std::atoi(v) != 0;
         if (const char* v = std::getenv("GI_X_SPREAD")) env.spread = std::atoi(v);
         if (const char* v = std::getenv("GI_R_SPLIT")) env.r_split = std::atoi(v);
+        if (const char* v = std::getenv("GI_R_BUDGET")) env.r_budget = std::max(0, std::atoi(v));
         if (const char* v = std::getenv("GI_X_LEAF8")) env.leaf8 = std::max(0, std::min(8, std::atoi(v)));
         if (const char* v = std::getenv("GI_X_WF")) env.wf = std::atoi(v);
         if (const char* v = std::getenv("GI_X_WF_CHUNK")) env.wf_chunk = std::max(1ll << 16, std::min(1ll << 30, std::atoll(v)));
@@ -1754,15 +1823,30 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
         // forces either
         const XEnv& env = x_env();
         const bool split = !dfs && (env.r_split >= 0 ? env.r_split != 0 : sc.n_ents > 4096);
+        // heavy-pixel hand-off (k_mode_r_heavy): the budget from GI_R_BUDGET, when the scratch list exists
+        RHeavy hv{xs.rheavy, sc.work + 2, xs.rheavy ? (unsigned)env.r_budget : 0u};
+        if (split && hv.budget) {
+            const hipError_t e0 = hipMemsetAsync(sc.work + 2, 0, sizeof(unsigned), stream);
+            if (e0 != hipSuccess) return e0;
+        }
         mark(ev_begin);
         if (split) {
             const dim3 sgrid((unsigned)((m.n_local * (kTile * kTile) * GI_R_NSUB + 255) / 256));
+            const dim3 hgrid(1024);   // k_mode_r_heavy: 4096 waves loop over the heavy pixels
             if (sc.r_tri_only && GI_R_TRI) {
-                if (stats) hipLaunchKernelGGL((k_mode_r_split<true, GI_R_NSUB, true>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
-                else hipLaunchKernelGGL((k_mode_r_split<false, GI_R_NSUB, true>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
+                if (stats) hipLaunchKernelGGL((k_mode_r_split<true, GI_R_NSUB, true>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, hv);
+                else hipLaunchKernelGGL((k_mode_r_split<false, GI_R_NSUB, true>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, hv);
+                if (hv.budget) {
+                    if (stats) hipLaunchKernelGGL((k_mode_r_heavy<true, true>), hgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, hv);
+                    else hipLaunchKernelGGL((k_mode_r_heavy<false, true>), hgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, hv);
+                }
             } else {
-                if (stats) hipLaunchKernelGGL((k_mode_r_split<true, GI_R_NSUB, false>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
-                else hipLaunchKernelGGL((k_mode_r_split<false, GI_R_NSUB, false>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
+                if (stats) hipLaunchKernelGGL((k_mode_r_split<true, GI_R_NSUB, false>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, hv);
+                else hipLaunchKernelGGL((k_mode_r_split<false, GI_R_NSUB, false>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, hv);
+                if (hv.budget) {
+                    if (stats) hipLaunchKernelGGL((k_mode_r_heavy<true, false>), hgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, hv);
+                    else hipLaunchKernelGGL((k_mode_r_heavy<false, false>), hgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, hv);
+                }
             }
         } else if (stats) {
             hipLaunchKernelGGL(k_mode_r<true>, grid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, dfs);

@@ -232,6 +232,9 @@ struct XScratch {
     unsigned* wcnt = nullptr;
     unsigned* h_nlist = nullptr;
     long long wcap = 0;
+    // Mode R heavy-pixel list of the budgeted split kernel: (pixel slot, rank) per entry, rcap entries
+    long long* rheavy = nullptr;
+    long long rcap = 0;
 };
 
 // Mode X launch configuration, computed once per scene when it is created (gi_capi.cpp, on the

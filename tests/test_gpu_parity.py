@@ -357,9 +357,9 @@ def test_mode_x_multi_sample_units_bit_exact(torch_cuda, tmp_path):
 
 
 def test_mode_x_c3_config_windows_and_shards(torch_cuda):
-    """The bench's own workload: C3 = Cornell 1920x1080, depth 8, 64 spp (the device picks 8-sample
-    work units for the whole frame and 1-sample units for an 8-way shard of it).  Two windows against
-    the oracle, and the 8-shard frame against the whole frame bit for bit."""
+    """The bench's own workload: C3 = Cornell 1920x1080, depth 8, 64 spp (single-sample work units by
+    default, GI_X_MAX_RUN = 1, for the whole frame and for an 8-way shard of it).  Three windows
+    against the oracle, and the 8-shard frame against the whole frame bit for bit."""
     torch = torch_cuda
     sc = S.cornell_scene()
     d = dev_scene("cornell")
