@@ -105,7 +105,7 @@ TILE_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ct
 
 EXPORTS = ["gi_abi_version", "gi_last_error", "gi_camera_init", "gi_scene_create", "gi_scene_destroy",
            "gi_scene_get_info", "gi_render", "gi_render_device", "gi_shard_tiles", "gi_unshard_device",
-           "gi_trace_ray", "gi_kat_expbox", "gi_scene_kernel_ms", "gi_octree_create", "gi_octree_destroy",
+           "gi_trace_ray", "gi_kat_expbox", "gi_scene_kernel_ms", "gi_scene_x_form", "gi_octree_create", "gi_octree_destroy",
            "gi_octree_intersect", "gi_multi_create", "gi_multi_destroy", "gi_multi_info", "gi_multi_render", "gi_device_count",
            "gi_device_list", "gi_build_id", "gi_obj_parse"]
 
@@ -144,6 +144,7 @@ def lib():
         L.gi_trace_ray.argtypes = [vp, dp, dp, dp, ctypes.POINTER(Hit), dp]
         L.gi_kat_expbox.argtypes = [i32, dp, ctypes.POINTER(ctypes.c_int32)]
         L.gi_scene_kernel_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int64)]
+        L.gi_scene_x_form.argtypes = [vp, ctypes.POINTER(Opts), ctypes.POINTER(ctypes.c_int32)]
         L.gi_octree_create.argtypes = [ctypes.POINTER(SceneDesc), ctypes.POINTER(vp)]
         L.gi_octree_destroy.argtypes = [vp]
         L.gi_octree_destroy.restype = None
@@ -479,6 +480,14 @@ class DeviceScene:
         o = self.opts(mode, spp, depth, seed, shard_count, shard_index, stats_ptr=stats_ptr, flags=flags)
         _check(lib().gi_render_device(self._h, ctypes.byref(cam._c), _d3(light), w, h, ctypes.byref(o),
                                       d_rgb or None, d_rgb8 or None, stream or None), "gi_render_device")
+
+    def x_form(self, mode=MODE_X, spp=1, depth=1, flags=0) -> str:
+        """The Mode X form a render with these options would run: "k_mode_x" (persistent path-state
+        kernel) or "k_wf_bounce" (wavefront, one launch per bounce) -- gi_scene_x_form."""
+        o = self.opts(mode, spp, depth, 0, flags=flags)
+        f = ctypes.c_int32()
+        _check(lib().gi_scene_x_form(self._h, ctypes.byref(o), ctypes.byref(f)), "gi_scene_x_form")
+        return "k_wf_bounce" if f.value else "k_mode_x"
 
     def kernel_ms(self):
         """(average ms, launches) of the dominant kernel over the renders issued with FLAG_TIME since

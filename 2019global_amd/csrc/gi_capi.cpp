@@ -654,6 +654,15 @@ int gi_scene_kernel_ms(gi_scene* s, float* avg_ms, int64_t* n) {
     });
 }
 
+int gi_scene_x_form(gi_scene* s, const gi_opts* o, int32_t* form) {
+    return guard([&]() -> int {
+        if (!s || !o || !form) return fail(GI_ERR_ARG, "null argument");
+        std::lock_guard<std::mutex> lk(s->mu);
+        *form = x_wf_choice(s->dev, s->xcfg, *o) ? 1 : 0;
+        return GI_OK;
+    });
+}
+
 int gi_unshard_device(int w, int h, int shard_count, const double* d_packed, const uint8_t* d_packed8, double* d_rgb,
                       uint8_t* d_rgb8, void* stream) {
     return guard([&]() -> int {

@@ -453,7 +453,7 @@ def main():
             # primary (w*h*spp) and total (primary + bounce + shadow) rays per second
             "mray_s_primary": round(w * h * spp * args.steps / elapsed / 1e6, 3),
             "mray_s_all_rays": round(rays_frame * args.steps / elapsed / 1e6, 3),
-            "roofline": {"bound": "hbm", "kernel": "k_mode_x" if mode == 1 else "k_mode_r",
+            "roofline": {"bound": "hbm", "kernel": (dev.x_form(mode, spp, depth) if mode == 1 else "k_mode_r"),
                          "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "alg_bytes_per_launch": int(alg),

@@ -17,6 +17,7 @@
  *   gi_trace_ray         one iteration of raytracer.h:41-84 for an arbitrary ray
  *   gi_unshard_device    reassembles a frame from per-rank packed tiles after the RCCL gather
  *   gi_scene_kernel_ms   HIP-event duration of the last timed render's dominant kernel (bench)
+ *   gi_scene_x_form      which Mode X form (persistent kernel / wavefront) a render would run
  *   gi_octree_*          Octree(min,max) + push_back (octree.h:14-43) and the public query
  *                        Octree::intersect(const Ray&) (octree.h:46-68 -> Node::intersect :132-155)
  *                        on the host, for reference-side callers of the candidate list
@@ -103,8 +104,9 @@ typedef enum gi_mode {
 #define GI_FLAG_STATS 1u   /* accumulate work counters into opts->stats (device pointer) */
 #define GI_FLAG_R_DFS 2u   /* Mode R: walk the whole reference octree in reverse DFS order instead of
                               reconstructing the candidate list (same result; A/B and tests) */
-#define GI_FLAG_TIME 4u    /* record HIP events around the frame's dominant kernel (k_mode_r / k_mode_x)
-                              on the render's stream; averaged by gi_scene_kernel_ms */
+#define GI_FLAG_TIME 4u    /* record HIP events around the frame's dominant kernel (k_mode_r / k_mode_x; the
+                              wavefront form: its whole sequence of bounce kernels) on the render's
+                              stream; averaged by gi_scene_kernel_ms */
 #define GI_FLAG_X_NO_SHADOW 8u   /* Mode X, test only: no shadow rays (every light is visible).  With
                                     depth 1 and spp 1 this reduces Mode X to the reference's own
                                     shading (raytracer.h:41-84, material.h:48-62), so its stages can
@@ -238,6 +240,9 @@ int gi_trace_ray(gi_scene* scene, const double origin[3], const double dir[3], c
  * since the previous call (waits for the last one; *n = how many, may be NULL), then resets.
  * GI_ERR_ARG if there was none. */
 int gi_scene_kernel_ms(gi_scene* scene, float* avg_ms, int64_t* n);
+/* Mode X form a render of `scene` with `opts` would run (bench labels, tests): 0 = the persistent
+ * path-state kernel k_mode_x, 1 = the wavefront form (k_wf_bounce once per bounce); Mode R: 0. */
+int gi_scene_x_form(gi_scene* scene, const gi_opts* opts, int32_t* form);
 
 /* ---- host-side reference octree (no device needed) --------------------------------------------
  * gi_octree_create builds the reference octree from the same descriptors as gi_scene_create (push

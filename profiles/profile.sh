@@ -9,9 +9,10 @@ TAG=$1; shift
 mkdir -p gpurun_out/${TAG}prof
 for W in "$@"; do
   w=$(echo $W | tr A-Z a-z)
-  KERN=k_mode_x; case $W in R-*) KERN=k_mode_r;; esac
+  # the dominant kernel (k_mode_x, k_wf_bounce or k_mode_r) is found by summarize.py; the wavefront
+  # form's figures are per frame (3 timed + 1 warm-up frames)
   bash profiles/run_profile.sh ${w}_${TAG} --workload $W --steps 3 --warmup 1 || { echo "profile $W failed"; exit 1; }
-  python3 profiles/summarize.py gpurun_out/prof_${w}_${TAG} $W $KERN gpurun_out/${TAG}prof/${TAG}_${w}_pmc.json || exit 1
+  python3 profiles/summarize.py gpurun_out/prof_${w}_${TAG} $W auto gpurun_out/${TAG}prof/${TAG}_${w}_pmc.json 4 || exit 1
   cp gpurun_out/prof_${w}_${TAG}/trace/run_kernel_stats.csv gpurun_out/${TAG}prof/${TAG}_${w}_kernel_stats.csv
 done
 echo profiles done

@@ -10,7 +10,12 @@
     half of the bytes of wide reads, MI355X_MICROARCH.md §HBM, so it is doubled — an upper bound
     for narrower access widths).
 
-    python profiles/summarize.py gpurun_out/prof_c3 C3 k_mode_x profiles/r01_c3_pmc.json
+    python profiles/summarize.py gpurun_out/prof_c3 C3 k_mode_x profiles/r01_c3_pmc.json [frames]
+
+kernel "auto": the dominant one of k_mode_x / k_wf_bounce / k_mode_r (by total time).  The wavefront
+form (k_wf_bounce) launches once per bounce, so its figures are per FRAME: `frames` (the bench's
+timed + warm-up frames) given, avg_launch_ns and every counter are the sums over the frame's
+dispatches (per PMC pass: sum over all dispatches / frames).
 """
 import csv
 import glob
@@ -20,19 +25,30 @@ import sys
 from collections import defaultdict
 
 
-def main(d, workload, kernel, out):
+def main(d, workload, kernel, out, frames=None):
+    frames = int(frames) if frames else None
     stats = {}
     for r in csv.DictReader(open(os.path.join(d, "trace", "run_kernel_stats.csv"))):
         stats[r["Name"]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                             "total_ns": float(r["TotalDurationNs"]), "pct": float(r["Percentage"])}
+    if kernel == "auto":
+        kernel = max(("k_mode_x", "k_wf_bounce", "k_mode_r"),
+                     key=lambda kn: sum(v["total_ns"] for k, v in stats.items() if kn + "<false" in k))
     # the timed launches: STATS=false is the kernel's first template argument (k_mode_x<false, ...>)
     dom = [k for k in stats if kernel + "<false" in k] or [k for k in stats if kernel in k]
     dom_name = max(dom, key=lambda k: stats[k]["total_ns"])
+    per_frame = frames is not None and "k_wf_bounce" in dom_name
     ctr = defaultdict(list)
     for f in sorted(glob.glob(os.path.join(d, "pmc*", "run_counter_collection.csv"))):
+        run = defaultdict(float)
         for r in csv.DictReader(open(f)):
             if r["Kernel_Name"] == dom_name:
-                ctr[r["Counter_Name"]].append(float(r["Counter_Value"]))
+                if per_frame:
+                    run[r["Counter_Name"]] += float(r["Counter_Value"]) / frames
+                else:
+                    ctr[r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for k, v in run.items():
+            ctr[k].append(v)
     avg = {k: sum(v) / len(v) for k, v in ctr.items()}
     der = {}
     if "SQ_THREAD_CYCLES_VALU" in avg and avg.get("SQ_ACTIVE_INST_VALU"):
@@ -46,7 +62,9 @@ def main(d, workload, kernel, out):
     hbm = None
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
         hbm = (2.0 * avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024.0
-    res = {"workload": workload, "kernel": dom_name, "avg_launch_ns": stats[dom_name]["avg_ns"],
+    launch_ns = stats[dom_name]["total_ns"] / frames if per_frame else stats[dom_name]["avg_ns"]
+    res = {"workload": workload, "kernel": dom_name, "avg_launch_ns": launch_ns,
+           "per": "frame (sum over the per-bounce dispatches)" if per_frame else "dispatch",
            "hbm_bytes_per_launch": hbm, "counters_per_launch": avg, "derived": der,
            "kernel_stats": stats}
     json.dump(res, open(out, "w"), indent=1)
@@ -54,4 +72,4 @@ def main(d, workload, kernel, out):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:5])
+    main(*sys.argv[1:6])
