@@ -48,7 +48,9 @@ FLAG_R_DFS = 2   # Mode R: reverse-DFS over the whole reference octree (A/B agai
 FLAG_TIME = 4    # HIP events around the dominant kernel; read with DeviceScene.kernel_ms()
 FLAG_X_NO_SHADOW = 8   # Mode X, tests only: no shadow rays (reduces depth-1 Mode X to the reference's shading)
 FLAG_X_WF = 16   # Mode X: the wavefront form (one launch per bounce over compacted path queues, gi_wf.hip)
-FLAG_X_MEGA = 32   # Mode X: the persistent path-state kernel k_mode_x (neither flag: chosen per launch)
+FLAG_X_MEGA = 32   # Mode X: the persistent path-state kernel k_mode_x
+FLAG_X_SEG = 64   # Mode X: the segment-synchronous persistent form k_seg (no form flag: chosen per launch)
+X_FORMS = ("k_mode_x", "k_wf_bounce", "k_seg")   # gi_scene_x_form's values
 STAT_RAYS, STAT_NODES, STAT_PRIMS, STAT_PIXELS, STAT_X_PATH_MAX = 0, 1, 2, 3, 4
 STAT_X_ITERS, STAT_X_TRAV, STAT_X_HANDLE, STAT_X_HLANES, STAT_X_HCLOSE, STAT_X_HSHADOW = 5, 6, 7, 8, 9, 10
 STAT_X_CYC_TRAV, STAT_X_CYC_HIT, STAT_X_CYC_NEXT, STAT_X_CYC_ALL = 11, 12, 13, 14
@@ -483,11 +485,12 @@ class DeviceScene:
 
     def x_form(self, mode=MODE_X, spp=1, depth=1, flags=0) -> str:
         """The Mode X form a render with these options would run: "k_mode_x" (persistent path-state
-        kernel) or "k_wf_bounce" (wavefront, one launch per bounce) -- gi_scene_x_form."""
+        kernel), "k_wf_bounce" (wavefront, one launch per bounce) or "k_seg" (segment-synchronous) --
+        gi_scene_x_form."""
         o = self.opts(mode, spp, depth, 0, flags=flags)
         f = ctypes.c_int32()
         _check(lib().gi_scene_x_form(self._h, ctypes.byref(o), ctypes.byref(f)), "gi_scene_x_form")
-        return "k_wf_bounce" if f.value else "k_mode_x"
+        return X_FORMS[f.value]
 
     def kernel_ms(self):
         """(average ms, launches) of the dominant kernel over the renders issued with FLAG_TIME since

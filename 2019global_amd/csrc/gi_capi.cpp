@@ -22,7 +22,7 @@ namespace gi {
 bool build_host_scene(const gi_scene_desc& desc, HostScene& hs, std::string& err);
 long long shard_tiles(int w, int h, int shard_count);
 hipError_t x_launch_config(const DevScene& sc, int device, XLaunchCfg& cfg);
-bool x_wf_choice(const DevScene& sc, const XLaunchCfg& xc, const gi_opts& o);
+int x_form_choice(const DevScene& sc, const XLaunchCfg& xc, const gi_opts& o);
 long long x_wf_chunk();
 hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev& cam, V3 light, int w, int h, int y0,
                          const gi_opts& o, double* rgb, uint8_t* rgb8, const XScratch& xs, KTimer* kt,
@@ -149,14 +149,15 @@ int ensure_xscratch(gi_scene* s, int w, int h, const gi_opts* o) {
             return hip_fail(e, "hipMalloc (per-sample radiance)");
         x.spp = o->spp;
     }
-    if (x_wf_choice(s->dev, s->xcfg, *o)) {   // wavefront form: path queues sized to a chunk of units
+    const int form = x_form_choice(s->dev, s->xcfg, *o);
+    if (form) {   // wavefront forms: counters; form 1 also path queues sized to a chunk of units
         const long long want = std::max(64ll, std::min(x_wf_chunk(), need * (long long)o->spp));
         if (!x.wcnt) {
             if ((e = hipMalloc((void**)&x.wcnt, 2 * 64 * sizeof(unsigned))) != hipSuccess) return hip_fail(e, "hipMalloc (wavefront counters)");
             if ((e = hipHostMalloc((void**)&x.h_nlist, sizeof(unsigned), hipHostMallocDefault)) != hipSuccess)
                 return hip_fail(e, "hipHostMalloc (wavefront)");
         }
-        if (x.wcap < want) {
+        if (form == 1 && x.wcap < want) {
             for (int q = 0; q < 2; ++q) {
                 (void)hipFree(x.wq[q]);
                 (void)hipFree(x.wid[q]);
@@ -658,7 +659,7 @@ int gi_scene_x_form(gi_scene* s, const gi_opts* o, int32_t* form) {
     return guard([&]() -> int {
         if (!s || !o || !form) return fail(GI_ERR_ARG, "null argument");
         std::lock_guard<std::mutex> lk(s->mu);
-        *form = x_wf_choice(s->dev, s->xcfg, *o) ? 1 : 0;
+        *form = x_form_choice(s->dev, s->xcfg, *o);
         return GI_OK;
     });
 }

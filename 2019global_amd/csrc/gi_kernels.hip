@@ -283,6 +283,29 @@ __device__ __forceinline__ uint32_t children_mask_line(const XWNode* nd, F3 of, 
     return m;
 }
 
+// The same 8 tests spread over the NSUB (>= 8) lanes of a pixel group that walk one line
+// (k_mode_r_split): lane sub tests child sub & 7 only -- its six bounds are one float each, and the
+// group's 8 lanes read 8 consecutive floats of each plane array -- and a ballot gathers the mask, the
+// same in every lane.  Per child the arithmetic is children_mask_line's, so the mask is identical.
+#ifndef GI_R_COOP
+#define GI_R_COOP 0   // cooperative line-BVH node tests in k_mode_r_split / k_mode_r_heavy
+#endif
+template <int NSUB>
+__device__ __forceinline__ uint32_t children_mask_line_coop(const XWNode* nd, F3 of, F3 ivf, float tau, int sub) {
+    const int c = sub & 7;
+    const int sm = iv_signs(ivf);
+    const float nx = (sm & 1) ? nd->hi[0][c] : nd->lo[0][c], fx = (sm & 1) ? nd->lo[0][c] : nd->hi[0][c];
+    const float ny = (sm & 2) ? nd->hi[1][c] : nd->lo[1][c], fy = (sm & 2) ? nd->lo[1][c] : nd->hi[1][c];
+    const float nz = (sm & 4) ? nd->hi[2][c] : nd->lo[2][c], fz = (sm & 4) ? nd->lo[2][c] : nd->hi[2][c];
+    const float sx = (sm & 1) ? tau : -tau, sy = (sm & 2) ? tau : -tau, sz = (sm & 4) ? tau : -tau;
+    const float tn = fmaxf(fmaxf(((nx + sx) - of.x) * ivf.x, ((ny + sy) - of.y) * ivf.y), ((nz + sz) - of.z) * ivf.z);
+    const float tf = fminf(fminf(((fx - sx) - of.x) * ivf.x, ((fy - sy) - of.y) * ivf.y), ((fz - sz) - of.z) * ivf.z);
+    const bool hit = (tn <= tf) & ((nd->exists >> c) & 1);
+    const unsigned long long b = __ballot(hit);
+    const int base = (int)(threadIdx.x & 63) & ~(NSUB - 1);
+    return (uint32_t)((b >> base) & 0xFFull);
+}
+
 // Per-ray memo of node-test results (k_mode_r_split): the candidates' root paths share their upper
 // levels -- every path starts at the root -- and an exact ExpBox node test is ~12 fp32/fp64 triangle
 // solves, so a ray that walks many appearances' paths would repeat the same tests.  Direct-mapped,
@@ -435,7 +458,8 @@ __device__ __forceinline__ bool trace_mode_r_split(const DevScene& sc, V3 o, V3 
     const F3 ivf = inv_dir(d);   // clamped to +-1e30: finite plane distances, near / far by sign
     uint64_t mlo = 0, mhi = 0;
     int node = 0, level = 0;
-    const uint32_t rm = children_mask_line(W, of, ivf, tau);
+    constexpr bool COOP = GI_R_COOP != 0 && NSUB >= 8;
+    const uint32_t rm = COOP ? children_mask_line_coop<NSUB>(W, of, ivf, tau, sub) : children_mask_line(W, of, ivf, tau);
     lvl_set(mlo, mhi, 0, rm);
     bool going = rm != 0;
     while (going) {
@@ -454,7 +478,8 @@ __device__ __forceinline__ bool trace_mode_r_split(const DevScene& sc, V3 o, V3 
             best = group_max<NSUB>(best);
             if (budget && k > budget) return true;
         } else {
-            const uint32_t cm = children_mask_line(W + ch, of, ivf, tau);
+            const uint32_t cm = COOP ? children_mask_line_coop<NSUB>(W + ch, of, ivf, tau, sub)
+                                     : children_mask_line(W + ch, of, ivf, tau);
             if (cm) {
                 node = ch;
                 ++level;
@@ -1747,27 +1772,28 @@ const XEnv& x_env() {
 }
 
 // wavefront Mode X (gi_wf.hip)
-hipError_t launch_wf(const DevScene& sc, int kv, size_t lds_bytes, int resident, const CamDev& cam, V3 light, int w,
-                     int h, int y0, const gi_opts& o, double* rgb, uint8_t* rgb8, const XScratch& xs,
+hipError_t launch_wf(const DevScene& sc, int kv, size_t lds_bytes, int resident, int form, const CamDev& cam, V3 light,
+                     int w, int h, int y0, const gi_opts& o, double* rgb, uint8_t* rgb8, const XScratch& xs,
                      const unsigned* n_list_dev, unsigned long long* stats, int xflags, hipStream_t stream,
                      hipEvent_t ev_begin, hipEvent_t ev_end);
-hipError_t wf_occupancy(const DevScene& sc, int kv, size_t lds_bytes, int* per_cu);
+hipError_t wf_occupancy(const DevScene& sc, int kv, size_t lds_bytes, int form, int* per_cu);
 size_t wf_slot_bytes();
 
 #ifndef GI_WF_MAX_DEPTH
 #define GI_WF_MAX_DEPTH 64   // the wavefront form launches once per bounce: deeper paths run k_mode_x
 #endif
-// Mode X form of a launch: the wavefront kernels (true) or the persistent path-state kernel.
-// GI_FLAG_X_WF / GI_FLAG_X_MEGA force either (tests, A/B), then GI_X_WF=0/1; by default the scenes
-// staged in LDS run the wavefront form (DESIGN.md §5 "Wavefront Mode X").
-bool x_wf_choice(const DevScene& sc, const XLaunchCfg& xc, const gi_opts& o) {
-    if (o.mode != GI_MODE_X || o.depth > GI_WF_MAX_DEPTH || (o.flags & GI_FLAG_X_MEGA)) return false;
-    if (o.flags & GI_FLAG_X_WF) return true;
+// Mode X form of a launch: 0 the persistent path-state kernel (k_mode_x), 1 the wavefront form
+// (k_wf_bounce once per bounce over compacted queues), 2 the segment-synchronous form (k_seg).
+// GI_FLAG_X_MEGA / _WF / _SEG force one (tests, A/B), then GI_X_WF=0/1/2; by default ....
+int x_form_choice(const DevScene& sc, const XLaunchCfg& xc, const gi_opts& o) {
+    if (o.mode != GI_MODE_X || (o.flags & GI_FLAG_X_MEGA)) return 0;
+    if (o.flags & GI_FLAG_X_SEG) return 2;
+    if (o.flags & GI_FLAG_X_WF) return o.depth <= GI_WF_MAX_DEPTH ? 1 : 0;
     const XEnv& env = x_env();
-    if (env.wf >= 0) return env.wf != 0;
+    if (env.wf >= 0) return env.wf == 1 ? (o.depth <= GI_WF_MAX_DEPTH ? 1 : 0) : env.wf == 2 ? 2 : 0;
     (void)sc;
     (void)xc;
-    return false;   // until measured on the GPU (round 4)
+    return 0;   // until measured on the GPU (round 4)
 }
 long long x_wf_chunk() { return x_env().wf_chunk; }
 
@@ -1791,9 +1817,12 @@ hipError_t x_launch_config(const DevScene& sc, int device, XLaunchCfg& cfg) {
     if (e != hipSuccess) return e;
     cfg.resident = std::max(1, cus) * std::max(1, per_cu);
     cfg.wf_lds_bytes = (lds ? (size_t)sc.x_lds_bytes : 16 * 256 * sizeof(int)) + wf_slot_bytes();
-    e = wf_occupancy(sc, cfg.kv, cfg.wf_lds_bytes, &per_cu);
+    e = wf_occupancy(sc, cfg.kv, cfg.wf_lds_bytes, 1, &per_cu);
     if (e != hipSuccess) return e;
     cfg.wf_resident = std::max(1, cus) * std::max(1, per_cu);
+    e = wf_occupancy(sc, cfg.kv, cfg.wf_lds_bytes, 2, &per_cu);
+    if (e != hipSuccess) return e;
+    cfg.seg_resident = std::max(1, cus) * std::max(1, per_cu);
     return hipSuccess;
 }
 
@@ -1891,10 +1920,10 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
         const int xf = (env.xf >= 0 ? env.xf : sc.x_flags) | (env.run_log2 << 8) |
                        ((o.flags & GI_FLAG_X_NO_SHADOW) ? 4 : 0) | (env.help ? 8 : 0) |
                        ((env.spread > 0 || (env.spread < 0 && help)) ? 16 : 0) | (env.leaf8 << 12);
-        if (x_wf_choice(sc, xc, o)) {   // the wavefront form (gi_wf.hip), timed as one pass
-            if (!xs.wq[0] || !xs.wq[1] || !xs.wcnt || !xs.h_nlist || xs.wcap <= 0) return hipErrorInvalidValue;
-            e = launch_wf(sc, xc.kv, xc.wf_lds_bytes, xc.wf_resident, cam, light, w, h, y0, o, rgb, rgb8, xs, sc.work + 1,
-                          stats ? st : nullptr, xf, stream, ev_begin, ev_end);
+        if (const int form = x_form_choice(sc, xc, o)) {   // gi_wf.hip's forms, timed as one pass
+            if (!xs.wcnt || (form == 1 && (!xs.wq[0] || !xs.wq[1] || !xs.h_nlist || xs.wcap <= 0))) return hipErrorInvalidValue;
+            e = launch_wf(sc, xc.kv, xc.wf_lds_bytes, form == 2 ? xc.seg_resident : xc.wf_resident, form, cam, light, w, h, y0,
+                          o, rgb, rgb8, xs, sc.work + 1, stats ? st : nullptr, xf, stream, ev_begin, ev_end);
             if (e != hipSuccess) return e;
             if (o.spp > 1) hipLaunchKernelGGL(k_x_reduce, sgrid, dim3(256), 0, stream, m, wk, o.spp, rgb, rgb8);
             if (timed) kt->recorded++;

@@ -243,8 +243,9 @@ struct XLaunchCfg {
     int kv = 0;              // kernel variant: 2 * (LDS-resident scene) + (4 waves per SIMD)
     size_t lds_bytes = 0;    // dynamic LDS per workgroup
     int resident = 1;        // resident 256-thread workgroups on the device (occupancy x CUs)
-    size_t wf_lds_bytes = 0; // wavefront Mode X (k_wf_bounce): dynamic LDS per workgroup
-    int wf_resident = 1;     //   and its resident workgroups
+    size_t wf_lds_bytes = 0; // wavefront Mode X (k_wf_bounce, k_seg): dynamic LDS per workgroup
+    int wf_resident = 1;     //   and the resident workgroups of k_wf_bounce
+    int seg_resident = 1;    //   and of k_seg
 };
 
 }  // namespace gi

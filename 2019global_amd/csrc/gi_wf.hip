@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <mutex>
+#include <type_traits>
 
 #include "gi.h"
 #include "gi_dev.h"
@@ -34,6 +35,9 @@ namespace {
 #endif
 #ifndef GI_WF_MIN_WAVES
 #define GI_WF_MIN_WAVES 3       // other scenes
+#endif
+#ifndef GI_WF_TAKE
+#define GI_WF_TAKE 16   // most 64-entry batches a wave takes per atomic on the queue's counter
 #endif
 #ifndef GI_WF_PSL
 // a path's L and T wait out the two traversals in a per-lane LDS slot (column layout, 6 x 256 fp64 per
@@ -164,29 +168,22 @@ struct WFArgs {
     unsigned long long u0, u1; // bounce 0: the chunk's units [u0, u1) of n_list * spp
 };
 
-// One bounce of every live path.  Persistent grid: each wave takes 64 queue entries with one atomic
-// until the queue is exhausted.  LDS: the scene (wide nodes, leaf records, primitives, entities) is
-// staged in LDS by each workgroup, as in k_mode_x; otherwise HBM-resident (CN: quantised nodes).
-template <bool STATS, bool LDS, bool W4, bool SH, bool TRI, bool CN>
-__global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_WAVES) void k_wf_bounce(
-    DevScene sc, CamDev cam, V3 light, TileMap m, int spp, int depth, uint64_t seed, int b, double* rgb, uint8_t* rgb8,
-    unsigned long long* stats, WFArgs a, WFQ qin, WFQ qout, int xflags) {
-    // the bounce's input length: bounce 0, the chunk's units of the work list; else the queue
-    unsigned n_in;
-    if (b == 0) {
-        const unsigned long long tot = (unsigned long long)*a.n_list * (unsigned long long)spp;
-        n_in = (unsigned)(min(tot, a.u1) > a.u0 ? min(tot, a.u1) - a.u0 : 0ull);
-    } else {
-        n_in = *a.n_in;
-    }
-    if (*(volatile unsigned*)a.take >= n_in) return;   // nothing left (before staging the scene)
-    extern __shared__ int4 lds_dyn[];
+// The scene views of a bounce / segment kernel.  LDS: wide nodes, leaf records, primitives and
+// entities staged in LDS by the workgroup (as k_mode_x does); then the per-lane path slots (GI_WF_PSL).
+// HBM-resident scenes: the per-lane level stack (16 x 256 ints), then the path slots.
+struct WFView {
     const XWNode* LW = nullptr;
     const XHot* LH = nullptr;
-    const XPrim* XP = sc.xprims;
-    const REnt* EN = sc.ents;
+    const XPrim* XP = nullptr;
+    const REnt* EN = nullptr;
     int* nst = nullptr;
-    double* pl = nullptr;   // GI_WF_PSL: this lane's L (fields 0-2) and T (3-5), pl[f * 256]
+    double* pl = nullptr;   // this lane's L (fields 0-2) and T (3-5), pl[f * 256]
+};
+template <bool LDS>
+__device__ __forceinline__ WFView wf_stage(const DevScene& sc, int4* lds_dyn) {
+    WFView v;
+    v.XP = sc.xprims;
+    v.EN = sc.ents;
     if constexpr (LDS) {
         const int nw = sc.n_xwnodes * (int)(sizeof(XWNode) / sizeof(int4));
         const int nh = sc.n_xhot * (int)(sizeof(XHot) / sizeof(int4));
@@ -201,30 +198,183 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
         for (int i = threadIdx.x; i < np; i += blockDim.x) lds_dyn[nw + nh + i] = gp[i];
         for (int i = threadIdx.x; i < ne; i += blockDim.x) lds_dyn[nw + nh + np + i] = ge[i];
         __syncthreads();
-        LW = reinterpret_cast<const XWNode*>(lds_dyn);
-        LH = reinterpret_cast<const XHot*>(lds_dyn + nw);
-        XP = reinterpret_cast<const XPrim*>(lds_dyn + nw + nh);
-        EN = reinterpret_cast<const REnt*>(lds_dyn + nw + nh + np);
-        pl = reinterpret_cast<double*>(lds_dyn + nw + nh + np + ne) + threadIdx.x;
+        v.LW = reinterpret_cast<const XWNode*>(lds_dyn);
+        v.LH = reinterpret_cast<const XHot*>(lds_dyn + nw);
+        v.XP = reinterpret_cast<const XPrim*>(lds_dyn + nw + nh);
+        v.EN = reinterpret_cast<const REnt*>(lds_dyn + nw + nh + np);
+        v.pl = reinterpret_cast<double*>(lds_dyn + nw + nh + np + ne) + threadIdx.x;
     } else {
-        nst = reinterpret_cast<int*>(lds_dyn) + threadIdx.x;   // 16 levels x 256 lanes
-        pl = reinterpret_cast<double*>(reinterpret_cast<int*>(lds_dyn) + 16 * 256) + threadIdx.x;
+        v.nst = reinterpret_cast<int*>(lds_dyn) + threadIdx.x;   // 16 levels x 256 lanes
+        v.pl = reinterpret_cast<double*>(reinterpret_cast<int*>(lds_dyn) + 16 * 256) + threadIdx.x;
     }
+    return v;
+}
+
+// The unit (work-list index li, sample smp) of a pixel's sample: its pixel, RNG key and primary
+// direction (the reference's corner ray, jittered for spp > 1).  idx: the output slot (the
+// per-sample radiance row for spp > 1, else the pixel).
+__device__ __forceinline__ V3 wf_primary(const CamDev& cam, const TileMap& m, unsigned ps, int spp, uint64_t seed,
+                                         unsigned li, unsigned smp, long long& idx, uint64_t& key) {
+    int x = 0, y = 0;   // ps: the work list's entry li (the pixel slot)
+    slot_pixel(m, (long long)(ps >> 6), (int)(ps & 63), idx, x, y);
+    y += m.y0;
+    if (spp > 1) idx = (long long)li;
+    key = mx_key(seed, (uint64_t)y * (uint64_t)m.w + (uint64_t)x);
+    double jx = 0.0, jy = 0.0;
+    if (spp > 1) {
+        jx = mx_u01k(key, smp, 0xFFFF, 0);
+        jy = mx_u01k(key, smp, 0xFFFF, 1);
+    }
+    return primary_dir(cam, (double)x + jx, (double)y + jy);
+}
+// conservative fp32 test of the scene's root box on the unnormalised primary direction: a miss adds
+// exactly +0 (the oracle traces it and adds L = 0)
+__device__ __forceinline__ bool wf_primary_misses(const DevScene& sc, const CamDev& cam, V3 d0) {
+    const F3 iv0 = f3(__builtin_amdgcn_rcpf((float)d0.x), __builtin_amdgcn_rcpf((float)d0.y), __builtin_amdgcn_rcpf((float)d0.z));
+    return !root_hit(sc, f3((float)cam.pos.x, (float)cam.pos.y, (float)cam.pos.z), iv0);
+}
+// the path's radiance once it ends: its per-sample row (spp > 1; k_x_reduce adds a pixel's rows in
+// sample order) or, with one sample, the pixel: min((0 + L) / 1, 1), the reduce pass's operations
+__device__ __forceinline__ void wf_store(double* part, double* rgb, uint8_t* rgb8, int spp, long long idx, unsigned smp, V3 L) {
+    if (spp > 1) {
+        double* q = part + 3 * ((size_t)idx * (size_t)spp + (size_t)smp);
+        q[0] = L.x; q[1] = L.y; q[2] = L.z;
+    } else {
+        const double c0 = smin((0.0 + L.x) / 1.0, 1.0), c1 = smin((0.0 + L.y) / 1.0, 1.0), c2 = smin((0.0 + L.z) / 1.0, 1.0);
+        if (rgb) { rgb[3 * idx] = c0; rgb[3 * idx + 1] = c1; rgb[3 * idx + 2] = c2; }
+        if (rgb8) quantize(c0, c1, c2, rgb8 + 3 * idx);
+    }
+}
+
+// One path segment, bounce b (every lane of the wave runs the same sequence): closest hit -> hit
+// point and light direction -> shadow any-hit -> texture and Blinn-Phong with the shadow answer ->
+// L += T * local -> the next direction (mirror with probability refl, else T *= texel / 2 and a
+// cosine-weighted direction).  The oracle's operations (sample_mode_x).  In: o, d and (GI_WF_PSL: in
+// the lane's path slot, else in L, T) the path's L and T.  Out: true when the path continues (o, d
+// set to its next ray; L, T in registers and, GI_WF_PSL, in the slot); false when it ends (L final).
+template <bool LDS, bool SH, bool TRI, bool CN>
+__device__ __forceinline__ bool x_segment(const DevScene& sc, const WFView& v, V3 light, int depth, bool no_shadow, bool act,
+                                          int b, uint64_t key, unsigned smp, V3& o, V3& d, V3& L, V3& T,
+                                          uint32_t& nnode, uint32_t& nprim, uint32_t& nrays) {
+    // ---- closest hit
+    double tbest = INFINITY;
+    int best;
+    if constexpr (LDS) best = wf_trace<false, true, true, SH, TRI, false>(v.LW, v.LH, o, d, INFINITY, act, v.nst, tbest, nnode, nprim);
+    else if constexpr (CN) best = wf_trace<false, false, false, SH, TRI, true>(sc.xcnodes, sc.xhot, o, d, INFINITY, act, v.nst, tbest, nnode, nprim);
+    else best = wf_trace<false, false, false, SH, TRI, true>(sc.xwnodes, sc.xhot, o, d, INFINITY, act, v.nst, tbest, nnode, nprim);
+    if (act) ++nrays;
+    const bool hit = act && best >= 0;
+    // ---- the hit point and its shadow ray toward the point light
+    V3 P = o, Ld = v3(0, 0, 1);
+    double ldist = 0.0;
+    if (hit) {
+        P = o + tbest * d;
+        const V3 lv = light - P;
+        ldist = gsqrt(dot(lv, lv));
+        Ld = normalize(lv);
+    }
+    bool occl = false;
+    if (!no_shadow) {
+        double tdummy;
+        int sb;
+        if constexpr (LDS) sb = wf_trace<true, true, true, SH, TRI, false>(v.LW, v.LH, P, Ld, ldist, hit, v.nst, tdummy, nnode, nprim);
+        else if constexpr (CN) sb = wf_trace<true, false, false, SH, TRI, true>(sc.xcnodes, sc.xhot, P, Ld, ldist, hit, v.nst, tdummy, nnode, nprim);
+        else sb = wf_trace<true, false, false, SH, TRI, true>(sc.xwnodes, sc.xhot, P, Ld, ldist, hit, v.nst, tdummy, nnode, nprim);
+        occl = sb >= 0;
+    }
+    if (GI_WF_PSL && act) {
+        L = v3(v.pl[0], v.pl[256], v.pl[512]);
+        T = v3(v.pl[768], v.pl[1024], v.pl[1280]);
+    }
+    // ---- shading (local = ambient, + diffuse + specular when lit)
+    bool cont = false;
+    if (hit) {
+        ++nrays;   // the shadow ray
+        const XPrim& p = v.XP[best];   // the facing normal (after the shadow ray: fewer live values)
+        V3 N = (TRI || p.kind == 0) ? ld3(p.n) : normalize(P - ld3(p.a));
+        if (!(dot(d, N) < 0)) N = -N;
+        const REnt& e = v.EN[p.ent];
+        int32_t tu, tv;
+        x_texcoord<TRI>(sc, e, P, tu, tv);
+        const V3 tc = texel(ld3(e.color), tu, tv);
+        const V3 la = tc * e.shader[0];
+        V3 loc = la;
+        if (!occl) {
+            const V3 ldf = (smax(0.0, dot(N, Ld)) * (tc * 0.5)) * e.shader[1];
+            const V3 bis = normalize(normalize(-d) + Ld);
+            const double spw = mx_pow(smax(0.0, dot(N, bis)), e.spec_pow);
+            const V3 ls = v3(spw, spw, spw) * e.shader[2];
+            loc = (la + ldf) + ls;
+        }
+        L = L + vmul(T, v3(smin(loc.x, 1.0), smin(loc.y, 1.0), smin(loc.z, 1.0)));
+        if (b != depth - 1) {
+            if (e.refl > 0.0 && mx_u01k(key, smp, b, 4) < e.refl) {   // mirror: T unchanged
+                d = normalize(d - N * (2.0 * dot(d, N)));
+                cont = true;
+            } else {
+                T = vmul(T, tc * 0.5);
+                if (!(T.x == 0.0 && T.y == 0.0 && T.z == 0.0)) {
+                    double sx, sy, r2;   // concentric disk + Malley
+                    mx_disk(mx_u01k(key, smp, b, 2), mx_u01k(key, smp, b, 3), sx, sy, r2);
+                    const double sz = gsqrt(1.0 - r2);
+                    const double sg = N.z >= 0.0 ? 1.0 : -1.0;   // Duff et al. 2017 basis
+                    const double aa = -1.0 / (sg + N.z);
+                    const double bb = N.x * N.y * aa;
+                    const V3 bt1 = v3(1.0 + sg * N.x * N.x * aa, sg * bb, -sg * N.x);
+                    const V3 bt2 = v3(bb, sg + N.y * N.y * aa, -N.y);
+                    d = normalize((bt1 * sx + bt2 * sy) + N * sz);
+                    cont = true;
+                }
+            }
+            o = P;
+        }
+        if (GI_WF_PSL && cont) {
+            v.pl[0] = L.x; v.pl[256] = L.y; v.pl[512] = L.z;
+            v.pl[768] = T.x; v.pl[1024] = T.y; v.pl[1280] = T.z;
+        }
+    }
+    return cont;
+}
+
+// One bounce of every live path (the wavefront form).  Persistent grid: each wave takes GI_WF_TAKE
+// batches of 64 queue entries per atomic until the queue is exhausted.
+template <bool STATS, bool LDS, bool W4, bool SH, bool TRI, bool CN>
+__global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_WAVES) void k_wf_bounce(
+    DevScene sc, CamDev cam, V3 light, TileMap m, int spp, int depth, uint64_t seed, int b, double* rgb, uint8_t* rgb8,
+    unsigned long long* stats, WFArgs a, WFQ qin, WFQ qout, int xflags) {
+    // the bounce's input length: bounce 0, the chunk's units of the work list; else the queue
+    unsigned n_in;
+    if (b == 0) {
+        const unsigned long long tot = (unsigned long long)*a.n_list * (unsigned long long)spp;
+        n_in = (unsigned)(min(tot, a.u1) > a.u0 ? min(tot, a.u1) - a.u0 : 0ull);
+    } else {
+        n_in = *a.n_in;
+    }
+    if (*(volatile unsigned*)a.take >= n_in) return;   // nothing left (before staging the scene)
+    extern __shared__ int4 lds_dyn[];
+    const WFView v = wf_stage<LDS>(sc, lds_dyn);
     const bool no_shadow = (xflags & 4) != 0;
     const int lane = threadIdx.x & 63;
     uint32_t nnode = 0, nprim = 0, nrays = 0, nres = 0, npx = 0;
     const long long qc = qin.cap, oc = qout.cap;
+    // batches per atomic: up to GI_WF_TAKE, fewer when the queue has fewer than about 8 runs per
+    // resident wave (small queues: every wave gets work)
+    const unsigned take = (unsigned)max(1u, min((unsigned)GI_WF_TAKE, n_in / (64u * 8u * (gridDim.x * (blockDim.x >> 6)))));
+    unsigned base = 0, left = 0;   // the wave's current run of take x 64 entries
     for (;;) {
-        unsigned base = 0;
-        if (lane == 0) base = atomicAdd(a.take, 64u);
-        base = __shfl(base, 0);
+        if (left == 0) {
+            if (lane == 0) base = atomicAdd(a.take, 64u * take);
+            base = __shfl(base, 0);
+            left = take;
+        }
         if (base >= n_in) break;
         const unsigned j = base + (unsigned)lane;
+        base += 64u;
+        --left;
         bool act = j < n_in;
         unsigned li = 0, smp = 0;
         V3 o = cam.pos, d = v3(1, 0, 0), L = v3(0, 0, 0), T = v3(1, 1, 1);
         long long idx = -1;
-        int x = 0, y = 0;
         uint64_t key = 0;
         if (act) {
             if (b == 0) {
@@ -246,118 +396,25 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
                 L = v3(r[6 * qc], r[7 * qc], r[8 * qc]);
                 T = v3(r[9 * qc], r[10 * qc], r[11 * qc]);
             }
-            const unsigned ps = a.list[li];
-            slot_pixel(m, (long long)(ps >> 6), (int)(ps & 63), idx, x, y);
-            y += m.y0;
-            if (spp > 1) idx = (long long)li;   // the per-sample radiance row
-            key = mx_key(seed, (uint64_t)y * (uint64_t)m.w + (uint64_t)x);
+            const V3 d0 = wf_primary(cam, m, a.list[li], spp, seed, li, smp, idx, key);
             if (b == 0) {   // the unit's primary ray
-                double jx = 0.0, jy = 0.0;
-                if (spp > 1) {
-                    jx = mx_u01k(key, smp, 0xFFFF, 0);
-                    jy = mx_u01k(key, smp, 0xFFFF, 1);
-                }
-                const V3 d0 = primary_dir(cam, (double)x + jx, (double)y + jy);
                 if (smp == 0) ++npx;
-                // conservative fp32 test of the scene's root box on the unnormalised direction: a
-                // miss adds exactly +0 (the oracle traces it and adds L = 0)
-                const F3 iv0 = f3(__builtin_amdgcn_rcpf((float)d0.x), __builtin_amdgcn_rcpf((float)d0.y),
-                                  __builtin_amdgcn_rcpf((float)d0.z));
-                if (!root_hit(sc, f3((float)cam.pos.x, (float)cam.pos.y, (float)cam.pos.z), iv0)) {
+                if (wf_primary_misses(sc, cam, d0)) {
                     ++nrays;
                     ++nres;
                     act = false;
-                    if (spp > 1) {
-                        double* q = a.part + 3 * ((size_t)idx * (size_t)spp + (size_t)smp);
-                        q[0] = 0.0; q[1] = 0.0; q[2] = 0.0;
-                    } else {
-                        if (rgb) { rgb[3 * idx] = 0.0; rgb[3 * idx + 1] = 0.0; rgb[3 * idx + 2] = 0.0; }
-                        if (rgb8) { rgb8[3 * idx] = 0; rgb8[3 * idx + 1] = 0; rgb8[3 * idx + 2] = 0; }
-                    }
+                    wf_store(a.part, rgb, rgb8, spp, idx, smp, v3(0, 0, 0));
                 } else {
                     d = normalize(d0);
                 }
             }
             if (GI_WF_PSL) {
-                pl[0] = L.x; pl[256] = L.y; pl[512] = L.z;
-                pl[768] = T.x; pl[1024] = T.y; pl[1280] = T.z;
+                v.pl[0] = L.x; v.pl[256] = L.y; v.pl[512] = L.z;
+                v.pl[768] = T.x; v.pl[1024] = T.y; v.pl[1280] = T.z;
             }
         }
-        // ---- closest hit
-        double tbest = INFINITY;
-        int best;
-        if constexpr (LDS) best = wf_trace<false, true, true, SH, TRI, false>(LW, LH, o, d, INFINITY, act, nst, tbest, nnode, nprim);
-        else if constexpr (CN) best = wf_trace<false, false, false, SH, TRI, true>(sc.xcnodes, sc.xhot, o, d, INFINITY, act, nst, tbest, nnode, nprim);
-        else best = wf_trace<false, false, false, SH, TRI, true>(sc.xwnodes, sc.xhot, o, d, INFINITY, act, nst, tbest, nnode, nprim);
-        if (act) ++nrays;
-        const bool hit = act && best >= 0;
-        // ---- the hit point and its shadow ray toward the point light
-        V3 P = o, Ld = v3(0, 0, 1);
-        double ldist = 0.0;
-        if (hit) {
-            P = o + tbest * d;
-            const V3 lv = light - P;
-            ldist = gsqrt(dot(lv, lv));
-            Ld = normalize(lv);
-        }
-        bool occl = false;
-        if (!no_shadow) {
-            double tdummy;
-            int sb;
-            if constexpr (LDS) sb = wf_trace<true, true, true, SH, TRI, false>(LW, LH, P, Ld, ldist, hit, nst, tdummy, nnode, nprim);
-            else if constexpr (CN) sb = wf_trace<true, false, false, SH, TRI, true>(sc.xcnodes, sc.xhot, P, Ld, ldist, hit, nst, tdummy, nnode, nprim);
-            else sb = wf_trace<true, false, false, SH, TRI, true>(sc.xwnodes, sc.xhot, P, Ld, ldist, hit, nst, tdummy, nnode, nprim);
-            occl = sb >= 0;
-        }
-        // ---- shading (the oracle's operations: local = ambient, + diffuse + specular when lit)
-        bool cont = false;
-        if (hit) {
-            ++nrays;   // the shadow ray
-            if (GI_WF_PSL) {
-                L = v3(pl[0], pl[256], pl[512]);
-                T = v3(pl[768], pl[1024], pl[1280]);
-            }
-            const XPrim& p = XP[best];   // the facing normal (after the shadow ray: fewer live values)
-            V3 N = (TRI || p.kind == 0) ? ld3(p.n) : normalize(P - ld3(p.a));
-            if (!(dot(d, N) < 0)) N = -N;
-            const REnt& e = EN[p.ent];
-            int32_t tu, tv;
-            x_texcoord<TRI>(sc, e, P, tu, tv);
-            const V3 tc = texel(ld3(e.color), tu, tv);
-            const V3 la = tc * e.shader[0];
-            V3 loc = la;
-            if (!occl) {
-                const V3 ldf = (smax(0.0, dot(N, Ld)) * (tc * 0.5)) * e.shader[1];
-                const V3 bis = normalize(normalize(-d) + Ld);
-                const double spw = mx_pow(smax(0.0, dot(N, bis)), e.spec_pow);
-                const V3 ls = v3(spw, spw, spw) * e.shader[2];
-                loc = (la + ldf) + ls;
-            }
-            L = L + vmul(T, v3(smin(loc.x, 1.0), smin(loc.y, 1.0), smin(loc.z, 1.0)));
-            if (b != depth - 1) {
-                // mirror bounce with probability e.refl (uniform dim 4): T unchanged, d reflected
-                // about the facing normal; otherwise T *= texel / 2 and a cosine-weighted direction
-                if (e.refl > 0.0 && mx_u01k(key, smp, b, 4) < e.refl) {
-                    d = normalize(d - N * (2.0 * dot(d, N)));
-                    cont = true;
-                } else {
-                    T = vmul(T, tc * 0.5);
-                    if (!(T.x == 0.0 && T.y == 0.0 && T.z == 0.0)) {
-                        double sx, sy, r2;   // concentric disk + Malley
-                        mx_disk(mx_u01k(key, smp, b, 2), mx_u01k(key, smp, b, 3), sx, sy, r2);
-                        const double sz = gsqrt(1.0 - r2);
-                        const double sg = N.z >= 0.0 ? 1.0 : -1.0;   // Duff et al. 2017 basis
-                        const double aa = -1.0 / (sg + N.z);
-                        const double bb = N.x * N.y * aa;
-                        const V3 bt1 = v3(1.0 + sg * N.x * N.x * aa, sg * bb, -sg * N.x);
-                        const V3 bt2 = v3(bb, sg + N.y * N.y * aa, -N.y);
-                        d = normalize((bt1 * sx + bt2 * sy) + N * sz);
-                        cont = true;
-                    }
-                }
-                o = P;
-            }
-        }
+        const bool cont = x_segment<LDS, SH, TRI, CN>(sc, v, light, depth, no_shadow, act, b, key, smp, o, d, L, T, nnode,
+                                                      nprim, nrays);
         // ---- live paths to the next bounce's queue: one atomic per wave, entries in lane order
         const unsigned long long mc = __ballot(cont);
         if (mc) {
@@ -375,18 +432,148 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
                 r[9 * oc] = T.x; r[10 * oc] = T.y; r[11 * oc] = T.z;
             }
         }
-        // ---- paths that end here: the sample's radiance (k_x_reduce sums a pixel's samples in
-        // order) or, with one sample, the pixel itself
-        if (act && !cont) {
-            if (GI_WF_PSL && !hit) L = v3(pl[0], pl[256], pl[512]);
-            if (spp > 1) {
-                double* q = a.part + 3 * ((size_t)idx * (size_t)spp + (size_t)smp);
-                q[0] = L.x; q[1] = L.y; q[2] = L.z;
+        if (act && !cont) wf_store(a.part, rgb, rgb8, spp, idx, smp, L);
+    }
+    if (STATS) {
+        wave_add_stats(stats, nrays, nnode, nprim, npx);
+        uint64_t r = nres;
+        for (int off = 32; off > 0; off >>= 1) r += __shfl_xor(r, off);
+        if (lane == 0 && r) atomicAdd(stats + GI_STAT_X_RESOLVED, (unsigned long long)r);
+    }
+}
+
+// The segment-synchronous form (SEG): one persistent kernel in which every loop iteration is one
+// whole path segment (x_segment) for every lane of the wave -- the wavefront form's uniform per-lane
+// sequence, with the path state kept in registers / the lane's LDS slot instead of HBM queues, and
+// no launch per bounce.  A lane whose path ends takes the next (pixel, sample) unit at the top of
+// the next iteration (units handed out from the wave's run of <= GI_SEG_TAKE x 64, one atomic per run);
+// primary rays that miss the scene's root box are resolved there, up to GI_SEG_BURST per lane.
+#ifndef GI_SEG_BURST
+#define GI_SEG_BURST 16
+#endif
+#ifndef GI_SEG_TAKE
+#define GI_SEG_TAKE 16   // k_seg: most batches of 64 units per run (one atomic per run)
+#endif
+template <bool STATS, bool LDS, bool W4, bool SH, bool TRI, bool CN>
+__global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_WAVES) void k_seg(
+    DevScene sc, CamDev cam, V3 light, TileMap m, int spp, int depth, uint64_t seed, double* rgb, uint8_t* rgb8,
+    unsigned long long* stats, WFArgs a, int xflags) {
+    extern __shared__ int4 lds_dyn[];
+    const WFView v = wf_stage<LDS>(sc, lds_dyn);
+    const bool no_shadow = (xflags & 4) != 0;
+    const int lane = threadIdx.x & 63;
+    const unsigned long long total = (unsigned long long)*a.n_list * (unsigned long long)spp;
+    // run length: up to GI_SEG_TAKE batches of 64 units per atomic, fewer when the launch has fewer
+    // than about 8 runs per resident wave (small launches: every wave gets work)
+    const unsigned long long n_waves = (unsigned long long)gridDim.x * (blockDim.x >> 6);
+    const unsigned long long run = 64ull * (unsigned long long)max(1ll, min((long long)GI_SEG_TAKE, (long long)(total / (64ull * 32ull * n_waves))));
+    uint32_t nnode = 0, nprim = 0, nrays = 0, nres = 0, npx = 0;
+    unsigned long long cur = 0, cur_end = 0;   // the wave's unhanded units [cur, cur_end) (uniform)
+    // the work-list entries of the current run's pixels, lane k holding pixel p0 + k (fetched when the
+    // run is taken, so a refill reads its pixel with a lane shuffle instead of a dependent load);
+    // np > 64 (runs of more than 64 pixels): read from the list instead
+    unsigned lst = 0;
+    unsigned long long p0 = 0, np = 0;
+    bool exhausted = false;                    // the frame's units are all handed out (uniform)
+    bool live = false;                         // this lane carries a path
+    unsigned li = 0, smp = 0;
+    int b = 0;
+    long long idx = -1;
+    uint64_t key = 0;
+    V3 o = cam.pos, d = v3(1, 0, 0), L = v3(0, 0, 0), T = v3(1, 1, 1);
+    for (;;) {
+        // ---- lanes without a path take units (primary rays; background samples resolved here)
+        for (int burst = 0; burst < GI_SEG_BURST; ++burst) {
+            const unsigned long long m_need = __ballot(!live);
+            if (m_need == 0 || (exhausted && cur >= cur_end)) break;
+            const unsigned rank = (unsigned)__popcll(m_need & ((1ull << lane) - 1));
+            const unsigned n_need = (unsigned)__popcll(m_need);
+            unsigned long long u = ~0ull;
+            const unsigned long long avail = cur_end - cur;
+            bool from_new = false;
+            unsigned lst_new = 0;
+            unsigned long long p0_new = 0, np_new = 0;
+            if (n_need > avail && !exhausted) {   // a new run of units for the lanes beyond it
+                unsigned long long nb = 0;
+                if (lane == 0) nb = atomicAdd(reinterpret_cast<unsigned long long*>(a.take), run);
+                nb = __shfl(nb, 0);
+                if (nb >= total) {
+                    exhausted = true;
+                    if (!live && rank < avail) u = cur + rank;
+                    cur = cur_end;
+                } else {
+                    const unsigned long long ne = min(total, nb + run);
+                    p0_new = nb / (unsigned long long)spp;
+                    np_new = (ne - 1) / (unsigned long long)spp - p0_new + 1;
+                    if (np_new <= 64 && (unsigned long long)lane < np_new) lst_new = a.list[p0_new + lane];
+                    if (!live) {
+                        if (rank < avail) u = cur + rank;
+                        else if (nb + (rank - avail) < ne) { u = nb + (rank - avail); from_new = true; }
+                    }
+                    cur = min(ne, nb + (n_need - avail));
+                    cur_end = ne;
+                    if (ne == total) exhausted = true;
+                }
             } else {
-                const double c0 = smin((0.0 + L.x) / 1.0, 1.0), c1 = smin((0.0 + L.y) / 1.0, 1.0),
-                             c2 = smin((0.0 + L.z) / 1.0, 1.0);
-                if (rgb) { rgb[3 * idx] = c0; rgb[3 * idx + 1] = c1; rgb[3 * idx + 2] = c2; }
-                if (rgb8) quantize(c0, c1, c2, rgb8 + 3 * idx);
+                if (!live && rank < avail) u = cur + rank;
+                cur += min((unsigned long long)n_need, avail);
+            }
+            unsigned li_u = 0, smp_u = 0;
+            if (u != ~0ull) {
+                if (u < (1ull << 32)) {
+                    li_u = (unsigned)u / (unsigned)spp;
+                    smp_u = (unsigned)u - li_u * (unsigned)spp;
+                } else {
+                    li_u = (unsigned)(u / (unsigned long long)spp);
+                    smp_u = (unsigned)(u - (unsigned long long)li_u * (unsigned long long)spp);
+                }
+            }
+            // the new unit's pixel from the prefetched entries (shuffles run in every lane)
+            const unsigned ps_cur = __shfl(lst, (int)((li_u - p0) & 63));
+            const unsigned ps_new = __shfl(lst_new, (int)((li_u - p0_new) & 63));
+            const bool pre = from_new ? np_new <= 64 : np <= 64;   // (np: the run the unit came from)
+            if (np_new) {   // a run was taken: it is the current one from now on
+                lst = lst_new;
+                p0 = p0_new;
+                np = np_new;
+            }
+            if (!live && u != ~0ull) {
+                li = li_u;
+                smp = smp_u;
+                const unsigned ps = pre ? (from_new ? ps_new : ps_cur) : a.list[li];
+                const V3 d0 = wf_primary(cam, m, ps, spp, seed, li, smp, idx, key);
+                if (smp == 0) ++npx;
+                if (wf_primary_misses(sc, cam, d0)) {
+                    ++nrays;
+                    ++nres;
+                    wf_store(a.part, rgb, rgb8, spp, idx, smp, v3(0, 0, 0));
+                } else {
+                    live = true;
+                    b = 0;
+                    o = cam.pos;
+                    d = normalize(d0);
+                    L = v3(0, 0, 0);
+                    T = v3(1, 1, 1);
+                    if (GI_WF_PSL) {
+                        v.pl[0] = 0.0; v.pl[256] = 0.0; v.pl[512] = 0.0;
+                        v.pl[768] = 1.0; v.pl[1024] = 1.0; v.pl[1280] = 1.0;
+                    }
+                }
+            }
+        }
+        if (__ballot(live) == 0) {
+            if (exhausted && cur >= cur_end) break;
+            continue;
+        }
+        // ---- one segment of every live path
+        const bool cont = x_segment<LDS, SH, TRI, CN>(sc, v, light, depth, no_shadow, live, b, key, smp, o, d, L, T, nnode,
+                                                      nprim, nrays);
+        if (live) {
+            if (cont) {
+                ++b;
+            } else {
+                wf_store(a.part, rgb, rgb8, spp, idx, smp, L);
+                live = false;
             }
         }
     }
@@ -403,41 +590,72 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
 // dynamic LDS of the bounce kernel beyond the scene / level stack: the per-lane path slots
 size_t wf_slot_bytes() { return kWfSlotBytes; }
 
-// resident workgroups per CU of the bounce kernel launch_wf picks for this scene
-hipError_t wf_occupancy(const DevScene& sc, int kv, size_t lds_bytes, int* per_cu) {
+// The kernel variant for a scene: f(LDS, W4, SH, TRI, CN) with each a std::integral_constant<bool>
+// (kv: 2 * LDS-resident + light-shading, XLaunchCfg::kv)
+template <typename F>
+void wf_dispatch(const DevScene& sc, int kv, F&& f) {
+    using B = std::true_type;
+    using N = std::false_type;
     const bool lds = kv >= 2, w4 = kv == 3, sh = sc.x_max_depth <= 7, tr = sc.x_tri_only != 0;
     const bool cn = !lds && sc.xcnodes != nullptr;
-    const void* f = lds ? (w4 ? (sh ? reinterpret_cast<const void*>(k_wf_bounce<false, true, true, true, true, false>)
-                                    : reinterpret_cast<const void*>(k_wf_bounce<false, true, true, false, true, false>))
-                              : (sh ? reinterpret_cast<const void*>(k_wf_bounce<false, true, false, true, false, false>)
-                                    : reinterpret_cast<const void*>(k_wf_bounce<false, true, false, false, false, false>)))
-                  : cn ? (tr ? reinterpret_cast<const void*>(k_wf_bounce<false, false, false, false, true, true>)
-                             : reinterpret_cast<const void*>(k_wf_bounce<false, false, false, false, false, true>))
-                       : (tr ? reinterpret_cast<const void*>(k_wf_bounce<false, false, false, false, true, false>)
-                             : reinterpret_cast<const void*>(k_wf_bounce<false, false, false, false, false, false>));
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, f, 256, lds_bytes);
+    if (lds) {
+        if (w4) { if (sh) f(B{}, B{}, B{}, B{}, N{}); else f(B{}, B{}, N{}, B{}, N{}); }
+        else { if (sh) f(B{}, N{}, B{}, N{}, N{}); else f(B{}, N{}, N{}, N{}, N{}); }
+    } else if (cn) {
+        if (tr) f(N{}, N{}, N{}, B{}, B{}); else f(N{}, N{}, N{}, N{}, B{});
+    } else {
+        if (tr) f(N{}, N{}, N{}, B{}, N{}); else f(N{}, N{}, N{}, N{}, N{});
+    }
 }
 
-// The wavefront Mode X pass (after k_x_classify, before k_x_reduce): reads the work list's length
-// back to the host (one stream synchronisation), then per chunk of units `depth` bounce launches.
-// kv: 2 * LDS-resident + light-shading (XLaunchCfg::kv).  Counters: 2 per bounce (take, n_out),
-// zeroed per chunk.
-hipError_t launch_wf(const DevScene& sc, int kv, size_t lds_bytes, int resident, const CamDev& cam, V3 light, int w,
-                     int h, int y0, const gi_opts& o, double* rgb, uint8_t* rgb8, const XScratch& xs,
+// resident workgroups per CU of the kernel a form (1: k_wf_bounce, 2: k_seg) runs for this scene
+hipError_t wf_occupancy(const DevScene& sc, int kv, size_t lds_bytes, int form, int* per_cu) {
+    hipError_t e = hipSuccess;
+    wf_dispatch(sc, kv, [&](auto L, auto W, auto SHt, auto T, auto C) {
+        constexpr bool l = decltype(L)::value, w = decltype(W)::value, sh = decltype(SHt)::value,
+                       t = decltype(T)::value, c = decltype(C)::value;
+        const void* f = form == 2 ? reinterpret_cast<const void*>(k_seg<false, l, w, sh, t, c>)
+                                  : reinterpret_cast<const void*>(k_wf_bounce<false, l, w, sh, t, c>);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, f, 256, lds_bytes);
+    });
+    return e;
+}
+
+// The Mode X pass after k_x_classify and before k_x_reduce in the wavefront forms.
+//  form 1 (wavefront): reads the work list's length back to the host (one stream synchronisation),
+//    then per chunk of units (the queue capacity) `depth` bounce launches; counters: 2 per bounce
+//    (take, n_out), zeroed per chunk.
+//  form 2 (segment-synchronous): one persistent launch; counter: a 64-bit unit count at xs.wcnt.
+hipError_t launch_wf(const DevScene& sc, int kv, size_t lds_bytes, int resident, int form, const CamDev& cam, V3 light,
+                     int w, int h, int y0, const gi_opts& o, double* rgb, uint8_t* rgb8, const XScratch& xs,
                      const unsigned* n_list_dev, unsigned long long* stats, int xflags, hipStream_t stream,
                      hipEvent_t ev_begin, hipEvent_t ev_end) {
     const TileMap m = make_map(w, h, o.shard_count, o.shard_index, y0);
-    hipError_t e = hipMemcpyAsync(xs.h_nlist, n_list_dev, sizeof(unsigned), hipMemcpyDeviceToHost, stream);
+    const int depth = o.depth;
+    const dim3 grid((unsigned)std::max(1, resident)), block(256);
+    hipError_t e = hipSuccess;
+    if (form == 2) {
+        e = hipMemsetAsync(xs.wcnt, 0, 2 * sizeof(unsigned), stream);
+        if (e != hipSuccess) return e;
+        WFArgs a{};
+        a.list = xs.list;
+        a.n_list = n_list_dev;
+        a.part = xs.part;
+        a.take = xs.wcnt;
+        if (ev_begin) (void)hipEventRecord(ev_begin, stream);
+        wf_dispatch(sc, kv, [&](auto L, auto W, auto SHt, auto T, auto C) {
+            constexpr bool l = decltype(L)::value, wv = decltype(W)::value, sh = decltype(SHt)::value,
+                           t = decltype(T)::value, c = decltype(C)::value;
+            if (stats) hipLaunchKernelGGL((k_seg<true, l, wv, sh, t, c>), grid, block, lds_bytes, stream, sc, cam, light, m, o.spp, depth, o.seed, rgb, rgb8, stats, a, xflags);
+            else hipLaunchKernelGGL((k_seg<false, l, wv, sh, t, c>), grid, block, lds_bytes, stream, sc, cam, light, m, o.spp, depth, o.seed, rgb, rgb8, stats, a, xflags);
+        });
+        if (ev_end) (void)hipEventRecord(ev_end, stream);
+        return hipGetLastError();
+    }
+    e = hipMemcpyAsync(xs.h_nlist, n_list_dev, sizeof(unsigned), hipMemcpyDeviceToHost, stream);
     if (e == hipSuccess) e = hipStreamSynchronize(stream);
     if (e != hipSuccess) return e;
     const unsigned long long units = (unsigned long long)*xs.h_nlist * (unsigned long long)o.spp;
-    const int depth = o.depth;
-    const bool lds = kv >= 2, w4 = kv == 3;
-    const bool sh = sc.x_max_depth <= 7;
-    const bool cn = !lds && sc.xcnodes != nullptr;
-    const bool tr = sc.x_tri_only != 0;
-    const size_t lbytes = lds_bytes;
-    const dim3 grid((unsigned)std::max(1, resident)), block(256);
     if (ev_begin) (void)hipEventRecord(ev_begin, stream);
     for (unsigned long long u0 = 0; u0 < units; u0 += (unsigned long long)xs.wcap) {
         e = hipMemsetAsync(xs.wcnt, 0, 2 * (size_t)depth * sizeof(unsigned), stream);
@@ -458,23 +676,12 @@ hipError_t launch_wf(const DevScene& sc, int kv, size_t lds_bytes, int resident,
             qin.id = reinterpret_cast<uint2*>(xs.wid[(b + 1) & 1]);
             qout.r = xs.wq[b & 1];
             qout.id = reinterpret_cast<uint2*>(xs.wid[b & 1]);
-#define GI_WF_LAUNCH(S, L, W, SHV, T, C) hipLaunchKernelGGL((k_wf_bounce<S, L, W, SHV, T, C>), grid, block, lbytes, stream, sc, cam, \
-                                                  light, m, o.spp, depth, o.seed, b, rgb, rgb8, stats, a, qin, qout, xflags)
-#define GI_WF_S(S)                                                                                   \
-    do {                                                                                             \
-        if (lds) {                                                                                   \
-            if (w4) { if (sh) GI_WF_LAUNCH(S, true, true, true, true, false); else GI_WF_LAUNCH(S, true, true, false, true, false); } \
-            else { if (sh) GI_WF_LAUNCH(S, true, false, true, false, false); else GI_WF_LAUNCH(S, true, false, false, false, false); } \
-        } else if (cn) {                                                                             \
-            if (tr) GI_WF_LAUNCH(S, false, false, false, true, true); else GI_WF_LAUNCH(S, false, false, false, false, true); \
-        } else {                                                                                     \
-            if (tr) GI_WF_LAUNCH(S, false, false, false, true, false); else GI_WF_LAUNCH(S, false, false, false, false, false); \
-        }                                                                                            \
-    } while (0)
-            if (stats) GI_WF_S(true);
-            else GI_WF_S(false);
-#undef GI_WF_S
-#undef GI_WF_LAUNCH
+            wf_dispatch(sc, kv, [&](auto L, auto W, auto SHt, auto T, auto C) {
+                constexpr bool l = decltype(L)::value, wv = decltype(W)::value, sh = decltype(SHt)::value,
+                               t = decltype(T)::value, c = decltype(C)::value;
+                if (stats) hipLaunchKernelGGL((k_wf_bounce<true, l, wv, sh, t, c>), grid, block, lds_bytes, stream, sc, cam, light, m, o.spp, depth, o.seed, b, rgb, rgb8, stats, a, qin, qout, xflags);
+                else hipLaunchKernelGGL((k_wf_bounce<false, l, wv, sh, t, c>), grid, block, lds_bytes, stream, sc, cam, light, m, o.spp, depth, o.seed, b, rgb, rgb8, stats, a, qin, qout, xflags);
+            });
         }
     }
     if (ev_end) (void)hipEventRecord(ev_end, stream);

@@ -113,8 +113,10 @@ typedef enum gi_mode {
                                     be checked against the reference's frames (tests) */
 #define GI_FLAG_X_WF 16u         /* Mode X: the wavefront form (one launch per bounce over a compacted queue of
                                     live paths, gi_wf.hip) whatever the scene; same frame bit for bit */
-#define GI_FLAG_X_MEGA 32u       /* Mode X: the persistent path-state kernel (k_mode_x) whatever the scene.
-                                    Neither flag: chosen per launch (GI_X_WF=0/1 overrides) */
+#define GI_FLAG_X_MEGA 32u       /* Mode X: the persistent path-state kernel (k_mode_x) whatever the scene */
+#define GI_FLAG_X_SEG 64u        /* Mode X: the segment-synchronous persistent form (k_seg: every loop
+                                    iteration one whole path segment per lane).  None of the three form
+                                    flags: chosen per launch (GI_X_WF=0/1/2 overrides) */
 
 typedef struct gi_opts {
     int32_t mode;          /* gi_mode */
@@ -241,7 +243,8 @@ int gi_trace_ray(gi_scene* scene, const double origin[3], const double dir[3], c
  * GI_ERR_ARG if there was none. */
 int gi_scene_kernel_ms(gi_scene* scene, float* avg_ms, int64_t* n);
 /* Mode X form a render of `scene` with `opts` would run (bench labels, tests): 0 = the persistent
- * path-state kernel k_mode_x, 1 = the wavefront form (k_wf_bounce once per bounce); Mode R: 0. */
+ * path-state kernel k_mode_x, 1 = the wavefront form (k_wf_bounce once per bounce), 2 = the
+ * segment-synchronous form (k_seg); Mode R: 0. */
 int gi_scene_x_form(gi_scene* scene, const gi_opts* opts, int32_t* form);
 
 /* ---- host-side reference octree (no device needed) --------------------------------------------

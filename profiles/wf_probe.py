@@ -21,7 +21,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--seed", type=int, default=2019)
-    ap.add_argument("--forms", default="mega,wf")
+    ap.add_argument("--forms", default="mega,wf,seg")
     ap.add_argument("workloads", nargs="+")
     args = ap.parse_args()
     import torch
@@ -30,7 +30,7 @@ def main():
     bench = import_module("bench")
     torch.cuda.set_device(0)
     stream = torch.cuda.current_stream()
-    forms = {"mega": gi.FLAG_X_MEGA, "wf": gi.FLAG_X_WF}
+    forms = {"mega": gi.FLAG_X_MEGA, "wf": gi.FLAG_X_WF, "seg": gi.FLAG_X_SEG}
     for wl in args.workloads:
         scene_name, w, h, mode, spp, depth, desc = bench.WORKLOADS[wl]
         sc = bench.make_scene(scene_name)
@@ -65,11 +65,13 @@ def main():
                          "resolved": st[gi.STAT_X_RESOLVED], "nodes": st[gi.STAT_NODES], "prims": st[gi.STAT_PRIMS],
                          "pixels": st[gi.STAT_PIXELS]}
         names = list(frames)
-        if len(names) == 2:
-            a, b = frames[names[0]], frames[names[1]]
-            out["identical"] = bool(torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]))
-            if not out["identical"]:
-                out["n_diff"] = int((a[0] != b[0]).sum().item())
+        for nm in names[1:]:   # every form's frame against the first form's, bit for bit
+            a, b = frames[names[0]], frames[nm]
+            same = bool(torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]))
+            out.setdefault("identical", True)
+            out["identical"] = out["identical"] and same
+            if not same:
+                out["n_diff_" + nm] = int((a[0] != b[0]).sum().item())
         print(json.dumps(out), flush=True)
 
 
