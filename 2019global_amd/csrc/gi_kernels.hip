@@ -288,7 +288,7 @@ __device__ __forceinline__ uint32_t children_mask_line(const XWNode* nd, F3 of, 
 // group's 8 lanes read 8 consecutive floats of each plane array -- and a ballot gathers the mask, the
 // same in every lane.  Per child the arithmetic is children_mask_line's, so the mask is identical.
 #ifndef GI_R_COOP
-#define GI_R_COOP 0   // cooperative line-BVH node tests in k_mode_r_split / k_mode_r_heavy
+#define GI_R_COOP 1   // cooperative line-BVH node tests in k_mode_r_split / k_mode_r_heavy
 #endif
 template <int NSUB>
 __device__ __forceinline__ uint32_t children_mask_line_coop(const XWNode* nd, F3 of, F3 ivf, float tau, int sub) {
@@ -527,6 +527,7 @@ struct RHeavy {
     unsigned* n;
     unsigned budget;   // 0: no budget (the first pass finishes every pixel)
 };
+
 
 #ifndef GI_R_BUDGET
 // candidates a pixel's 8 lanes may meet in k_mode_r_split before the pixel is handed to
@@ -1784,7 +1785,12 @@ size_t wf_slot_bytes();
 #endif
 // Mode X form of a launch: 0 the persistent path-state kernel (k_mode_x), 1 the wavefront form
 // (k_wf_bounce once per bounce over compacted queues), 2 the segment-synchronous form (k_seg).
-// GI_FLAG_X_MEGA / _WF / _SEG force one (tests, A/B), then GI_X_WF=0/1/2; by default ....
+// GI_FLAG_X_MEGA / _WF / _SEG force one (tests, A/B), then GI_X_WF=0/1/2.  By default (DESIGN.md §5,
+// round-4 A/B): scenes staged in LDS run k_seg (C3 5.8 -> 5.2 ms, C2 0.29 -> 0.15-0.17 ms, X-zoo
+// 5.7 -> 4.9 ms; short traversals, so a wave's lanes finish a segment together); HBM-resident scenes
+// keep k_mode_x, whose lanes refill independently (C4: k_seg 3.2 against 1.7 ms -- one long
+// traversal would hold its whole wave).  The wavefront form loses everywhere (queue traffic and its
+// atomics: C3 12.5-20 ms); it stays selectable.
 int x_form_choice(const DevScene& sc, const XLaunchCfg& xc, const gi_opts& o) {
     if (o.mode != GI_MODE_X || (o.flags & GI_FLAG_X_MEGA)) return 0;
     if (o.flags & GI_FLAG_X_SEG) return 2;
@@ -1792,8 +1798,7 @@ int x_form_choice(const DevScene& sc, const XLaunchCfg& xc, const gi_opts& o) {
     const XEnv& env = x_env();
     if (env.wf >= 0) return env.wf == 1 ? (o.depth <= GI_WF_MAX_DEPTH ? 1 : 0) : env.wf == 2 ? 2 : 0;
     (void)sc;
-    (void)xc;
-    return 0;   // until measured on the GPU (round 4)
+    return xc.kv >= 2 ? 2 : 0;
 }
 long long x_wf_chunk() { return x_env().wf_chunk; }
 

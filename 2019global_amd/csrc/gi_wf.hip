@@ -446,13 +446,13 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
 // whole path segment (x_segment) for every lane of the wave -- the wavefront form's uniform per-lane
 // sequence, with the path state kept in registers / the lane's LDS slot instead of HBM queues, and
 // no launch per bounce.  A lane whose path ends takes the next (pixel, sample) unit at the top of
-// the next iteration (units handed out from the wave's run of <= GI_SEG_TAKE x 64, one atomic per run);
+// the next iteration (units handed out from the wave's run, one atomic per run);
 // primary rays that miss the scene's root box are resolved there, up to GI_SEG_BURST per lane.
 #ifndef GI_SEG_BURST
 #define GI_SEG_BURST 16
 #endif
 #ifndef GI_SEG_TAKE
-#define GI_SEG_TAKE 16   // k_seg: most batches of 64 units per run (one atomic per run)
+#define GI_SEG_TAKE 4   // k_seg: most batches of 64 units per run (one atomic per run)
 #endif
 template <bool STATS, bool LDS, bool W4, bool SH, bool TRI, bool CN>
 __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_WAVES) void k_seg(
@@ -463,10 +463,13 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
     const bool no_shadow = (xflags & 4) != 0;
     const int lane = threadIdx.x & 63;
     const unsigned long long total = (unsigned long long)*a.n_list * (unsigned long long)spp;
-    // run length: up to GI_SEG_TAKE batches of 64 units per atomic, fewer when the launch has fewer
-    // than about 8 runs per resident wave (small launches: every wave gets work)
+    // run length: up to GI_SEG_TAKE batches of 64 units per atomic (background-heavy frames burn units
+    // fast: longer runs, fewer atomics on the one counter), fewer when the launch has less than about
+    // 8 runs per resident wave (small launches: every wave gets work).  Guided self-scheduling --
+    // run sizes from a relaxed read of the counter -- measured 1.2-2.6x slower (the read waits behind
+    // the atomics on that L2 line).
     const unsigned long long n_waves = (unsigned long long)gridDim.x * (blockDim.x >> 6);
-    const unsigned long long run = 64ull * (unsigned long long)max(1ll, min((long long)GI_SEG_TAKE, (long long)(total / (64ull * 32ull * n_waves))));
+    const unsigned long long run = 64ull * (unsigned long long)max(1ll, min((long long)GI_SEG_TAKE, (long long)(total / (64ull * 8ull * n_waves))));
     uint32_t nnode = 0, nprim = 0, nrays = 0, nres = 0, npx = 0;
     unsigned long long cur = 0, cur_end = 0;   // the wave's unhanded units [cur, cur_end) (uniform)
     // the work-list entries of the current run's pixels, lane k holding pixel p0 + k (fetched when the

@@ -977,3 +977,37 @@ def test_mode_x_other_acceleration_structures_bit_exact(torch_cuda, accel):
         rgb, _ = devs[name].render(cam_of(sc), sc.light, w, h, mode=gi.MODE_X, spp=spp, depth=depth, seed=7)
         o = U.oracle_render(sc.to_scn(), w, h, mode=1, spp=spp, depth=depth, seed=7)
         assert U.bits_equal(rgb.reshape(-1, 3), o["rgb"]).all(), (name, accel)
+
+
+@pytest.mark.parametrize("name,w,h,spp,depth,shard", [
+    ("cornell", 96, 80, 16, 8, (1, 0)), ("cornell_mirror", 64, 48, 4, 8, (3, 1)), ("zoo", 64, 48, 2, 4, (1, 0)),
+    ("main", 80, 60, 3, 5, (1, 0)), ("soup1000", 64, 64, 2, 8, (2, 1)), ("sphere", 40, 40, 5, 3, (1, 0))])
+def test_mode_x_forms_bit_identical(torch_cuda, name, w, h, spp, depth, shard):
+    """The three Mode X forms -- the persistent path-state kernel (k_mode_x), the wavefront form (one
+    k_wf_bounce launch per bounce over ballot-compacted path queues) and the segment-synchronous form
+    (k_seg) -- run the same per-path operations, so every frame is bit-identical across them and to
+    the oracle (LDS- and HBM-resident scenes, mirrors, spheres, a packed shard; gi_scene_x_form names
+    the form each flag selects)."""
+    sc = _scene(name)
+    d = dev_scene(name)
+    kw = dict(mode=gi.MODE_X, spp=spp, depth=depth, seed=7)
+    frames = {}
+    for form, fl in (("k_mode_x", gi.FLAG_X_MEGA), ("k_wf_bounce", gi.FLAG_X_WF), ("k_seg", gi.FLAG_X_SEG)):
+        assert d.x_form(gi.MODE_X, spp, depth, flags=fl) == form
+        if shard[0] == 1:
+            frames[form] = d.render(cam_of(sc), sc.light, w, h, flags=fl, **kw)
+        else:
+            torch = torch_cuda
+            n = gi.shard_tiles(w, h, shard[0]) * 64 * 3
+            buf = torch.zeros(n, dtype=torch.float64, device="cuda")
+            buf8 = torch.zeros(n, dtype=torch.uint8, device="cuda")
+            d.render_device(cam_of(sc), sc.light, w, h, buf.data_ptr(), buf8.data_ptr(), shard_count=shard[0],
+                            shard_index=shard[1], flags=fl, **kw)
+            torch.cuda.synchronize()
+            frames[form] = (buf.cpu().numpy(), buf8.cpu().numpy())
+    for form in ("k_wf_bounce", "k_seg"):
+        assert U.bits_equal(frames[form][0], frames["k_mode_x"][0]).all(), form
+        assert (frames[form][1] == frames["k_mode_x"][1]).all(), form
+    if shard[0] == 1:
+        o = U.oracle_render(sc.to_scn(), w, h, mode=1, spp=spp, depth=depth, seed=7)
+        assert U.bits_equal(frames["k_seg"][0].reshape(-1, 3), o["rgb"]).all()
