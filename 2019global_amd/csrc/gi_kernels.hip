@@ -1786,10 +1786,10 @@ size_t wf_slot_bytes();
 // Mode X form of a launch: 0 the persistent path-state kernel (k_mode_x), 1 the wavefront form
 // (k_wf_bounce once per bounce over compacted queues), 2 the segment-synchronous form (k_seg).
 // GI_FLAG_X_MEGA / _WF / _SEG force one (tests, A/B), then GI_X_WF=0/1/2.  By default (DESIGN.md §5,
-// round-4 A/B): scenes staged in LDS run k_seg (C3 5.8 -> 5.2 ms, C2 0.29 -> 0.15-0.17 ms, X-zoo
-// 5.7 -> 4.9 ms; short traversals, so a wave's lanes finish a segment together); HBM-resident scenes
-// keep k_mode_x, whose lanes refill independently (C4: k_seg 3.2 against 1.7 ms -- one long
-// traversal would hold its whole wave).  The wavefront form loses everywhere (queue traffic and its
+// round-4 A/B): scenes staged in LDS run k_seg (C3 5.8 -> 5.2 ms, C2 0.29 -> 0.15-0.17 ms; short
+// traversals, so a wave's lanes finish a segment together); large HBM-resident scenes keep
+// k_mode_x, whose lanes refill independently (C4: k_seg 3.2 against 1.7 ms -- one long traversal
+// would hold its whole wave).  The wavefront form loses everywhere (queue traffic and its
 // atomics: C3 12.5-20 ms); it stays selectable.
 int x_form_choice(const DevScene& sc, const XLaunchCfg& xc, const gi_opts& o) {
     if (o.mode != GI_MODE_X || (o.flags & GI_FLAG_X_MEGA)) return 0;
@@ -1797,8 +1797,9 @@ int x_form_choice(const DevScene& sc, const XLaunchCfg& xc, const gi_opts& o) {
     if (o.flags & GI_FLAG_X_WF) return o.depth <= GI_WF_MAX_DEPTH ? 1 : 0;
     const XEnv& env = x_env();
     if (env.wf >= 0) return env.wf == 1 ? (o.depth <= GI_WF_MAX_DEPTH ? 1 : 0) : env.wf == 2 ? 2 : 0;
-    (void)sc;
-    return xc.kv >= 2 ? 2 : 0;
+    // small HBM-resident trees (<= 1 MB of wide nodes: L2-resident, short traversals -- X-zoo 5.7 ->
+    // 4.8-5.0 ms, the 1k soup even) run k_seg too
+    return (xc.kv >= 2 || (size_t)sc.n_xwnodes * sizeof(XWNode) <= ((size_t)1 << 20)) ? 2 : 0;
 }
 long long x_wf_chunk() { return x_env().wf_chunk; }
 

@@ -36,6 +36,9 @@ namespace {
 #ifndef GI_WF_MIN_WAVES
 #define GI_WF_MIN_WAVES 3       // other scenes
 #endif
+#ifndef GI_WF_PAIR
+#define GI_WF_PAIR 1   // LDS-resident scenes: leaf records tested two at a time (two interleaved fp64 chains)
+#endif
 #ifndef GI_WF_TAKE
 #define GI_WF_TAKE 16   // most 64-entry batches a wave takes per atomic on the queue's counter
 #endif
@@ -57,12 +60,12 @@ struct WFQ {
 // (ANY: a shadow ray; true on the first primitive found) of the ray o + t d through the 8-wide BVH.
 // Stackless: 8-bit "children left" mask per level (SH: one 64-bit word, trees of <= 8 levels);
 // climbing by parent pointers (LDS-resident scenes) or the per-lane level stack nst (HBM).
-// PAIR: leaf records two at a time (two interleaved fp64 chains; LDS records); otherwise global
-// records fetched one ahead of their test.  RECULL (closest, LDS): a popped child is re-tested
-// against the current best t (its box is a ds_read away).
+// PAIR: leaf records two at a time (two interleaved fp64 chains; LDS records); otherwise records
+// fetched one ahead of their test.  LDS-resident scenes (!NST), closest hit: a popped child is
+// re-tested against the current best t (its box is a ds_read away).
 template <bool ANY, bool PAIR, bool AXIS, bool SH, bool TRI, bool NST, typename NodeP, typename HotP>
 __device__ __forceinline__ int wf_trace(NodeP W, HotP H, V3 o, V3 d, double tmax, bool act, int* nst, double& t_out,
-                                        uint32_t& nnode, uint32_t& nprim) {
+                                        uint32_t& nnode, uint32_t& nprim, uint32_t& nsteps) {
     const F3 of = f3((float)o.x, (float)o.y, (float)o.z);
     const F3 ivf = inv_dir(d);
     const int dmask = (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
@@ -78,6 +81,7 @@ __device__ __forceinline__ int wf_trace(NodeP W, HotP H, V3 o, V3 d, double tmax
         raying = rm != 0;
     }
     while (raying) {
+        ++nsteps;
         const auto* nd = W + node;
         const uint32_t msk = lvl_get<SH>(mlo, mhi, level);
         const int kc = __builtin_ctz(msk);   // next child in front-to-back order
@@ -85,7 +89,7 @@ __device__ __forceinline__ int wf_trace(NodeP W, HotP H, V3 o, V3 d, double tmax
         const int c = kc ^ dmask;
         const int ch = nd->child[c];
         bool keep = true;
-        if (!ANY && PAIR && best >= 0) keep = child_hit(nd, c, of, ivf, tbf);
+        if (!ANY && !NST && best >= 0) keep = child_hit(nd, c, of, ivf, tbf);   // (LDS scenes)
         if (keep) {
             if (ch < 0) {   // leaf: the fp64 primitive tests decide
                 const int cnt = nd->cnt[c];
@@ -252,20 +256,44 @@ __device__ __forceinline__ void wf_store(double* part, double* rgb, uint8_t* rgb
 // cosine-weighted direction).  The oracle's operations (sample_mode_x).  In: o, d and (GI_WF_PSL: in
 // the lane's path slot, else in L, T) the path's L and T.  Out: true when the path continues (o, d
 // set to its next ray; L, T in registers and, GI_WF_PSL, in the slot); false when it ends (L final).
-template <bool LDS, bool SH, bool TRI, bool CN>
-__device__ __forceinline__ bool x_segment(const DevScene& sc, const WFView& v, V3 light, int depth, bool no_shadow, bool act,
+// STATS: the wave's traversal-loop iterations (closest, shadow) and the lanes' own steps, summed into
+// ws (lane 0) -- the divergence profile of a segment
+struct WFSegStats {
+    uint64_t it_c = 0, ln_c = 0, it_s = 0, ln_s = 0, segs = 0, live = 0, iters = 0;
+    uint64_t cyc_c = 0, cyc_s = 0, cyc_sh = 0, cyc_ref = 0, cyc_all = 0;   // wave clock cycles per phase
+};
+__device__ __forceinline__ void wf_wave_steps(uint32_t n, uint64_t& it, uint64_t& ln) {
+    uint32_t mx = n, sm = n;
+    for (int off = 32; off > 0; off >>= 1) {
+        mx = max(mx, (uint32_t)__shfl_xor(mx, off));
+        sm += __shfl_xor(sm, off);
+    }
+    if ((threadIdx.x & 63) == 0) { it += mx; ln += sm; }
+}
+template <bool STATS, bool LDS, bool SH, bool TRI, bool CN>
+__device__ __forceinline__ bool x_segment(const DevScene& sc, const WFView& v, const V3& light, int depth, bool no_shadow, bool act,
                                           int b, uint64_t key, unsigned smp, V3& o, V3& d, V3& L, V3& T,
-                                          uint32_t& nnode, uint32_t& nprim, uint32_t& nrays) {
+                                          uint32_t& nnode, uint32_t& nprim, uint32_t& nrays, WFSegStats& ws) {
+    uint32_t st_steps = 0;
+    uint64_t c0 = STATS ? clock64() : 0;
+    V3 P = o, Ld = v3(0, 0, 1);
+    bool occl = false;
     // ---- closest hit
     double tbest = INFINITY;
     int best;
-    if constexpr (LDS) best = wf_trace<false, true, true, SH, TRI, false>(v.LW, v.LH, o, d, INFINITY, act, v.nst, tbest, nnode, nprim);
-    else if constexpr (CN) best = wf_trace<false, false, false, SH, TRI, true>(sc.xcnodes, sc.xhot, o, d, INFINITY, act, v.nst, tbest, nnode, nprim);
-    else best = wf_trace<false, false, false, SH, TRI, true>(sc.xwnodes, sc.xhot, o, d, INFINITY, act, v.nst, tbest, nnode, nprim);
+    if constexpr (LDS) best = wf_trace<false, GI_WF_PAIR != 0, true, SH, TRI, false>(v.LW, v.LH, o, d, INFINITY, act, v.nst, tbest, nnode, nprim, st_steps);
+    else if constexpr (CN) best = wf_trace<false, false, false, SH, TRI, true>(sc.xcnodes, sc.xhot, o, d, INFINITY, act, v.nst, tbest, nnode, nprim, st_steps);
+    else best = wf_trace<false, false, false, SH, TRI, true>(sc.xwnodes, sc.xhot, o, d, INFINITY, act, v.nst, tbest, nnode, nprim, st_steps);
     if (act) ++nrays;
+    if (STATS) {
+        wf_wave_steps(st_steps, ws.it_c, ws.ln_c);
+        st_steps = 0;
+        const uint64_t c1 = clock64();
+        ws.cyc_c += c1 - c0;
+        c0 = c1;
+    }
     const bool hit = act && best >= 0;
     // ---- the hit point and its shadow ray toward the point light
-    V3 P = o, Ld = v3(0, 0, 1);
     double ldist = 0.0;
     if (hit) {
         P = o + tbest * d;
@@ -273,14 +301,19 @@ __device__ __forceinline__ bool x_segment(const DevScene& sc, const WFView& v, V
         ldist = gsqrt(dot(lv, lv));
         Ld = normalize(lv);
     }
-    bool occl = false;
     if (!no_shadow) {
         double tdummy;
         int sb;
-        if constexpr (LDS) sb = wf_trace<true, true, true, SH, TRI, false>(v.LW, v.LH, P, Ld, ldist, hit, v.nst, tdummy, nnode, nprim);
-        else if constexpr (CN) sb = wf_trace<true, false, false, SH, TRI, true>(sc.xcnodes, sc.xhot, P, Ld, ldist, hit, v.nst, tdummy, nnode, nprim);
-        else sb = wf_trace<true, false, false, SH, TRI, true>(sc.xwnodes, sc.xhot, P, Ld, ldist, hit, v.nst, tdummy, nnode, nprim);
+        if constexpr (LDS) sb = wf_trace<true, GI_WF_PAIR != 0, true, SH, TRI, false>(v.LW, v.LH, P, Ld, ldist, hit, v.nst, tdummy, nnode, nprim, st_steps);
+        else if constexpr (CN) sb = wf_trace<true, false, false, SH, TRI, true>(sc.xcnodes, sc.xhot, P, Ld, ldist, hit, v.nst, tdummy, nnode, nprim, st_steps);
+        else sb = wf_trace<true, false, false, SH, TRI, true>(sc.xwnodes, sc.xhot, P, Ld, ldist, hit, v.nst, tdummy, nnode, nprim, st_steps);
         occl = sb >= 0;
+        if (STATS) wf_wave_steps(st_steps, ws.it_s, ws.ln_s);
+    }
+    if (STATS) {
+        const uint64_t c1 = clock64();
+        ws.cyc_s += c1 - c0;
+        c0 = c1;
     }
     if (GI_WF_PSL && act) {
         L = v3(v.pl[0], v.pl[256], v.pl[512]);
@@ -333,6 +366,7 @@ __device__ __forceinline__ bool x_segment(const DevScene& sc, const WFView& v, V
             v.pl[768] = T.x; v.pl[1024] = T.y; v.pl[1280] = T.z;
         }
     }
+    if (STATS) ws.cyc_sh += clock64() - c0;
     return cont;
 }
 
@@ -413,8 +447,9 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
                 v.pl[768] = T.x; v.pl[1024] = T.y; v.pl[1280] = T.z;
             }
         }
-        const bool cont = x_segment<LDS, SH, TRI, CN>(sc, v, light, depth, no_shadow, act, b, key, smp, o, d, L, T, nnode,
-                                                      nprim, nrays);
+        WFSegStats ws;
+        const bool cont = x_segment<false, LDS, SH, TRI, CN>(sc, v, light, depth, no_shadow, act, b, key, smp, o, d, L, T,
+                                                             nnode, nprim, nrays, ws);
         // ---- live paths to the next bounce's queue: one atomic per wave, entries in lane order
         const unsigned long long mc = __ballot(cont);
         if (mc) {
@@ -451,6 +486,9 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
 #ifndef GI_SEG_BURST
 #define GI_SEG_BURST 16
 #endif
+#ifndef GI_SEG_PREFETCH
+#define GI_SEG_PREFETCH 0   // k_seg: a run's work-list entries fetched when it is taken (lane shuffles)
+#endif
 #ifndef GI_SEG_TAKE
 #define GI_SEG_TAKE 4   // k_seg: most batches of 64 units per run (one atomic per run)
 #endif
@@ -484,7 +522,11 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
     long long idx = -1;
     uint64_t key = 0;
     V3 o = cam.pos, d = v3(1, 0, 0), L = v3(0, 0, 0), T = v3(1, 1, 1);
+    WFSegStats ws;
+    const uint64_t t_begin = STATS ? clock64() : 0;
     for (;;) {
+        if (STATS && lane == 0) ++ws.iters;
+        const uint64_t t_ref = STATS ? clock64() : 0;
         // ---- lanes without a path take units (primary rays; background samples resolved here)
         for (int burst = 0; burst < GI_SEG_BURST; ++burst) {
             const unsigned long long m_need = __ballot(!live);
@@ -508,7 +550,7 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
                     const unsigned long long ne = min(total, nb + run);
                     p0_new = nb / (unsigned long long)spp;
                     np_new = (ne - 1) / (unsigned long long)spp - p0_new + 1;
-                    if (np_new <= 64 && (unsigned long long)lane < np_new) lst_new = a.list[p0_new + lane];
+                    if (GI_SEG_PREFETCH && np_new <= 64 && (unsigned long long)lane < np_new) lst_new = a.list[p0_new + lane];
                     if (!live) {
                         if (rank < avail) u = cur + rank;
                         else if (nb + (rank - avail) < ne) { u = nb + (rank - avail); from_new = true; }
@@ -534,7 +576,7 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
             // the new unit's pixel from the prefetched entries (shuffles run in every lane)
             const unsigned ps_cur = __shfl(lst, (int)((li_u - p0) & 63));
             const unsigned ps_new = __shfl(lst_new, (int)((li_u - p0_new) & 63));
-            const bool pre = from_new ? np_new <= 64 : np <= 64;   // (np: the run the unit came from)
+            const bool pre = GI_SEG_PREFETCH && (from_new ? np_new <= 64 : np <= 64);   // (np: the unit's run)
             if (np_new) {   // a run was taken: it is the current one from now on
                 lst = lst_new;
                 p0 = p0_new;
@@ -564,13 +606,18 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
                 }
             }
         }
+        if (STATS) ws.cyc_ref += clock64() - t_ref;
         if (__ballot(live) == 0) {
             if (exhausted && cur >= cur_end) break;
             continue;
         }
         // ---- one segment of every live path
-        const bool cont = x_segment<LDS, SH, TRI, CN>(sc, v, light, depth, no_shadow, live, b, key, smp, o, d, L, T, nnode,
-                                                      nprim, nrays);
+        if (STATS) {
+            const unsigned long long ml = __ballot(live);
+            if (lane == 0) { ++ws.segs; ws.live += __popcll(ml); }
+        }
+        const bool cont = x_segment<STATS, LDS, SH, TRI, CN>(sc, v, light, depth, no_shadow, live, b, key, smp, o, d, L, T,
+                                                             nnode, nprim, nrays, ws);
         if (live) {
             if (cont) {
                 ++b;
@@ -579,6 +626,20 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
                 live = false;
             }
         }
+    }
+    if (STATS && lane == 0) {   // the segment divergence profile (bench "schedule")
+        atomicAdd(stats + GI_STAT_X_ITERS, (unsigned long long)ws.iters);
+        atomicAdd(stats + GI_STAT_X_HANDLE, (unsigned long long)ws.segs);
+        atomicAdd(stats + GI_STAT_X_HLANES, (unsigned long long)ws.live);
+        atomicAdd(stats + GI_STAT_X_IT_LEAF, (unsigned long long)ws.it_c);
+        atomicAdd(stats + GI_STAT_X_LN_LEAF, (unsigned long long)ws.ln_c);
+        atomicAdd(stats + GI_STAT_X_IT_NODE, (unsigned long long)ws.it_s);
+        atomicAdd(stats + GI_STAT_X_LN_NODE, (unsigned long long)ws.ln_s);
+        atomicAdd(stats + GI_STAT_X_CYC_TRAV, (unsigned long long)(ws.cyc_c + ws.cyc_s));
+        atomicAdd(stats + GI_STAT_X_IT_RS, (unsigned long long)ws.cyc_c);   // (k_seg: closest-trace cycles)
+        atomicAdd(stats + GI_STAT_X_CYC_HIT, (unsigned long long)ws.cyc_sh);
+        atomicAdd(stats + GI_STAT_X_CYC_NEXT, (unsigned long long)ws.cyc_ref);
+        atomicAdd(stats + GI_STAT_X_CYC_ALL, (unsigned long long)(clock64() - t_begin));
     }
     if (STATS) {
         wave_add_stats(stats, nrays, nnode, nprim, npx);

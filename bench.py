@@ -419,6 +419,7 @@ def main():
         # reached the acceleration structure; the primary samples the pixel-frustum classify and the
         # root-box pretest resolve without traversal (each adds exactly +0) are counted apart
         rays_traced = rays_frame - resolved
+        form = dev.x_form(mode, spp, depth) if mode == 1 else None   # the Mode X form this launch ran
         value = rays_traced * args.steps / elapsed / 1e6
         # algorithmic bytes per launch of the dominant kernel (this rank's launch; N=1: the frame)
         node_bytes = dev.info()["x_node_bytes"] if mode == 1 else NODE_BYTES[0]
@@ -453,7 +454,7 @@ def main():
             # primary (w*h*spp) and total (primary + bounce + shadow) rays per second
             "mray_s_primary": round(w * h * spp * args.steps / elapsed / 1e6, 3),
             "mray_s_all_rays": round(rays_frame * args.steps / elapsed / 1e6, 3),
-            "roofline": {"bound": "hbm", "kernel": (dev.x_form(mode, spp, depth) if mode == 1 else "k_mode_r"),
+            "roofline": {"bound": "hbm", "kernel": (form if mode == 1 else "k_mode_r"),
                          "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "alg_bytes_per_launch": int(alg),
@@ -479,7 +480,22 @@ def main():
             out["frame_check"] = frame_check
             if args.dist_backend != "nccl":
                 out["rehearsal"] = f"{args.dist_backend}: {world} ranks on {ndev} device(s)"
-        if mode == 1 and st[gi.STAT_X_ITERS]:   # k_mode_x schedule (STATS launch; wave = 64 lanes)
+        if form == "k_seg" and st[gi.STAT_X_ITERS]:   # k_seg divergence profile (STATS launch)
+            segs = max(1, st[gi.STAT_X_HANDLE])
+            out["schedule"] = {
+                "form": form, "wave_iterations": st[gi.STAT_X_ITERS], "wave_segments": st[gi.STAT_X_HANDLE],
+                # lanes carrying a path when a segment starts / 64
+                "segment_lane_fill": round(st[gi.STAT_X_HLANES] / (64.0 * segs), 4),
+                # traversal loops: the wave's iterations (its slowest lane's steps) and the lanes' own steps
+                "closest_trav": {"wave_iterations": st[gi.STAT_X_IT_LEAF],
+                                 "lane_fill": round(st[gi.STAT_X_LN_LEAF] / (64.0 * max(1, st[gi.STAT_X_IT_LEAF])), 4)},
+                "shadow_trav": {"wave_iterations": st[gi.STAT_X_IT_NODE],
+                                "lane_fill": round(st[gi.STAT_X_LN_NODE] / (64.0 * max(1, st[gi.STAT_X_IT_NODE])), 4)},
+                # wave clock shares: closest trace, shadow trace, shading + next direction, unit refill
+                "cycle_share": {k: round(v / max(1, st[gi.STAT_X_CYC_ALL]), 4) for k, v in (
+                    ("closest", st[gi.STAT_X_IT_RS]), ("shadow", st[gi.STAT_X_CYC_TRAV] - st[gi.STAT_X_IT_RS]),
+                    ("shade", st[gi.STAT_X_CYC_HIT]), ("refill", st[gi.STAT_X_CYC_NEXT]))}}
+        elif mode == 1 and st[gi.STAT_X_ITERS]:   # k_mode_x schedule (STATS launch; wave = 64 lanes)
             it, hd = st[gi.STAT_X_ITERS], max(1, st[gi.STAT_X_HANDLE])
             out["schedule"] = {"wave_iterations": it, "lane_trav_steps": st[gi.STAT_X_TRAV],
                                "trav_lane_fill": round(st[gi.STAT_X_TRAV] / (64.0 * it), 4),
