@@ -74,21 +74,28 @@ FP64_VALU_PEAK_TFS = 78.6     # MI355X FP64 vector peak (AMD spec; half the guid
 N_SIMDS = 1024                 # 256 CUs x 4 SIMDs
 
 
-def pmc_summary(workload: str):
+def pmc_summary(workload: str, kernel: str = ""):
     """The latest committed rocprofv3 PMC summary of this workload's dominant kernel
-    (profiles/rNN_<workload>_pmc.json, written by profiles/summarize.py), or None."""
+    (profiles/rNN[tag]_<workload>_pmc.json, written by profiles/summarize.py) whose kernel is the one
+    this run launches (k_seg / k_mode_x / k_wf_bounce / k_mode_r...: A/B profiles of the other forms
+    sit beside it), or None.  Latest = highest round number."""
     best = None
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json"))):
+    for p in glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")):
         try:
             d = json.load(open(p))
         except Exception:
             continue
-        if d.get("workload") == workload and d.get("counters_per_launch"):
-            best = (os.path.relpath(p, ROOT), d)
-    return best
+        if d.get("workload") != workload or not d.get("counters_per_launch"):
+            continue
+        if kernel and kernel + "<" not in d.get("kernel", "") and kernel + "_split<" not in d.get("kernel", ""):
+            continue
+        rnd = os.path.basename(p)[1:3]
+        if best is None or rnd > best[0]:
+            best = (rnd, os.path.relpath(p, ROOT), d)
+    return best[1:] if best else None
 
 
-def counter_ceilings(workload: str, kern_ms: float):
+def counter_ceilings(workload: str, kern_ms: float, kernel: str = ""):
     """What the dominant kernel meets, from the committed PMC summary of the same workload:
       * HBM: counter bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction) / live kernel
         time / 8 TB/s -- the bytes that actually reach HBM;
@@ -101,7 +108,7 @@ def counter_ceilings(workload: str, kern_ms: float):
     `binding` names the tightest: valu_pipe when the VALU pipe is busy >= 75% of the cycles (2 cycles
     per wave64 instruction, 4 for f64), else hbm when counter traffic is >= 60% of peak, else latency
     (the waves wait on dependent instructions and memory)."""
-    got = pmc_summary(workload)
+    got = pmc_summary(workload, kernel)
     if got is None:
         return None
     src, d = got
@@ -426,7 +433,7 @@ def main():
         alg = (st[gi.STAT_NODES] * node_bytes + st[gi.STAT_PRIMS] * PRIM_BYTES[mode] +
                st[gi.STAT_PIXELS] * 27) / world
         achieved = alg / (kern_ms * 1e-3) / 1e9
-        ceil = counter_ceilings(args.workload, kern_ms) if world == 1 else None
+        ceil = counter_ceilings(args.workload, kern_ms, form if mode == 1 else "k_mode_r") if world == 1 else None
         traffic = ceil.get("hbm_counter_bytes") if ceil else None
         out = {
             "metric": "Mray/s + ms/frame at 1920x1080, depth 8; %HBM roofline",
