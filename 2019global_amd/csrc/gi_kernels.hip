@@ -1626,11 +1626,17 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
 // Mode X pass 1: one thread per pixel slot (tile order; a wave = one 8x8 tile).  A pixel none of
 // whose jittered primary rays can meet the scene's root box (conservative fp64 frustum test) is 0:
 // every sample adds exactly +0, as in the oracle, which traces them.  Padding slots of a packed
-// tile are zeroed.  The other pixels are appended to the work list (one atomic per wave).
+// tile are zeroed.  The other pixels are appended to the work list: one atomic per 1024-thread
+// workgroup (the waves' counts combined in LDS) -- one per wave on the single n_list counter
+// serialised at L2: 49 us per frame for C2 and C3 alike.
+// zero2: two words zeroed by the first thread (the wavefront forms' unit counters), saving a memset
+// launch per frame.
+constexpr int kClassifyBlock = 1024;
 template <bool STATS>
-__global__ __launch_bounds__(256) void k_x_classify(DevScene sc, CamDev cam, TileMap m, int spp, double* rgb,
+__global__ __launch_bounds__(kClassifyBlock) void k_x_classify(DevScene sc, CamDev cam, TileMap m, int spp, double* rgb,
                                                      uint8_t* rgb8, unsigned* list, unsigned* n_list,
-                                                     unsigned long long* stats) {
+                                                     unsigned long long* stats, unsigned* zero2) {
+    if (zero2 && blockIdx.x == 0 && threadIdx.x < 2) zero2[threadIdx.x] = 0u;
     const long long s = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     const long long lt = s >> 6;
     const int lane = threadIdx.x & 63;
@@ -1651,13 +1657,21 @@ __global__ __launch_bounds__(256) void k_x_classify(DevScene sc, CamDev cam, Til
         if (rgb8) { rgb8[3 * idx] = 0; rgb8[3 * idx + 1] = 0; rgb8[3 * idx + 2] = 0; }
     }
     const unsigned long long ms = __ballot(scene);
-    if (ms) {
-        const int leader = __ffsll((long long)ms) - 1;
-        unsigned base = 0;
-        if (lane == leader) base = atomicAdd(n_list, (unsigned)__popcll(ms));
-        base = __shfl(base, leader);
-        if (scene) list[base + (unsigned)__popcll(ms & ((1ull << lane) - 1))] = (unsigned)s;
+    __shared__ unsigned s_cnt[kClassifyBlock / 64 + 1];
+    const int wv = threadIdx.x >> 6;
+    if (lane == 0) s_cnt[wv] = (unsigned)__popcll(ms);
+    __syncthreads();
+    if (threadIdx.x == 0) {   // exclusive offsets of the waves, then one atomic for the workgroup
+        unsigned acc = 0;
+        for (int k = 0; k < kClassifyBlock / 64; ++k) {
+            const unsigned c = s_cnt[k];
+            s_cnt[k] = acc;
+            acc += c;
+        }
+        s_cnt[kClassifyBlock / 64] = acc ? atomicAdd(n_list, acc) : 0u;
     }
+    __syncthreads();
+    if (scene) list[s_cnt[kClassifyBlock / 64] + s_cnt[wv] + (unsigned)__popcll(ms & ((1ull << lane) - 1))] = (unsigned)s;
     if (STATS && (s & ~63ll) < m.n_local * 64) {
         wave_add_stats(stats, bg ? (uint64_t)spp : 0, 0, 0, bg ? 1 : 0);
         uint64_t r = bg ? (uint64_t)spp : 0;   // samples resolved here, without traversal
@@ -1915,8 +1929,11 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
         wk.part = xs.part;
         wk.blocks = sc.work;
         const dim3 sgrid((unsigned)((n_slots + 255) / 256));
-        if (stats) hipLaunchKernelGGL(k_x_classify<true>, sgrid, dim3(256), 0, stream, sc, cam, m, o.spp, rgb, rgb8, xs.list, sc.work + 1, st);
-        else hipLaunchKernelGGL(k_x_classify<false>, sgrid, dim3(256), 0, stream, sc, cam, m, o.spp, rgb, rgb8, xs.list, sc.work + 1, st);
+        const dim3 cgrid((unsigned)((n_slots + kClassifyBlock - 1) / kClassifyBlock));
+        const int form = x_form_choice(sc, xc, o);
+        unsigned* zero2 = form == 2 ? xs.wcnt : nullptr;   // k_seg's unit counter, zeroed by the classify pass
+        if (stats) hipLaunchKernelGGL(k_x_classify<true>, cgrid, dim3(kClassifyBlock), 0, stream, sc, cam, m, o.spp, rgb, rgb8, xs.list, sc.work + 1, st, zero2);
+        else hipLaunchKernelGGL(k_x_classify<false>, cgrid, dim3(kClassifyBlock), 0, stream, sc, cam, m, o.spp, rgb, rgb8, xs.list, sc.work + 1, st, zero2);
         // shading-handler threshold (eighths of the live lanes that must wait): the builder's
         // estimate for the scene (DevScene::x_handle8) unless GI_X_HANDLE8 overrides it
         const int h8 = env.h8 > 0 ? env.h8 : sc.x_handle8;
@@ -1926,7 +1943,7 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
         const int xf = (env.xf >= 0 ? env.xf : sc.x_flags) | (env.run_log2 << 8) |
                        ((o.flags & GI_FLAG_X_NO_SHADOW) ? 4 : 0) | (env.help ? 8 : 0) |
                        ((env.spread > 0 || (env.spread < 0 && help)) ? 16 : 0) | (env.leaf8 << 12);
-        if (const int form = x_form_choice(sc, xc, o)) {   // gi_wf.hip's forms, timed as one pass
+        if (form) {   // gi_wf.hip's forms, timed as one pass
             if (!xs.wcnt || (form == 1 && (!xs.wq[0] || !xs.wq[1] || !xs.h_nlist || xs.wcap <= 0))) return hipErrorInvalidValue;
             e = launch_wf(sc, xc.kv, xc.wf_lds_bytes, form == 2 ? xc.seg_resident : xc.wf_resident, form, cam, light, w, h, y0,
                           o, rgb, rgb8, xs, sc.work + 1, stats ? st : nullptr, xf, stream, ev_begin, ev_end);

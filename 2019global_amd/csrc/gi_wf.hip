@@ -698,9 +698,7 @@ hipError_t launch_wf(const DevScene& sc, int kv, size_t lds_bytes, int resident,
     const int depth = o.depth;
     const dim3 grid((unsigned)std::max(1, resident)), block(256);
     hipError_t e = hipSuccess;
-    if (form == 2) {
-        e = hipMemsetAsync(xs.wcnt, 0, 2 * sizeof(unsigned), stream);
-        if (e != hipSuccess) return e;
+    if (form == 2) {   // (the unit counter xs.wcnt[0..1] was zeroed by k_x_classify)
         WFArgs a{};
         a.list = xs.list;
         a.n_list = n_list_dev;
