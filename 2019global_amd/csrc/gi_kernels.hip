@@ -521,6 +521,148 @@ __device__ __forceinline__ void r_split_write(const DevScene& sc, V3 d, V3 light
     }
 }
 
+// Mode R with the line-BVH WALK itself split over a pixel's 8 lanes (GI_R_PAR; k_mode_r_par).  The
+// heavy-pixel experiments show a slow pixel's time is its serial walk -- a chain of dependent node
+// loads that k_mode_r_split's 8 lanes all repeat -- so here the group walks the top two levels
+// together (cooperative node tests) and lists the hit nodes / leaves below them in rank order (at
+// most 64 items); item i is then walked by lane i mod 8 alone (its own stackless walk of that
+// subtree).  Pruning: every lane reads the group's best rank from LDS before each slot (ranks only
+// rise, and only ranks of hitting reachable candidates are posted), so a slot whose bound is <= it
+// holds no better candidate; each candidate is considered by the one lane walking its leaf.  The
+// answer -- the highest reachable hitting rank, shaded by the lane holding it -- is the same.
+#ifndef GI_R_PAR
+#define GI_R_PAR 0   // Mode R large scenes: k_mode_r_par instead of k_mode_r_split
+#endif
+#ifndef GI_R_MIN_WAVES
+#define GI_R_MIN_WAVES 1   // minimum waves per SIMD asked of the register allocator (Mode R kernels)
+#endif
+template <bool TRI>
+__device__ __forceinline__ void r_par_consider(const DevScene& sc, int e, V3 o, V3 d, unsigned long long* gb, long long& best,
+                                               long long& mine, RResult& r, uint32_t& nnode, uint32_t& nprim, RMemo memo) {
+    const long long before = best;
+    r_consider<TRI>(sc, e, o, d, best, r, nnode, nprim, memo);
+    if (best != before) {
+        mine = best;
+        atomicMax(gb, (unsigned long long)(best + 1));
+    }
+}
+// one lane's walk of the subtree below wide node `root` (its hit children m0), leaves considered
+template <bool TRI>
+__device__ __forceinline__ void r_par_walk(const DevScene& sc, int root, uint32_t m0, F3 of, F3 ivf, float tau, V3 o, V3 d,
+                                           unsigned long long* gb, long long& best, long long& mine, RResult& r,
+                                           uint32_t& nnode, uint32_t& nprim, RMemo memo) {
+    const XWNode* W = sc.rc_nodes;
+    uint64_t mlo = 0, mhi = 0;
+    int node = root, level = 0;
+    lvl_set(mlo, mhi, 0, m0);
+    bool going = m0 != 0;
+    while (going) {
+        const uint32_t msk = lvl_get(mlo, mhi, level);
+        const int c = __builtin_ctz(msk);
+        lvl_set(mlo, mhi, level, msk & (msk - 1));
+        const XWNode* nd = W + node;
+        const int ch = nd->child[c];
+        best = max(best, (long long)*(volatile unsigned long long*)gb - 1);   // the group's best so far
+        if (sc.rc_maxkey[node * 8 + c] <= best) {
+            lvl_set(mlo, mhi, level, 0);
+        } else if (ch < 0) {
+            const int cnt = nd->cnt[c];
+            for (int j = 0; j < cnt; ++j) r_par_consider<TRI>(sc, sc.rc_ent[~ch + j], o, d, gb, best, mine, r, nnode, nprim, memo);
+        } else {
+            const uint32_t cm = children_mask_line(W + ch, of, ivf, tau);
+            if (cm) {
+                node = ch;
+                ++level;
+                lvl_set(mlo, mhi, level, cm);
+            }
+        }
+        uint32_t rest = lvl_get(mlo, mhi, level);
+        while (rest == 0 && level > 0) {
+            --level;
+            node = level == 0 ? root : W[node].parent;
+            rest = lvl_get(mlo, mhi, level);
+        }
+        going = rest != 0;
+    }
+}
+template <bool STATS, bool TRI>
+__global__ __launch_bounds__(256, GI_R_MIN_WAVES) void k_mode_r_par(DevScene sc, CamDev cam, V3 light, TileMap m, double* rgb,
+                                                     uint8_t* rgb8, unsigned long long* stats, float tau) {
+    constexpr int NSUB = 8;
+    const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long ps = g / NSUB;
+    const int sub = (int)(g % NSUB), grp = threadIdx.x / NSUB;
+    __shared__ int s_memo[GI_R_MEMO > 0 ? (256 / NSUB) * GI_R_MEMO : 1];
+    __shared__ unsigned long long s_best[256 / NSUB];   // the group's best rank + 1 (0: none)
+    __shared__ int s_item[256 / NSUB][64];              // (node << 3) | slot, in rank order
+    RMemo memo{GI_R_MEMO > 0 ? s_memo + grp * GI_R_MEMO : nullptr};
+    if (GI_R_MEMO > 0)
+        for (int k = sub; k < GI_R_MEMO; k += NSUB) memo.e[k] = -1;
+    if (sub == 0) s_best[grp] = 0ull;
+    __builtin_amdgcn_wave_barrier();
+    const long long lt = ps >> 6;
+    long long idx = -1;
+    int x = 0, y = 0;
+    const bool ok = lt < m.n_local && slot_pixel(m, lt, (int)(ps & 63), idx, x, y);
+    y += m.y0;
+    uint32_t nnode = 0, nprim = 0;
+    if (ok) {
+        const V3 o = cam.pos;
+        const V3 d = normalize(primary_dir(cam, (double)x, (double)y));
+        unsigned long long* gb = s_best + grp;
+        RResult r;
+        r.ent = -1;
+        long long best = -1, mine = -1;
+        for (int i = sub; i < sc.n_r_always; i += NSUB) r_par_consider<TRI>(sc, sc.r_always[i], o, d, gb, best, mine, r, nnode, nprim, memo);
+        const XWNode* W = sc.rc_nodes;
+        const F3 of = f3((float)o.x, (float)o.y, (float)o.z);
+        const F3 ivf = inv_dir(d);
+        // the items: the root's hit slots, an interior one replaced by its own hit slots (coop tests)
+        int n = 0;
+        uint32_t rm = children_mask_line_coop<NSUB>(W, of, ivf, tau, sub);
+        while (rm) {
+            const int c = __builtin_ctz(rm);
+            rm &= rm - 1;
+            const int ch = W[0].child[c];
+            if (ch < 0) {
+                if (sub == 0) s_item[grp][n] = c;
+                ++n;
+            } else {
+                uint32_t cm = children_mask_line_coop<NSUB>(W + ch, of, ivf, tau, sub);
+                while (cm) {
+                    const int c2 = __builtin_ctz(cm);
+                    cm &= cm - 1;
+                    if (sub == 0) s_item[grp][n] = (ch << 3) | c2;
+                    ++n;
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        for (int i = sub; i < n; i += NSUB) {   // lane sub walks items sub, sub + 8, ...
+            const int it = s_item[grp][i];
+            const int node = it >> 3, c = it & 7;
+            best = max(best, (long long)*(volatile unsigned long long*)gb - 1);
+            if (sc.rc_maxkey[node * 8 + c] <= best) continue;
+            const int ch = W[node].child[c];
+            if (ch < 0) {
+                const int cnt = W[node].cnt[c];
+                for (int j = 0; j < cnt; ++j) r_par_consider<TRI>(sc, sc.rc_ent[~ch + j], o, d, gb, best, mine, r, nnode, nprim, memo);
+            } else {
+                const uint32_t cm = children_mask_line(W + ch, of, ivf, tau);
+                r_par_walk<TRI>(sc, ch, cm, of, ivf, tau, o, d, gb, best, mine, r, nnode, nprim, memo);
+            }
+        }
+        r_split_write<NSUB, TRI>(sc, d, light, r, mine, sub, idx, rgb, rgb8);
+    } else if (sub == 0 && idx >= 0 && m.shard_count > 1) {   // padding slot of a packed tile
+        if (rgb) { rgb[3 * idx] = 0; rgb[3 * idx + 1] = 0; rgb[3 * idx + 2] = 0; }
+        if (rgb8) { rgb8[3 * idx] = 0; rgb8[3 * idx + 1] = 0; rgb8[3 * idx + 2] = 0; }
+    }
+    if (STATS) {
+        const bool px = ok && sub == 0;
+        wave_add_stats(stats, px ? 1 : 0, nnode, nprim, px ? 1 : 0);
+    }
+}
+
 // pixels whose first pass gave up (k_mode_r_split with a budget): (pixel slot, rank found) pairs
 struct RHeavy {
     long long* list;   // 2 per entry
@@ -1761,6 +1903,7 @@ long long shard_tiles(int w, int h, int shard_count) { return make_map(w, h, sha
 struct XEnv {
     int lds = 1, h8 = 0, xf = -1, run_log2 = 0, help = 1, spread = -1, r_split = -1, leaf8 = 0, wf = -1;
     int r_budget = GI_R_BUDGET;       // Mode R heavy-pixel hand-off (GI_R_BUDGET, candidates; 0: off)
+    int r_par = GI_R_PAR;             // Mode R walk split over the pixel's lanes (GI_R_PAR=0/1)
     long long wf_chunk = 8ll << 20;   // wavefront Mode X: units (pixel samples) per chunk = queue capacity
 };
 const XEnv& x_env() {
@@ -1774,6 +1917,7 @@ const XEnv& x_env() {
         if (const char* v = std::getenv("GI_X_SPREAD")) env.spread = std::atoi(v);
         if (const char* v = std::getenv("GI_R_SPLIT")) env.r_split = std::atoi(v);
         if (const char* v = std::getenv("GI_R_BUDGET")) env.r_budget = std::max(0, std::atoi(v));
+        if (const char* v = std::getenv("GI_R_PAR")) env.r_par = std::atoi(v) != 0;
         if (const char* v = std::getenv("GI_X_LEAF8")) env.leaf8 = std::max(0, std::min(8, std::atoi(v)));
         if (const char* v = std::getenv("GI_X_WF")) env.wf = std::atoi(v);
         if (const char* v = std::getenv("GI_X_WF_CHUNK")) env.wf_chunk = std::max(1ll << 16, std::min(1ll << 30, std::atoll(v)));
@@ -1879,7 +2023,16 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
             if (e0 != hipSuccess) return e0;
         }
         mark(ev_begin);
-        if (split) {
+        if (split && env.r_par) {   // the walk split over the pixel's 8 lanes (k_mode_r_par)
+            const dim3 sgrid((unsigned)((m.n_local * (kTile * kTile) * 8 + 255) / 256));
+            if (sc.r_tri_only && GI_R_TRI) {
+                if (stats) hipLaunchKernelGGL((k_mode_r_par<true, true>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
+                else hipLaunchKernelGGL((k_mode_r_par<false, true>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
+            } else {
+                if (stats) hipLaunchKernelGGL((k_mode_r_par<true, false>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
+                else hipLaunchKernelGGL((k_mode_r_par<false, false>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
+            }
+        } else if (split) {
             const dim3 sgrid((unsigned)((m.n_local * (kTile * kTile) * GI_R_NSUB + 255) / 256));
             const dim3 hgrid(1024);   // k_mode_r_heavy: 4096 waves loop over the heavy pixels
             if (sc.r_tri_only && GI_R_TRI) {
