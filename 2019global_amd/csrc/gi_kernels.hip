@@ -531,7 +531,11 @@ __device__ __forceinline__ void r_split_write(const DevScene& sc, V3 d, V3 light
 // holds no better candidate; each candidate is considered by the one lane walking its leaf.  The
 // answer -- the highest reachable hitting rank, shaded by the lane holding it -- is the same.
 #ifndef GI_R_PAR
-#define GI_R_PAR 0   // Mode R large scenes: k_mode_r_par instead of k_mode_r_split
+// Mode R large scenes: k_mode_r_par instead of k_mode_r_split (R-C4 5.47 -> 4.34 ms, R-C3 equal)
+#define GI_R_PAR 1
+#endif
+#ifndef GI_R_PAR_DYN
+#define GI_R_PAR_DYN 1   // k_mode_r_par: items taken from a per-group LDS counter (0: item i by lane i mod 8)
 #endif
 #ifndef GI_R_MIN_WAVES
 #define GI_R_MIN_WAVES 1   // minimum waves per SIMD asked of the register allocator (Mode R kernels)
@@ -598,7 +602,11 @@ __global__ __launch_bounds__(256, GI_R_MIN_WAVES) void k_mode_r_par(DevScene sc,
     RMemo memo{GI_R_MEMO > 0 ? s_memo + grp * GI_R_MEMO : nullptr};
     if (GI_R_MEMO > 0)
         for (int k = sub; k < GI_R_MEMO; k += NSUB) memo.e[k] = -1;
-    if (sub == 0) s_best[grp] = 0ull;
+    __shared__ unsigned s_next[256 / NSUB];             // GI_R_PAR_DYN: the group's next item
+    if (sub == 0) {
+        s_best[grp] = 0ull;
+        s_next[grp] = 0u;
+    }
     __builtin_amdgcn_wave_barrier();
     const long long lt = ps >> 6;
     long long idx = -1;
@@ -638,7 +646,15 @@ __global__ __launch_bounds__(256, GI_R_MIN_WAVES) void k_mode_r_par(DevScene sc,
             }
         }
         __builtin_amdgcn_wave_barrier();
+#if GI_R_PAR_DYN
+        // items handed out in rank order from the group's LDS counter: a lane that finishes a short
+        // walk takes the next item instead of waiting behind a long one of its own
+        for (;;) {
+            const int i = (int)atomicAdd(s_next + grp, 1u);
+            if (i >= n) break;
+#else
         for (int i = sub; i < n; i += NSUB) {   // lane sub walks items sub, sub + 8, ...
+#endif
             const int it = s_item[grp][i];
             const int node = it >> 3, c = it & 7;
             best = max(best, (long long)*(volatile unsigned long long*)gb - 1);
@@ -803,7 +819,7 @@ __global__ __launch_bounds__(256) void k_mode_r(DevScene sc, CamDev cam, V3 ligh
 // live lanes have a finished ray, or when none is still traversing, so it executes with a
 // well-filled EXEC mask.  The per-path operation sequence is exactly the oracle's (pixel_mode_x in
 // oracle/gi_oracle.cpp), so results are bit-identical whatever the schedule.
-enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD = 4, PH_DONEPX = 5, PH_HELP = 6 };
+enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD = 4, PH_DONEPX = 5, PH_HELP = 6, PH_SUB = 7 };
 
 #ifndef GI_X_START_BURST
 #define GI_X_START_BURST 16   // primary rays a lane may resolve by the root test per handler run
@@ -819,6 +835,10 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 #endif
 #ifndef GI_X_HELP
 #define GI_X_HELP 1   // HBM-resident scenes: shadow rays handed to idle lanes of the wave (XHelp)
+#endif
+#ifndef GI_X_SUBS
+#define GI_X_SUBS 0   // handoff build: most closest-hit subtrees a lane has out with idle lanes (measured slower: C4
+                      // 1.65 -> 1.96 ms with 2 or 3, 2.17 with 4 -- the owner waits on subtrees it would have culled)
 #endif
 #ifndef GI_X_LEAFQ
 // quantised-node scenes, long launches: leaf tests postponed into leaf phases (LQ, mode_x_wave):
@@ -929,10 +949,27 @@ struct XWork {
 // and the frame, bit for bit -- are the oracle's.  Per lane in LDS (column layout, 256 lanes):
 // ray[7][256] (origin, direction, tmax), own[256] (owner lane within the wave, -1: none) and
 // res[256] (the owner's answer: 0 pending, 1 lit, 2 occluded).
+// Closest-hit subtrees (GI_X_SUBS): a lane tracing a closest-hit ray while its wave has idle lanes
+// gives a pending child of its shallowest unfinished level to one of them (at most GI_X_SUBS out at a
+// time).  The helper traverses that subtree from the owner's (t, primitive) best at the hand-over
+// and leaves its own best in the owner's slot; the owner, once its own traversal ends, takes the
+// (t, primitive) minimum over its own and its slots' answers.  The closest hit is that minimum over
+// every primitive whatever the order the boxes are visited in (culling is conservative), so the
+// frame is the same bit for bit.  own[] then carries the owner lane | 0x100 | slot << 9 | child << 12;
+// snode[256] / sbest[256] the subtree's node and the starting best primitive (the starting t in
+// ray[6]); per owner and slot: st[slot][256] (t), sp[slot][256] (primitive), sf[slot][256] (done);
+// sg[256]: per owner, the least t found so far by the ray's lanes (LDS atomic min), which every one
+// of them culls with.
 struct XHelp {
     double* ray;
     int* own;
     int* res;
+    int* snode;
+    int* sbest;
+    double* st;
+    double* sg;
+    int* sp;
+    int* sf;
 };
 __device__ __forceinline__ int nth_set_bit(unsigned long long m, unsigned n) {
     for (unsigned i = 0; i < n; ++i) m &= m - 1;
@@ -987,7 +1024,11 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     }
     bool pend = false;       // this lane's last shadow ray is being traced by a helper
     bool any_gave = false;   // some lane of the wave handed a shadow ray over in the last iteration
-    int howner = 0;          // PH_HELP: the owner lane
+    int howner = 0;          // PH_HELP / PH_SUB: the owner lane
+    constexpr bool SUB = HELP && NST && GI_X_SUBS > 0;
+    int nsub = 0;            // SUB: slots of this lane's closest-hit ray handed out (answered or not)
+    int hslot = 0;           // PH_SUB: the owner's slot
+    int root0 = 0;           // the node of traversal level 0 (the root; PH_SUB: the subtree's parent)
     uint32_t nnode = 0, nprim = 0, nrays = 0, nres = 0, npx = 0, nsteps = 0;
     long long idx = -1;
     int x = 0, y = 0;
@@ -1035,7 +1076,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             ++nprim;
             const double t = x_prim_t<TRI>(rec.h, o, d, MX_TMIN);
             const int pi = rec.h.prim;
-            if (phase != PH_CLOSEST) {
+            if (phase != PH_CLOSEST && phase != PH_SUB) {
                 if (t < tmax) { best = pi; raying = false; return; }   // any hit occludes
             } else if (t < tbest || (t == tbest && pi < best)) {
                 tbest = t;
@@ -1054,7 +1095,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 const double ta = x_prim_t<TRI>(r0.h, o, d, MX_TMIN);
                 const double tb = two ? x_prim_t<TRI>(r1.h, o, d, MX_TMIN) : INFINITY;
                 nprim += two ? 2 : 1;
-                if (phase != PH_CLOSEST) {
+                if (phase != PH_CLOSEST && phase != PH_SUB) {
                     if (ta < tmax || tb < tmax) {   // any hit occludes
                         best = ta < tmax ? r0.h.prim : r1.h.prim;
                         raying = false;
@@ -1096,30 +1137,44 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             const int ow = hp_.own[tid];
             if (ow >= 0) {
                 hp_.own[tid] = -1;
-                howner = ow;
+                howner = ow & 0xFF;
                 const double* r = hp_.ray + tid;
                 o = v3(r[0], r[256], r[512]);
                 d = v3(r[768], r[1024], r[1280]);
-                tmax = r[1536];
-                tbest = tmax;
-                tbest_f = up32(tmax);
-                phase = PH_HELP;
-                best = -1;
                 of = f3((float)o.x, (float)o.y, (float)o.z);
                 ivf = inv_dir(d);
                 dmask = (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
-                const uint32_t rm = children_mask<PAIR>(W, of, ivf, tbest_f, dmask);
-                node = 0;
                 level = 0;
                 mlo = mhi = 0;
-                lvl_set<SH>(mlo, mhi, 0, rm);
-                raying = rm != 0;
+                if (SUB && (ow & 0x100)) {   // a closest-hit subtree: child (ow >> 12) of node snode
+                    hslot = (ow >> 9) & 7;
+                    tmax = INFINITY;
+                    tbest = r[1536];
+                    tbest_f = tbest < INFINITY ? up32(tbest) : INFINITY;
+                    best = hp_.sbest[tid];
+                    phase = PH_SUB;
+                    root0 = hp_.snode[tid];
+                    node = root0;
+                    lvl_set<SH>(mlo, mhi, 0, 1u << ((ow >> 12) & 7));
+                    raying = true;
+                } else {                     // a shadow ray
+                    tmax = r[1536];
+                    tbest = tmax;
+                    tbest_f = up32(tmax);
+                    phase = PH_HELP;
+                    best = -1;
+                    const uint32_t rm = children_mask<PAIR>(W, of, ivf, tbest_f, dmask);
+                    root0 = 0;
+                    node = 0;
+                    lvl_set<SH>(mlo, mhi, 0, rm);
+                    raying = rm != 0;
+                }
                 if (PF && raying) prefetch();
             }
         }
         const unsigned long long m_live = __ballot(phase != PH_DEAD);
         if (m_live == 0) break;
-        const unsigned long long m_idle = HELP ? ~m_live : 0ull;   // lanes free to take a shadow ray
+        unsigned long long m_idle = HELP ? ~m_live : 0ull;   // lanes free to take a shadow ray
         bool gave = false;
         const bool trav = raying;
         const unsigned long long m_trav = __ballot(trav);
@@ -1176,6 +1231,11 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             // ---- one traversal step (stackless: 8-bit "children left" mask per level).  Invariant:
             // the current level has a child left; the step pops it, then climbs past exhausted
             // levels, so a ray ends in the step that exhausts the root level (no empty iteration).
+            const double tb0 = tbest;
+            if (SUB && (phase == PH_SUB || nsub > 0)) {   // the best t of the ray's lanes culls too
+                const double gb = hp_.sg[phase == PH_SUB ? wbase + howner : tid];
+                if (gb < tbest) tbest_f = up32(gb);
+            }
             const auto* nd = W + node;
             const uint32_t msk = lvl_get<SH>(mlo, mhi, level);
             const int kc = __builtin_ctz(msk);         // next child in front-to-back order
@@ -1191,7 +1251,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             // 1.82; the LDS kernel, whose re-cull is cheaper than a node test, keeps it: C3 +0.9%
             // without)
             bool keep = true;
-            if (phase == PH_CLOSEST && best >= 0 && (PAIR || GI_X_RECULL_INT_HBM || (ch < 0 && GI_X_RECULL_LEAF_HBM)))
+            if ((phase == PH_CLOSEST || phase == PH_SUB) && best >= 0 && (PAIR || GI_X_RECULL_INT_HBM || (ch < 0 && GI_X_RECULL_LEAF_HBM)))
                 keep = child_hit(nd, c, of, ivf, tbest_f);
             if (STATS) {
                 const unsigned long long mn = __ballot(keep && ch >= 0), ml = __ballot(keep && ch < 0);
@@ -1248,6 +1308,9 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     }
                 }
             }
+            if (SUB && tbest < tb0 && (phase == PH_SUB || nsub > 0))   // (t > 0: its bits order as t)
+                atomicMin(reinterpret_cast<unsigned long long*>(hp_.sg + (phase == PH_SUB ? wbase + howner : tid)),
+                          (unsigned long long)__double_as_longlong(tbest));
             if (raying && !desc) {        // climb to the nearest level with children left
                 uint32_t rest = lvl_get<SH>(mlo, mhi, level);
                 if constexpr (NST) {
@@ -1264,7 +1327,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                             rest = lvl_get<SH>(mlo, mhi, level);
                         } while (rest == 0 && level > 0);
 #endif
-                        node = level == 0 ? 0 : nst[level * 256];
+                        node = level == 0 ? root0 : nst[level * 256];
                     }
                 } else {
                     while (rest == 0 && level > 0) {
@@ -1347,6 +1410,50 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             }
             }
         }
+        if (SUB && phase == PH_SUB && !raying) {   // a finished subtree: its answer, at once; idle again
+            const int si = hslot * 256 + wbase + howner;
+            hp_.st[si] = tbest;
+            hp_.sp[si] = best;
+            __builtin_amdgcn_wave_barrier();
+            hp_.sf[si] = 1;
+            phase = PH_DEAD;
+            root0 = 0;
+        }
+        // SUB: closest-hit lanes give a pending child of their shallowest unfinished level (above the
+        // current one) to an idle lane -- the k-th giver the k-th idle lane
+        if (SUB && handoff && m_idle) {
+            int gl = -1;
+            if (phase == PH_CLOSEST && raying && nsub < GI_X_SUBS && level > 0) {
+                const uint64_t lm = level >= 8 ? mlo : mlo & ((1ull << (8 * level)) - 1);
+                const uint64_t hm = (SH || level <= 8) ? 0ull : mhi & ((1ull << (8 * (level - 8))) - 1);
+                gl = lm ? __builtin_ctzll(lm) / 8 : hm ? 8 + __builtin_ctzll(hm) / 8 : -1;
+            }
+            const unsigned long long m_want = __ballot(gl >= 0);
+            if (m_want) {
+                const unsigned n_idle = (unsigned)__popcll(m_idle);
+                if (gl >= 0) {
+                    const unsigned r = (unsigned)__popcll(m_want & ((1ull << lane) - 1));
+                    if (r < n_idle) {
+                        const int ht = wbase + nth_set_bit(m_idle, r);
+                        const uint32_t gm = lvl_get<SH>(mlo, mhi, gl);
+                        const int kc = __builtin_ctz(gm);
+                        lvl_set<SH>(mlo, mhi, gl, gm & (gm - 1));
+                        double* hr = hp_.ray + ht;
+                        hr[0] = o.x; hr[256] = o.y; hr[512] = o.z;
+                        hr[768] = d.x; hr[1024] = d.y; hr[1280] = d.z;
+                        hr[1536] = tbest;
+                        hp_.snode[ht] = gl == 0 ? root0 : nst[gl * 256];
+                        hp_.sbest[ht] = best;
+                        hp_.sf[nsub * 256 + tid] = 0;
+                        if (nsub == 0) hp_.sg[tid] = tbest;
+                        hp_.own[ht] = lane | 0x100 | (nsub << 9) | (kc << 12);
+                        ++nsub;
+                        gave = true;
+                    }
+                }
+                for (unsigned i = min(n_idle, (unsigned)__popcll(m_want)); i > 0; --i) m_idle &= m_idle - 1;
+            }
+        }
         const uint64_t t1 = STATS ? clock64() : 0;
         uint64_t t2 = t1;
         if (HELP && handle && phase == PH_HELP) {   // a helper's answer to its owner; idle again
@@ -1357,6 +1464,21 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
         bool hold = false;   // an owner whose helper has not answered yet: no handling this time
         if (HELP) {
             __builtin_amdgcn_wave_barrier();
+            if (SUB && handle && phase == PH_CLOSEST && nsub > 0) {
+                // the ray's subtrees: once all have answered, the (t, primitive) minimum
+                bool all = true;
+                for (int s2 = 0; s2 < nsub; ++s2) all = all && hp_.sf[s2 * 256 + tid] != 0;
+                if (!all) {
+                    hold = true;
+                } else {
+                    for (int s2 = 0; s2 < nsub; ++s2) {
+                        const double t = hp_.st[s2 * 256 + tid];
+                        const int pi = hp_.sp[s2 * 256 + tid];
+                        if (t < tbest || (t == tbest && pi < best)) { tbest = t; best = pi; }
+                    }
+                    nsub = 0;
+                }
+            }
             if (handle && pend) {
                 const int r = hp_.res[tid];
                 if (r == 0) {
@@ -1713,12 +1835,19 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
                                                                         wk, handle8, xflags, c);
     } else {
         // dynamic LDS: GI_X_NSTK's 16 levels x 256 lanes of node indices, then GI_X_HELP's handoff
-        // slots (7 x 256 doubles, 2 x 256 ints)
+        // slots (7 x 256 doubles, 2 x 256 ints) and GI_X_SUBS's (2 x 256 ints, 256 doubles per slot,
+        // 256 doubles of shared best t, 2 x 256 ints per slot)
         extern __shared__ int lds_nst[];
         XHelp hp;
         hp.ray = reinterpret_cast<double*>(lds_nst + (GI_X_NSTK ? 16 * 256 : 0));
         hp.own = reinterpret_cast<int*>(hp.ray + 7 * 256);
         hp.res = hp.own + 256;
+        hp.snode = hp.res + 256;   // GI_X_SUBS: the subtree hand-over and the owners' slots
+        hp.sbest = hp.snode + 256;
+        hp.st = reinterpret_cast<double*>(hp.sbest + 256);
+        hp.sg = hp.st + GI_X_SUBS * 256;
+        hp.sp = reinterpret_cast<int*>(hp.sg + 256);
+        hp.sf = hp.sp + GI_X_SUBS * 256;
         if constexpr (CN)   // quantised nodes (the default for large HBM-resident scenes); LQ in
                             // long launches (the handoff build's short launches are latency-bound)
             mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0, SH, GI_X_LEAFQ != 0 && !W4, TR && GI_X_TRI>(sc, sc.xcnodes, sc.xhot, sc.xprims,
@@ -1965,7 +2094,8 @@ hipError_t x_launch_config(const DevScene& sc, int device, XLaunchCfg& cfg) {
     const bool lds = x_env().lds != 0 && sc.x_lds_bytes > 0;
     cfg.lds_bytes = lds ? (size_t)sc.x_lds_bytes + ((sc.x_waves4 && GI_X_PSL) ? 256 * 10 * sizeof(double) : 0)
                         : (GI_X_NSTK ? 16 * 256 * sizeof(int) : 0) +
-                              (GI_X_HELP ? 256 * (7 * sizeof(double) + 2 * sizeof(int)) : 0);
+                              (GI_X_HELP ? 256 * (7 * sizeof(double) + 2 * sizeof(int)) : 0) +
+                              (GI_X_HELP && GI_X_SUBS ? 256 * (2 * sizeof(int) + sizeof(double) + GI_X_SUBS * (sizeof(double) + 2 * sizeof(int))) : 0);
     cfg.kv = 2 * (int)lds + ((lds && sc.x_waves4) ? 1 : 0);   // 0 / 1 (per launch, HELP): HBM-resident
     int cus = 0, per_cu = 0;
     hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);

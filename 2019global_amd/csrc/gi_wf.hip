@@ -39,6 +39,11 @@ namespace {
 #ifndef GI_WF_PAIR
 #define GI_WF_PAIR 1   // LDS-resident scenes: leaf records tested two at a time (two interleaved fp64 chains)
 #endif
+#ifndef GI_WF_SKIP
+// closest-hit traversal, LDS scenes: re-culled siblings skipped within one step -- measured slower
+// (k_seg C3 5.31 -> 5.39 ms, C2 0.161 -> 0.170, X-zoo 4.39 -> 4.48: a longer divergent step)
+#define GI_WF_SKIP 0
+#endif
 #ifndef GI_WF_TAKE
 #define GI_WF_TAKE 16   // most 64-entry batches a wave takes per atomic on the queue's counter
 #endif
@@ -86,10 +91,21 @@ __device__ __forceinline__ int wf_trace(NodeP W, HotP H, V3 o, V3 d, double tmax
         const uint32_t msk = lvl_get<SH>(mlo, mhi, level);
         const int kc = __builtin_ctz(msk);   // next child in front-to-back order
         lvl_set<SH>(mlo, mhi, level, msk & (msk - 1));
-        const int c = kc ^ dmask;
-        const int ch = nd->child[c];
+        int c = kc ^ dmask;
         bool keep = true;
-        if (!ANY && !NST && best >= 0) keep = child_hit(nd, c, of, ivf, tbf);   // (LDS scenes)
+        if (!ANY && !NST && best >= 0) {   // (LDS scenes) re-cull against the current best t
+            keep = child_hit(nd, c, of, ivf, tbf);
+            if (GI_WF_SKIP) {   // culled siblings are passed over inside this step, not one per step
+                uint32_t rest = lvl_get<SH>(mlo, mhi, level);
+                while (!keep && rest) {
+                    c = __builtin_ctz(rest) ^ dmask;
+                    rest &= rest - 1;
+                    lvl_set<SH>(mlo, mhi, level, rest);
+                    keep = child_hit(nd, c, of, ivf, tbf);
+                }
+            }
+        }
+        const int ch = nd->child[c];
         if (keep) {
             if (ch < 0) {   // leaf: the fp64 primitive tests decide
                 const int cnt = nd->cnt[c];
