@@ -531,8 +531,9 @@ __device__ __forceinline__ void r_split_write(const DevScene& sc, V3 d, V3 light
 // holds no better candidate; each candidate is considered by the one lane walking its leaf.  The
 // answer -- the highest reachable hitting rank, shaded by the lane holding it -- is the same.
 #ifndef GI_R_PAR
-// Mode R large scenes: k_mode_r_par instead of k_mode_r_split (R-C4 5.47 -> 4.34 ms, R-C3 equal)
-#define GI_R_PAR 1
+// Mode R large scenes: 1 k_mode_r_par instead of k_mode_r_split (R-C4 5.47 -> 4.41 ms, R-C3 equal),
+// 2 k_mode_r_batch (R-C4 3.19 ms)
+#define GI_R_PAR 2
 #endif
 #ifndef GI_R_PAR_DYN
 #define GI_R_PAR_DYN 1   // k_mode_r_par: items taken from a per-group LDS counter (0: item i by lane i mod 8)
@@ -589,6 +590,32 @@ __device__ __forceinline__ void r_par_walk(const DevScene& sc, int root, uint32_
         going = rest != 0;
     }
 }
+// the items of a pixel's walk: the root's hit slots, an interior one replaced by its own hit slots
+// (cooperative node tests), in rank order -- (node << 3) | slot, at most 64; written by sub-lane 0
+template <int NSUB>
+__device__ __forceinline__ int r_items(const XWNode* W, F3 of, F3 ivf, float tau, int sub, int* items) {
+    int n = 0;
+    uint32_t rm = children_mask_line_coop<NSUB>(W, of, ivf, tau, sub);
+    while (rm) {
+        const int c = __builtin_ctz(rm);
+        rm &= rm - 1;
+        const int ch = W[0].child[c];
+        if (ch < 0) {
+            if (sub == 0) items[n] = c;
+            ++n;
+        } else {
+            uint32_t cm = children_mask_line_coop<NSUB>(W + ch, of, ivf, tau, sub);
+            while (cm) {
+                const int c2 = __builtin_ctz(cm);
+                cm &= cm - 1;
+                if (sub == 0) items[n] = (ch << 3) | c2;
+                ++n;
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    return n;
+}
 template <bool STATS, bool TRI>
 __global__ __launch_bounds__(256, GI_R_MIN_WAVES) void k_mode_r_par(DevScene sc, CamDev cam, V3 light, TileMap m, double* rgb,
                                                      uint8_t* rgb8, unsigned long long* stats, float tau) {
@@ -625,27 +652,7 @@ __global__ __launch_bounds__(256, GI_R_MIN_WAVES) void k_mode_r_par(DevScene sc,
         const XWNode* W = sc.rc_nodes;
         const F3 of = f3((float)o.x, (float)o.y, (float)o.z);
         const F3 ivf = inv_dir(d);
-        // the items: the root's hit slots, an interior one replaced by its own hit slots (coop tests)
-        int n = 0;
-        uint32_t rm = children_mask_line_coop<NSUB>(W, of, ivf, tau, sub);
-        while (rm) {
-            const int c = __builtin_ctz(rm);
-            rm &= rm - 1;
-            const int ch = W[0].child[c];
-            if (ch < 0) {
-                if (sub == 0) s_item[grp][n] = c;
-                ++n;
-            } else {
-                uint32_t cm = children_mask_line_coop<NSUB>(W + ch, of, ivf, tau, sub);
-                while (cm) {
-                    const int c2 = __builtin_ctz(cm);
-                    cm &= cm - 1;
-                    if (sub == 0) s_item[grp][n] = (ch << 3) | c2;
-                    ++n;
-                }
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
+        const int n = r_items<NSUB>(W, of, ivf, tau, sub, s_item[grp]);
 #if GI_R_PAR_DYN
         // items handed out in rank order from the group's LDS counter: a lane that finishes a short
         // walk takes the next item instead of waiting behind a long one of its own
@@ -667,6 +674,165 @@ __global__ __launch_bounds__(256, GI_R_MIN_WAVES) void k_mode_r_par(DevScene sc,
                 const uint32_t cm = children_mask_line(W + ch, of, ivf, tau);
                 r_par_walk<TRI>(sc, ch, cm, of, ivf, tau, o, d, gb, best, mine, r, nnode, nprim, memo);
             }
+        }
+        r_split_write<NSUB, TRI>(sc, d, light, r, mine, sub, idx, rgb, rgb8);
+    } else if (sub == 0 && idx >= 0 && m.shard_count > 1) {   // padding slot of a packed tile
+        if (rgb) { rgb[3 * idx] = 0; rgb[3 * idx + 1] = 0; rgb[3 * idx + 2] = 0; }
+        if (rgb8) { rgb8[3 * idx] = 0; rgb8[3 * idx + 1] = 0; rgb8[3 * idx + 2] = 0; }
+    }
+    if (STATS) {
+        const bool px = ok && sub == 0;
+        wave_add_stats(stats, px ? 1 : 0, nnode, nprim, px ? 1 : 0);
+    }
+}
+
+// Mode R in rounds (GI_R_PAR=2; k_mode_r_batch).  k_mode_r_par's lanes run a candidate's exact tests
+// (ent_hit, the reachability node tests: fp64, ~55% of its VALU instructions) in the middle of their
+// own walks, so each test runs with the few lanes whose walks are at a leaf just then (VALU lane
+// utilisation 0.09 on R-C4).  Here every lane of the wave alternates two phases: a walk phase of at
+// most GI_R_BATCH_STEPS node steps, which only queues the entities of the leaves it meets (those
+// whose highest rank beats the group's best) in the lane's own LDS segment, and a test phase in which
+// the pixel's 8 lanes share the group's queued candidates (compacted, then candidate j by lane j mod
+// 8) -- the tests of all 8 pixels of the wave in one dense block.  Pruning and the answer are
+// k_mode_r_par's: the highest reachable hitting rank, every candidate considered by one lane.
+#ifndef GI_R_BATCH_STEPS
+#define GI_R_BATCH_STEPS 16   // node steps a lane's walk takes per round (R-C4: 2 4.04, 4 3.56, 8 3.41,
+                             // 16 3.19, 32 3.33 ms)
+#endif
+#ifndef GI_R_BATCH_SEG
+#define GI_R_BATCH_SEG 8     // candidates a lane queues per round (4 and 16: equal or slower)
+#endif
+template <bool STATS, bool TRI>
+__global__ __launch_bounds__(256, GI_R_MIN_WAVES) void k_mode_r_batch(DevScene sc, CamDev cam, V3 light, TileMap m, double* rgb,
+                                                       uint8_t* rgb8, unsigned long long* stats, float tau) {
+    constexpr int NSUB = 8, SEG = GI_R_BATCH_SEG;   // lanes per pixel; queued candidates per lane and round
+    const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long ps = g / NSUB;
+    const int sub = (int)(g % NSUB), grp = threadIdx.x / NSUB;
+    __shared__ int s_memo[GI_R_MEMO > 0 ? (256 / NSUB) * GI_R_MEMO : 1];
+    __shared__ unsigned long long s_best[256 / NSUB];   // the group's best rank + 1 (0: none)
+    __shared__ int s_item[256 / NSUB][64];              // (node << 3) | slot, in rank order
+    __shared__ unsigned s_next[256 / NSUB];             // the group's next item
+    __shared__ int s_seg[256 / NSUB][NSUB * SEG];       // each lane's queued candidates (SEG slots)
+    __shared__ int s_cand[256 / NSUB][NSUB * SEG];      // the group's candidates of the round, compacted
+    RMemo memo{GI_R_MEMO > 0 ? s_memo + grp * GI_R_MEMO : nullptr};
+    if (GI_R_MEMO > 0)
+        for (int k = sub; k < GI_R_MEMO; k += NSUB) memo.e[k] = -1;
+    if (sub == 0) {
+        s_best[grp] = 0ull;
+        s_next[grp] = 0u;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const long long lt = ps >> 6;
+    long long idx = -1;
+    int x = 0, y = 0;
+    const bool ok = lt < m.n_local && slot_pixel(m, lt, (int)(ps & 63), idx, x, y);
+    y += m.y0;
+    uint32_t nnode = 0, nprim = 0;
+    if (ok) {
+        const V3 o = cam.pos;
+        const V3 d = normalize(primary_dir(cam, (double)x, (double)y));
+        unsigned long long* gb = s_best + grp;
+        RResult r;
+        r.ent = -1;
+        long long best = -1, mine = -1;
+        for (int i = sub; i < sc.n_r_always; i += NSUB) r_par_consider<TRI>(sc, sc.r_always[i], o, d, gb, best, mine, r, nnode, nprim, memo);
+        const XWNode* W = sc.rc_nodes;
+        const F3 of = f3((float)o.x, (float)o.y, (float)o.z);
+        const F3 ivf = inv_dir(d);
+        const int n = r_items<NSUB>(W, of, ivf, tau, sub, s_item[grp]);
+        int* seg = s_seg[grp] + sub * SEG;
+        int* cand = s_cand[grp];
+        // the lane's walk: (root, node, level, masks) while walking; a leaf's entities [pcur, pend)
+        // still to queue; done once the group's items are all taken
+        bool walking = false, done = false;
+        int root = 0, node = 0, level = 0, pcur = 0, pend = 0;
+        uint64_t mlo = 0, mhi = 0;
+        for (;;) {
+            // ---- walk phase: queue up to SEG candidates within GI_R_BATCH_STEPS node steps
+            int nq = 0, steps = 0;
+            while (nq < SEG) {
+                best = max(best, (long long)*(volatile unsigned long long*)gb - 1);
+                if (pcur < pend) {   // the current leaf's entities: those that can still win
+                    const int e = sc.rc_ent[pcur++];
+                    const int a0 = sc.app_off[e];
+                    if (a0 != sc.app_off[e + 1] && sc.app_rank[a0] > best) seg[nq++] = e;
+                    continue;
+                }
+                if (steps >= GI_R_BATCH_STEPS || done) break;
+                ++steps;
+                if (!walking) {      // the group's next item
+                    const int i = (int)atomicAdd(s_next + grp, 1u);
+                    if (i >= n) {
+                        done = true;
+                        break;
+                    }
+                    const int it = s_item[grp][i];
+                    const int in = it >> 3, ic = it & 7;
+                    if (sc.rc_maxkey[in * 8 + ic] <= best) continue;
+                    const int ch = W[in].child[ic];
+                    if (ch < 0) {
+                        pcur = ~ch;
+                        pend = ~ch + W[in].cnt[ic];
+                    } else {
+                        ++nnode;
+                        const uint32_t cm = children_mask_line(W + ch, of, ivf, tau);
+                        if (cm) {
+                            root = node = ch;
+                            level = 0;
+                            mlo = mhi = 0;
+                            lvl_set(mlo, mhi, 0, cm);
+                            walking = true;
+                        }
+                    }
+                    continue;
+                }
+                // one step of the walk (r_par_walk's)
+                const uint32_t msk = lvl_get(mlo, mhi, level);
+                const int c = __builtin_ctz(msk);
+                lvl_set(mlo, mhi, level, msk & (msk - 1));
+                const XWNode* nd = W + node;
+                const int ch = nd->child[c];
+                if (sc.rc_maxkey[node * 8 + c] <= best) {
+                    lvl_set(mlo, mhi, level, 0);
+                } else if (ch < 0) {
+                    pcur = ~ch;
+                    pend = ~ch + nd->cnt[c];
+                } else {
+                    ++nnode;
+                    const uint32_t cm = children_mask_line(W + ch, of, ivf, tau);
+                    if (cm) {
+                        node = ch;
+                        ++level;
+                        lvl_set(mlo, mhi, level, cm);
+                    }
+                }
+                uint32_t rest = lvl_get(mlo, mhi, level);
+                while (rest == 0 && level > 0) {
+                    --level;
+                    node = level == 0 ? root : W[node].parent;
+                    rest = lvl_get(mlo, mhi, level);
+                }
+                walking = rest != 0;
+            }
+            // ---- the group's queue, compacted (inclusive prefix of the lanes' counts)
+            int incl = nq;
+#pragma unroll
+            for (int off = 1; off < NSUB; off <<= 1) {
+                const int t = __shfl_up(incl, off, NSUB);
+                if (sub >= off) incl += t;
+            }
+            const int total = __shfl(incl, NSUB - 1, NSUB);
+            for (int k = 0; k < nq; ++k) cand[incl - nq + k] = seg[k];
+            __builtin_amdgcn_wave_barrier();
+            // ---- test phase: candidate j by lane j mod 8
+            for (int j = sub; j < total; j += NSUB) {
+                best = max(best, (long long)*(volatile unsigned long long*)gb - 1);
+                r_par_consider<TRI>(sc, cand[j], o, d, gb, best, mine, r, nnode, nprim, memo);
+            }
+            __builtin_amdgcn_wave_barrier();
+            // the wave leaves the loop once none of its lanes has anything left (groups stay in step)
+            if (__ballot(!(done && !walking && pcur >= pend)) == 0) break;
         }
         r_split_write<NSUB, TRI>(sc, d, light, r, mine, sub, idx, rgb, rgb8);
     } else if (sub == 0 && idx >= 0 && m.shard_count > 1) {   // padding slot of a packed tile
@@ -2032,7 +2198,7 @@ long long shard_tiles(int w, int h, int shard_count) { return make_map(w, h, sha
 struct XEnv {
     int lds = 1, h8 = 0, xf = -1, run_log2 = 0, help = 1, spread = -1, r_split = -1, leaf8 = 0, wf = -1;
     int r_budget = GI_R_BUDGET;       // Mode R heavy-pixel hand-off (GI_R_BUDGET, candidates; 0: off)
-    int r_par = GI_R_PAR;             // Mode R walk split over the pixel's lanes (GI_R_PAR=0/1)
+    int r_par = GI_R_PAR;             // Mode R walk split over the pixel's lanes (GI_R_PAR=0/1; 2: in rounds)
     long long wf_chunk = 8ll << 20;   // wavefront Mode X: units (pixel samples) per chunk = queue capacity
 };
 const XEnv& x_env() {
@@ -2046,7 +2212,7 @@ const XEnv& x_env() {
         if (const char* v = std::getenv("GI_X_SPREAD")) env.spread = std::atoi(v);
         if (const char* v = std::getenv("GI_R_SPLIT")) env.r_split = std::atoi(v);
         if (const char* v = std::getenv("GI_R_BUDGET")) env.r_budget = std::max(0, std::atoi(v));
-        if (const char* v = std::getenv("GI_R_PAR")) env.r_par = std::atoi(v) != 0;
+        if (const char* v = std::getenv("GI_R_PAR")) env.r_par = std::atoi(v);
         if (const char* v = std::getenv("GI_X_LEAF8")) env.leaf8 = std::max(0, std::min(8, std::atoi(v)));
         if (const char* v = std::getenv("GI_X_WF")) env.wf = std::atoi(v);
         if (const char* v = std::getenv("GI_X_WF_CHUNK")) env.wf_chunk = std::max(1ll << 16, std::min(1ll << 30, std::atoll(v)));
@@ -2153,7 +2319,16 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
             if (e0 != hipSuccess) return e0;
         }
         mark(ev_begin);
-        if (split && env.r_par) {   // the walk split over the pixel's 8 lanes (k_mode_r_par)
+        if (split && env.r_par == 2) {   // walk and candidate tests in rounds (k_mode_r_batch)
+            const dim3 sgrid((unsigned)((m.n_local * (kTile * kTile) * 8 + 255) / 256));
+            if (sc.r_tri_only && GI_R_TRI) {
+                if (stats) hipLaunchKernelGGL((k_mode_r_batch<true, true>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
+                else hipLaunchKernelGGL((k_mode_r_batch<false, true>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
+            } else {
+                if (stats) hipLaunchKernelGGL((k_mode_r_batch<true, false>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
+                else hipLaunchKernelGGL((k_mode_r_batch<false, false>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
+            }
+        } else if (split && env.r_par) {   // the walk split over the pixel's 8 lanes (k_mode_r_par)
             const dim3 sgrid((unsigned)((m.n_local * (kTile * kTile) * 8 + 255) / 256));
             if (sc.r_tri_only && GI_R_TRI) {
                 if (stats) hipLaunchKernelGGL((k_mode_r_par<true, true>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);

@@ -87,7 +87,7 @@ def pmc_summary(workload: str, kernel: str = ""):
             continue
         if d.get("workload") != workload or not d.get("counters_per_launch"):
             continue
-        if kernel and kernel + "<" not in d.get("kernel", "") and kernel + "_split<" not in d.get("kernel", ""):
+        if kernel and not any(kernel + suf in d.get("kernel", "") for suf in ("<", "_split<", "_par<", "_batch<")):
             continue
         rnd = os.path.basename(p)[1:3]
         if best is None or rnd > best[0]:

@@ -12,7 +12,7 @@
 
     python profiles/summarize.py gpurun_out/prof_c3 C3 k_mode_x profiles/r01_c3_pmc.json [frames]
 
-kernel "auto": the dominant one of k_mode_x / k_wf_bounce / k_seg / k_mode_r_split / k_mode_r (by
+kernel "auto": the dominant one of k_mode_x / k_wf_bounce / k_seg / k_mode_r_par / k_mode_r_split / k_mode_r (by
 total time).  The wavefront
 form (k_wf_bounce) launches once per bounce, so its figures are per FRAME: `frames` (the bench's
 timed + warm-up frames) given, avg_launch_ns and every counter are the sums over the frame's
@@ -33,7 +33,7 @@ def main(d, workload, kernel, out, frames=None):
         stats[r["Name"]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                             "total_ns": float(r["TotalDurationNs"]), "pct": float(r["Percentage"])}
     if kernel == "auto":
-        kernel = max(("k_mode_x", "k_wf_bounce", "k_seg", "k_mode_r_split", "k_mode_r"),
+        kernel = max(("k_mode_x", "k_wf_bounce", "k_seg", "k_mode_r_par", "k_mode_r_batch", "k_mode_r_split", "k_mode_r"),
                      key=lambda kn: sum(v["total_ns"] for k, v in stats.items() if kn + "<false" in k))
     # the timed launches: STATS=false is the kernel's first template argument (k_mode_x<false, ...>)
     dom = [k for k in stats if kernel + "<false" in k] or [k for k in stats if kernel in k]
