@@ -672,6 +672,9 @@ void build_rcand(HostScene& hs) {
         }
     };
     if (nn > 0) dfs(0);
+    hs.r_leaf_of_rank.assign((size_t)next, -1);
+    for (int n = 0; n < nn; ++n)
+        if (leaf_rank[n] >= 0) hs.r_leaf_of_rank[(size_t)leaf_rank[n]] = n;
     hs.rpath_off.assign((size_t)nn + 1, 0);
     hs.rpath.clear();
     for (int n = 0; n < nn; ++n) {

@@ -24,6 +24,8 @@ long long shard_tiles(int w, int h, int shard_count);
 hipError_t x_launch_config(const DevScene& sc, int device, XLaunchCfg& cfg);
 int x_form_choice(const DevScene& sc, const XLaunchCfg& xc, const gi_opts& o);
 long long x_wf_chunk();
+int x_env_r_par();
+int x_env_rf_per_slot();
 hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev& cam, V3 light, int w, int h, int y0,
                          const gi_opts& o, double* rgb, uint8_t* rgb8, const XScratch& xs, KTimer* kt,
                          hipStream_t stream);
@@ -125,6 +127,32 @@ int ensure_xscratch(gi_scene* s, int w, int h, const gi_opts* o) {
             if ((e = hipMalloc((void**)&x.rheavy, (size_t)need * 2 * sizeof(long long))) != hipSuccess)
                 return hip_fail(e, "hipMalloc (heavy-pixel list)");
             x.rcap = need;
+        }
+        // the flat Mode R pipeline's buffers (GI_R_PAR=4): 128 candidate pairs per pixel slot of a
+        // tile's region (GI_RF_PER_SLOT; 1 GB per 1080p frame); a tile with more makes the frame fall
+        // back to k_mode_r_batch on the device (the overflow word)
+        if (s->dev.n_ents > 4096 && x_env_r_par() == 4 && x.rf_slots < need) {
+            (void)hipFree(x.rf_pairs);
+            (void)hipFree(x.rf_best);
+            (void)hipFree(x.rf_dir);
+            (void)hipFree(x.rf_rcnt);
+            (void)hipFree(x.rf_hcnt);
+            x.rf_rcnt = x.rf_hcnt = nullptr;
+            x.rf_pairs = nullptr;
+            x.rf_best = nullptr;
+            x.rf_dir = nullptr;
+            x.rf_cap = x.rf_slots = 0;
+            const long long cap = (long long)x_env_rf_per_slot() * need;
+            if ((e = hipMalloc((void**)&x.rf_pairs, (size_t)cap * 2 * sizeof(unsigned))) != hipSuccess ||
+                (e = hipMalloc((void**)&x.rf_best, (size_t)need * sizeof(unsigned long long))) != hipSuccess ||
+                (e = hipMalloc((void**)&x.rf_dir, (size_t)need * 3 * sizeof(double))) != hipSuccess ||
+                (e = hipMalloc((void**)&x.rf_rcnt, (size_t)(need / 64) * sizeof(unsigned))) != hipSuccess ||
+                (e = hipMalloc((void**)&x.rf_hcnt, (size_t)(need / 64) * sizeof(unsigned))) != hipSuccess)
+                return hip_fail(e, "hipMalloc (flat Mode R)");
+            if (!x.rf_cnt && (e = hipMalloc((void**)&x.rf_cnt, 8 * sizeof(unsigned))) != hipSuccess)
+                return hip_fail(e, "hipMalloc (flat Mode R counters)");
+            x.rf_cap = cap;
+            x.rf_slots = need;
         }
         return GI_OK;
     }
@@ -286,6 +314,12 @@ void destroy_scene(gi_scene* s) noexcept {
     }
     (void)hipFree(s->xs.wcnt);
     (void)hipFree(s->xs.rheavy);
+    (void)hipFree(s->xs.rf_pairs);
+    (void)hipFree(s->xs.rf_best);
+    (void)hipFree(s->xs.rf_dir);
+    (void)hipFree(s->xs.rf_rcnt);
+    (void)hipFree(s->xs.rf_hcnt);
+    (void)hipFree(s->xs.rf_cnt);
     (void)hipHostFree(s->xs.h_nlist);
     for (int i = 0; i < KTimer::kRing; i++) {
         if (s->kt.ev0[i]) (void)hipEventDestroy(static_cast<hipEvent_t>(s->kt.ev0[i]));
@@ -399,7 +433,8 @@ int scene_create_on(const gi_scene_desc* desc, int device, gi_scene** out) {
         (e = upload(sp, h.app_rank, &d.app_rank)) != hipSuccess || (e = upload(sp, h.rpath_off, &d.rpath_off)) != hipSuccess ||
         (e = upload(sp, h.rpath, &d.rpath)) != hipSuccess || (e = upload(sp, h.rc_nodes, &d.rc_nodes)) != hipSuccess ||
         (e = upload(sp, h.rc_ent, &d.rc_ent)) != hipSuccess || (e = upload(sp, h.rc_maxkey, &d.rc_maxkey)) != hipSuccess ||
-        (e = upload(sp, h.r_always, &d.r_always)) != hipSuccess)
+        (e = upload(sp, h.r_always, &d.r_always)) != hipSuccess ||
+        (e = upload(sp, h.r_leaf_of_rank, &d.r_leaf_of_rank)) != hipSuccess)
         return hip_fail(e, "scene upload");
     d.n_rnodes = (int32_t)h.rnodes.size();
     d.n_ents = (int32_t)h.ents.size();

@@ -532,8 +532,8 @@ __device__ __forceinline__ void r_split_write(const DevScene& sc, V3 d, V3 light
 // answer -- the highest reachable hitting rank, shaded by the lane holding it -- is the same.
 #ifndef GI_R_PAR
 // Mode R large scenes: 1 k_mode_r_par instead of k_mode_r_split (R-C4 5.47 -> 4.41 ms, R-C3 equal),
-// 2 k_mode_r_batch (R-C4 3.19 ms)
-#define GI_R_PAR 2
+// 2 k_mode_r_batch (3.19 ms), 4 the flat phases k_rf_* (2.58 ms)
+#define GI_R_PAR 4
 #endif
 #ifndef GI_R_PAR_DYN
 #define GI_R_PAR_DYN 1   // k_mode_r_par: items taken from a per-group LDS counter (0: item i by lane i mod 8)
@@ -704,7 +704,10 @@ __global__ __launch_bounds__(256, GI_R_MIN_WAVES) void k_mode_r_par(DevScene sc,
 #endif
 template <bool STATS, bool TRI>
 __global__ __launch_bounds__(256, GI_R_MIN_WAVES) void k_mode_r_batch(DevScene sc, CamDev cam, V3 light, TileMap m, double* rgb,
-                                                       uint8_t* rgb8, unsigned long long* stats, float tau) {
+                                                       uint8_t* rgb8, unsigned long long* stats, float tau,
+                                                       const unsigned* only_if) {
+    // only_if: the flat pipeline's counters -- run only when its candidate list overflowed
+    if (only_if && *(volatile const unsigned*)only_if == 0) return;
     constexpr int NSUB = 8, SEG = GI_R_BATCH_SEG;   // lanes per pixel; queued candidates per lane and round
     const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     const long long ps = g / NSUB;
@@ -843,6 +846,225 @@ __global__ __launch_bounds__(256, GI_R_MIN_WAVES) void k_mode_r_batch(DevScene s
         const bool px = ok && sub == 0;
         wave_add_stats(stats, px ? 1 : 0, nnode, nprim, px ? 1 : 0);
     }
+}
+
+// Flat Mode R (GI_R_PAR=4; VERDICT r03's chip-wide phases).  k_rf_walk: one lane per pixel slot
+// walks the whole line BVH (no rank pruning) and appends a (slot, entity) pair for every entity of
+// every leaf its line crosses; k_rf_hit: ent_hit over the pairs, the hitting ones kept; k_rf_reach:
+// per hitting pair, the entity's appearances latest first against the pixel's best rank so far
+// (atomic max), the first reachable one raising it; k_rf_shade: per pixel, the entity of the best
+// rank (r_leaf_of_rank) tested again for its hit point and normal, shaded.  The answer -- the
+// highest reachable hitting rank -- is the other kernels'.  No global counter: the walk's wave for
+// tile t owns region t of the pair buffer (per_slot x 64 pairs; through per-lane LDS buffers, the
+// wave keeping its own fill), rcnt[t] its pairs; k_rf_hit compacts a region's hitting pairs in place
+// of its pairs (hcnt[t]); persistent waves take regions in turn.  A region that fills raises the overflow word:
+// k_rf_hit / k_rf_reach / k_rf_shade then do nothing and k_mode_r_batch, guarded by the same word,
+// renders the frame.  (A first version appended through one device-wide counter: its per-wave
+// atomics serialised, k_rf_hit waited 95% of its cycles.)
+#ifndef GI_RF_BUF
+#define GI_RF_BUF 16   // k_rf_walk: pairs a lane buffers in LDS before the wave flushes
+#endif
+struct RFlat {
+    unsigned* pairs;            // n_regions x rs pairs (slot, entity)
+    unsigned* hits;             // = pairs: each region's hitting pairs compacted in place (a hit is
+                                //   written at or before its pair's position, after the wave read it)
+    unsigned long long* best;   // per pixel slot: best rank + 1
+    unsigned* cnt;              // word 0: overflow
+    unsigned* rcnt;             // per region: pairs
+    unsigned* hcnt;             // per region: hitting pairs
+    double* dir;                // per pixel slot: its primary direction (k_rf_walk writes, the others read)
+    unsigned rs;                // pairs per region
+};
+__device__ __forceinline__ V3 rf_dir(const RFlat& f, unsigned slot) {
+    const double* q = f.dir + 3 * (size_t)slot;
+    return v3(q[0], q[1], q[2]);
+}
+template <bool STATS>
+__global__ __launch_bounds__(256) void k_rf_walk(DevScene sc, CamDev cam, TileMap m, float tau, RFlat f,
+                                                 unsigned long long* stats) {
+    __shared__ int s_buf[256][GI_RF_BUF];
+    const long long slot = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long region = slot >> 6;
+    const int lane = threadIdx.x & 63;
+    int* buf = s_buf[threadIdx.x];
+    long long idx = -1;
+    int x = 0, y = 0;
+    const bool in = slot < m.n_local * 64;
+    const bool ok = in && slot_pixel(m, slot >> 6, (int)(slot & 63), idx, x, y);
+    if (in) f.best[slot] = 0ull;
+    uint32_t nnode = 0;
+    const XWNode* W = sc.rc_nodes;
+    uint64_t mlo = 0, mhi = 0;
+    int node = 0, level = 0, pcur = 0, pend = 0, ai = 0, nb = 0;
+    unsigned fill = 0;   // the wave's pairs in its region so far (the same in every lane)
+    bool walking = false;
+    F3 of = f3(0, 0, 0), ivf = f3(1, 1, 1);
+    if (ok) {
+        const V3 d = normalize(primary_dir(cam, (double)x, (double)(y + m.y0)));
+        double* q = f.dir + 3 * slot;
+        q[0] = d.x; q[1] = d.y; q[2] = d.z;
+        of = f3((float)cam.pos.x, (float)cam.pos.y, (float)cam.pos.z);
+        ivf = inv_dir(d);
+        const uint32_t rm = children_mask_line(W, of, ivf, tau);
+        lvl_set(mlo, mhi, 0, rm);
+        walking = rm != 0;
+    }
+    for (;;) {
+        if (ok) {
+            while (ai < sc.n_r_always && nb < GI_RF_BUF) buf[nb++] = sc.r_always[ai++];   // every ray's ImpSpheres
+            while (pcur < pend && nb < GI_RF_BUF) {
+                const int e = sc.rc_ent[pcur++];
+                if (sc.app_off[e] != sc.app_off[e + 1]) buf[nb++] = e;
+            }
+            if (pcur >= pend && walking) {   // one step of the whole walk
+                const uint32_t msk = lvl_get(mlo, mhi, level);
+                const int c = __builtin_ctz(msk);
+                lvl_set(mlo, mhi, level, msk & (msk - 1));
+                const XWNode* nd = W + node;
+                const int ch = nd->child[c];
+                if (ch < 0) {
+                    pcur = ~ch;
+                    pend = ~ch + nd->cnt[c];
+                } else {
+                    ++nnode;
+                    const uint32_t cm = children_mask_line(W + ch, of, ivf, tau);
+                    if (cm) {
+                        node = ch;
+                        ++level;
+                        lvl_set(mlo, mhi, level, cm);
+                    }
+                }
+                uint32_t rest = lvl_get(mlo, mhi, level);
+                while (rest == 0 && level > 0) {
+                    --level;
+                    node = level == 0 ? 0 : W[node].parent;
+                    rest = lvl_get(mlo, mhi, level);
+                }
+                walking = rest != 0;
+            }
+        }
+        const bool more = ok && (walking || pcur < pend || ai < sc.n_r_always);
+        const unsigned long long m_more = __ballot(more);
+        if (m_more == 0 || __ballot(nb > GI_RF_BUF / 2) != 0) {   // flush the wave's buffers into its region
+            int incl = nb;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int t = __shfl_up(incl, off);
+                if (lane >= off) incl += t;
+            }
+            const unsigned tot = (unsigned)__shfl(incl, 63);
+            for (int k = 0; k < nb; ++k) {
+                const unsigned j = fill + (unsigned)(incl - nb + k);
+                if (j < f.rs) {
+                    const size_t at = (size_t)region * f.rs + j;
+                    f.pairs[2 * at] = (unsigned)slot;
+                    f.pairs[2 * at + 1] = (unsigned)buf[k];
+                } else {
+                    f.cnt[0] = 1u;
+                }
+            }
+            fill += tot;
+            nb = 0;
+        }
+        if (m_more == 0) break;
+    }
+    if (in && lane == 0) f.rcnt[region] = min(fill, f.rs);
+    if (STATS) wave_add_stats(stats, 0, nnode, 0, 0);
+}
+// the pairs' exact entity tests; each region's hitting pairs compacted in place of the region
+template <bool STATS, bool TRI>
+__global__ __launch_bounds__(256) void k_rf_hit(DevScene sc, CamDev cam, TileMap m, RFlat f, unsigned long long* stats) {
+    if (*(volatile const unsigned*)f.cnt) return;
+    const int lane = threadIdx.x & 63;
+    const long long n_regions = m.n_local;
+    const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_w = ((long long)gridDim.x * blockDim.x) >> 6;
+    uint32_t nprim = 0;
+    for (long long r = gw; r < n_regions; r += n_w) {
+        const unsigned n = f.rcnt[r];
+        const size_t base = (size_t)r * f.rs;
+        unsigned kept = 0;
+        for (unsigned i0 = 0; i0 < n; i0 += 64) {
+            const unsigned i = i0 + lane;
+            bool hit = false;
+            unsigned slot = 0, e = 0;
+            if (i < n) {
+                slot = f.pairs[2 * (base + i)];
+                e = f.pairs[2 * (base + i) + 1];
+                const V3 d = rf_dir(f, slot);
+                V3 P, N;
+                hit = ent_hit<TRI>(sc, sc.ents[e], cam.pos, d, P, N, nprim) && sq3(P - cam.pos) < DBL_MAX;   // raytracer.h:58-65
+            }
+            const unsigned long long mh = __ballot(hit);
+            if (hit) {
+                const size_t at = base + kept + (unsigned)__popcll(mh & ((1ull << lane) - 1));
+                f.hits[2 * at] = slot;
+                f.hits[2 * at + 1] = e;
+            }
+            kept += (unsigned)__popcll(mh);
+        }
+        if (lane == 0) f.hcnt[r] = kept;
+    }
+    if (STATS) wave_add_stats(stats, 0, 0, nprim, 0);
+}
+// per hitting pair: its entity's latest reachable appearance that beats the pixel's best rank
+template <bool STATS>
+__global__ __launch_bounds__(256) void k_rf_reach(DevScene sc, CamDev cam, TileMap m, RFlat f, unsigned long long* stats) {
+    if (*(volatile const unsigned*)f.cnt) return;
+    const int lane = threadIdx.x & 63;
+    const long long n_regions = m.n_local;
+    const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_w = ((long long)gridDim.x * blockDim.x) >> 6;
+    uint32_t nnode = 0;
+    for (long long r = gw; r < n_regions; r += n_w) {
+        const unsigned n = f.hcnt[r];
+        const size_t base = (size_t)r * f.rs;
+        for (unsigned i = lane; i < n; i += 64) {
+            const unsigned slot = f.hits[2 * (base + i)];
+            const int e = (int)f.hits[2 * (base + i) + 1];
+            const V3 d = rf_dir(f, slot);
+            const int a1 = sc.app_off[e + 1];
+            for (int a = sc.app_off[e]; a < a1; ++a) {
+                const long long rk = sc.app_rank[a];
+                if (rk <= (long long)*(volatile unsigned long long*)(f.best + slot) - 1) break;
+                if (r_leaf_reachable(sc, sc.app_leaf[a], cam.pos, d, nnode)) {
+                    atomicMax(f.best + slot, (unsigned long long)(rk + 1));
+                    break;
+                }
+            }
+        }
+    }
+    if (STATS) wave_add_stats(stats, 0, nnode, 0, 0);
+}
+// per pixel: the best rank's entity, shaded
+template <bool STATS, bool TRI>
+__global__ __launch_bounds__(256) void k_rf_shade(DevScene sc, CamDev cam, V3 light, TileMap m, double* rgb, uint8_t* rgb8,
+                                                  RFlat f, unsigned long long* stats) {
+    if (*(volatile const unsigned*)f.cnt) return;
+    const long long slot = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    long long idx = -1;
+    int x = 0, y = 0;
+    const bool ok = slot < m.n_local * 64 && slot_pixel(m, slot >> 6, (int)(slot & 63), idx, x, y);
+    uint32_t nprim = 0;
+    if (ok) {
+        const V3 d = rf_dir(f, (unsigned)slot);
+        const long long b = (long long)f.best[slot] - 1;
+        double c0 = 0, c1 = 0, c2 = 0;
+        if (b >= 0) {
+            const int leaf = sc.r_leaf_of_rank[b >> 32];
+            const REnt& e = sc.ents[sc.leaf_ents[sc.rnodes[leaf].ent_off + (int)(b & 0xFFFFFFFFll)]];
+            V3 P, N;
+            ent_hit<TRI>(sc, e, cam.pos, d, P, N, nprim);
+            int32_t u, v;
+            tex_coord<TRI>(sc, e, P, u, v);
+            const V3 col = shade_ref(e, d, light, P, N, u, v);
+            c0 = col.x; c1 = col.y; c2 = col.z;
+        }
+        if (rgb) { rgb[3 * idx] = c0; rgb[3 * idx + 1] = c1; rgb[3 * idx + 2] = c2; }
+        if (rgb8) quantize(c0, c1, c2, rgb8 + 3 * idx);
+    } else if (idx >= 0 && m.shard_count > 1) {   // padding slot of a packed tile
+        if (rgb) { rgb[3 * idx] = 0; rgb[3 * idx + 1] = 0; rgb[3 * idx + 2] = 0; }
+        if (rgb8) { rgb8[3 * idx] = 0; rgb8[3 * idx + 1] = 0; rgb8[3 * idx + 2] = 0; }
+    }
+    if (STATS) wave_add_stats(stats, ok ? 1 : 0, 0, nprim, ok ? 1 : 0);
 }
 
 // pixels whose first pass gave up (k_mode_r_split with a budget): (pixel slot, rank found) pairs
@@ -2198,8 +2420,9 @@ long long shard_tiles(int w, int h, int shard_count) { return make_map(w, h, sha
 struct XEnv {
     int lds = 1, h8 = 0, xf = -1, run_log2 = 0, help = 1, spread = -1, r_split = -1, leaf8 = 0, wf = -1;
     int r_budget = GI_R_BUDGET;       // Mode R heavy-pixel hand-off (GI_R_BUDGET, candidates; 0: off)
-    int r_par = GI_R_PAR;             // Mode R walk split over the pixel's lanes (GI_R_PAR=0/1; 2: in rounds)
+    int r_par = GI_R_PAR;             // Mode R walk split over the pixel's lanes (GI_R_PAR=0/1; 2: in rounds; 4: flat)
     long long wf_chunk = 8ll << 20;   // wavefront Mode X: units (pixel samples) per chunk = queue capacity
+    int rf_per_slot = 128;            // flat Mode R: candidate pairs per pixel slot of a tile's region (GI_RF_PER_SLOT)
 };
 const XEnv& x_env() {
     static XEnv env;
@@ -2213,6 +2436,7 @@ const XEnv& x_env() {
         if (const char* v = std::getenv("GI_R_SPLIT")) env.r_split = std::atoi(v);
         if (const char* v = std::getenv("GI_R_BUDGET")) env.r_budget = std::max(0, std::atoi(v));
         if (const char* v = std::getenv("GI_R_PAR")) env.r_par = std::atoi(v);
+        if (const char* v = std::getenv("GI_RF_PER_SLOT")) env.rf_per_slot = std::max(1, std::min(1024, std::atoi(v)));
         if (const char* v = std::getenv("GI_X_LEAF8")) env.leaf8 = std::max(0, std::min(8, std::atoi(v)));
         if (const char* v = std::getenv("GI_X_WF")) env.wf = std::atoi(v);
         if (const char* v = std::getenv("GI_X_WF_CHUNK")) env.wf_chunk = std::max(1ll << 16, std::min(1ll << 30, std::atoll(v)));
@@ -2255,6 +2479,8 @@ int x_form_choice(const DevScene& sc, const XLaunchCfg& xc, const gi_opts& o) {
     return (xc.kv >= 2 || (size_t)sc.n_xwnodes * sizeof(XWNode) <= ((size_t)1 << 20)) ? 2 : 0;
 }
 long long x_wf_chunk() { return x_env().wf_chunk; }
+int x_env_r_par() { return x_env().r_par; }
+int x_env_rf_per_slot() { return x_env().rf_per_slot; }
 
 hipError_t x_launch_config(const DevScene& sc, int device, XLaunchCfg& cfg) {
     const bool lds = x_env().lds != 0 && sc.x_lds_bytes > 0;
@@ -2319,14 +2545,44 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
             if (e0 != hipSuccess) return e0;
         }
         mark(ev_begin);
-        if (split && env.r_par == 2) {   // walk and candidate tests in rounds (k_mode_r_batch)
+        if (split && env.r_par == 4 && xs.rf_pairs && xs.rf_slots >= m.n_local * (kTile * kTile)) {   // flat phases
+            const RFlat f{xs.rf_pairs, xs.rf_pairs, xs.rf_best, xs.rf_cnt, xs.rf_rcnt, xs.rf_hcnt, xs.rf_dir,
+                          (unsigned)(xs.rf_cap / xs.rf_slots * 64)};
+            const dim3 pgrid((unsigned)((m.n_local * (kTile * kTile) + 255) / 256)), fgrid(4096);
+            hipError_t e1 = hipMemsetAsync(xs.rf_cnt, 0, sizeof(unsigned), stream);
+            if (e1 != hipSuccess) return e1;
+            const dim3 sgrid((unsigned)((m.n_local * (kTile * kTile) * 8 + 255) / 256));
+            if (stats) hipLaunchKernelGGL(k_rf_walk<true>, pgrid, block, 0, stream, sc, cam, m, tau, f, st);
+            else hipLaunchKernelGGL(k_rf_walk<false>, pgrid, block, 0, stream, sc, cam, m, tau, f, st);
+            if (sc.r_tri_only && GI_R_TRI) {
+                if (stats) hipLaunchKernelGGL((k_rf_hit<true, true>), fgrid, block, 0, stream, sc, cam, m, f, st);
+                else hipLaunchKernelGGL((k_rf_hit<false, true>), fgrid, block, 0, stream, sc, cam, m, f, st);
+            } else {
+                if (stats) hipLaunchKernelGGL((k_rf_hit<true, false>), fgrid, block, 0, stream, sc, cam, m, f, st);
+                else hipLaunchKernelGGL((k_rf_hit<false, false>), fgrid, block, 0, stream, sc, cam, m, f, st);
+            }
+            if (stats) hipLaunchKernelGGL(k_rf_reach<true>, fgrid, block, 0, stream, sc, cam, m, f, st);
+            else hipLaunchKernelGGL(k_rf_reach<false>, fgrid, block, 0, stream, sc, cam, m, f, st);
+            if (sc.r_tri_only && GI_R_TRI) {
+                if (stats) hipLaunchKernelGGL((k_rf_shade<true, true>), pgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, f, st);
+                else hipLaunchKernelGGL((k_rf_shade<false, true>), pgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, f, st);
+                // the candidate buffer overflowed: the batch kernel renders the frame instead
+                if (stats) hipLaunchKernelGGL((k_mode_r_batch<true, true>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, xs.rf_cnt);
+                else hipLaunchKernelGGL((k_mode_r_batch<false, true>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, xs.rf_cnt);
+            } else {
+                if (stats) hipLaunchKernelGGL((k_rf_shade<true, false>), pgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, f, st);
+                else hipLaunchKernelGGL((k_rf_shade<false, false>), pgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, f, st);
+                if (stats) hipLaunchKernelGGL((k_mode_r_batch<true, false>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, xs.rf_cnt);
+                else hipLaunchKernelGGL((k_mode_r_batch<false, false>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, xs.rf_cnt);
+            }
+        } else if (split && env.r_par >= 2) {   // walk and candidate tests in rounds (k_mode_r_batch)
             const dim3 sgrid((unsigned)((m.n_local * (kTile * kTile) * 8 + 255) / 256));
             if (sc.r_tri_only && GI_R_TRI) {
-                if (stats) hipLaunchKernelGGL((k_mode_r_batch<true, true>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
-                else hipLaunchKernelGGL((k_mode_r_batch<false, true>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
+                if (stats) hipLaunchKernelGGL((k_mode_r_batch<true, true>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, nullptr);
+                else hipLaunchKernelGGL((k_mode_r_batch<false, true>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, nullptr);
             } else {
-                if (stats) hipLaunchKernelGGL((k_mode_r_batch<true, false>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
-                else hipLaunchKernelGGL((k_mode_r_batch<false, false>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
+                if (stats) hipLaunchKernelGGL((k_mode_r_batch<true, false>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, nullptr);
+                else hipLaunchKernelGGL((k_mode_r_batch<false, false>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, nullptr);
             }
         } else if (split && env.r_par) {   // the walk split over the pixel's 8 lanes (k_mode_r_par)
             const dim3 sgrid((unsigned)((m.n_local * (kTile * kTile) * 8 + 255) / 256));

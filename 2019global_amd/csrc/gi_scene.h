@@ -142,6 +142,7 @@ struct HostScene {
     std::vector<int64_t> rc_maxkey;  //   per node slot (8 per node): the highest app_rank under it;
                                      //   a node's slots are in decreasing order of it
     std::vector<int32_t> r_always;   // ImpSpheres that appear in a leaf (tested by every ray)
+    std::vector<int32_t> r_leaf_of_rank;   // leaf node of each DFS rank (app_rank >> 32)
     double rc_ext = 0;               // max |coordinate| of the line BVH's boxes
     int32_t x_handle8 = 6;   // Mode X handler threshold (eighths), chosen by the builder
     int32_t x_flags = 0;     // Mode X schedule flags (DevScene::x_flags), chosen by the builder
@@ -200,6 +201,7 @@ struct DevScene {
     const int32_t* rc_ent;
     const int64_t* rc_maxkey;
     const int32_t* r_always;
+    const int32_t* r_leaf_of_rank;
     int32_t n_r_always;
     float rc_ext;
 };
@@ -235,6 +237,17 @@ struct XScratch {
     // Mode R heavy-pixel list of the budgeted split kernel: (pixel slot, rank) per entry, rcap entries
     long long* rheavy = nullptr;
     long long rcap = 0;
+    // flat Mode R (GI_R_PAR=4): candidate pairs (pixel slot, entity), rf_cap, in regions of
+    // rf_cap / rf_slots x 64 per tile, the hitting ones compacted in place; per tile the pairs / hits
+    // in its region, the best
+    // rank + 1 and the primary direction per pixel slot (rf_slots), and the overflow word
+    unsigned* rf_pairs = nullptr;
+    unsigned long long* rf_best = nullptr;
+    double* rf_dir = nullptr;   // per pixel slot: the primary direction (3 doubles), written by the walk
+    unsigned* rf_cnt = nullptr;
+    unsigned* rf_rcnt = nullptr;
+    unsigned* rf_hcnt = nullptr;
+    long long rf_cap = 0, rf_slots = 0;
 };
 
 // Mode X launch configuration, computed once per scene when it is created (gi_capi.cpp, on the

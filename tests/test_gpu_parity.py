@@ -1011,3 +1011,42 @@ def test_mode_x_forms_bit_identical(torch_cuda, name, w, h, spp, depth, shard):
     if shard[0] == 1:
         o = U.oracle_render(sc.to_scn(), w, h, mode=1, spp=spp, depth=depth, seed=7)
         assert U.bits_equal(frames["k_seg"][0].reshape(-1, 3), o["rgb"]).all()
+
+
+def test_mode_r_kernels_frame_identical(torch_cuda, tmp_path):
+    """The Mode R kernels for large scenes -- the walk split over a pixel's lanes (GI_R_PAR=1,
+    k_mode_r_par), walk / test rounds (2, k_mode_r_batch) and the flat phases (4: k_rf_walk, k_rf_hit,
+    k_rf_reach, k_rf_shade), also with a candidate buffer too small for the frame (GI_RF_PER_SLOT=1:
+    the device falls back to k_mode_r_batch) -- render the whole R-C4 frame (the 100k soup, 1920x1080)
+    and a 2-way sharded, packed 480x270 frame of it bit for bit alike (read once per process: child
+    processes render)."""
+    import subprocess
+    import sys
+    code = ("import sys, numpy as np, torch; sys.path.insert(0, %r); sys.path.insert(0, %r); import oracle_util as U; "
+            "gi = U.pkg(); S = U.scenes(); res = {}\n"
+            "sc = S.named_scene('soup100000'); d = gi.DeviceScene.from_scene(sc)\n"
+            "cam = gi.Camera(sc.cam_pos, sc.cam_look, sc.focal)\n"
+            "res['c4'] = d.render(cam, sc.light, 1920, 1080)[0]\n"
+            "per = gi.shard_tiles(480, 270, 2) * gi.TILE * gi.TILE * 3\n"
+            "p = torch.zeros(2 * per, dtype=torch.float64, device='cuda')\n"
+            "for r in range(2): d.render_device(cam, sc.light, 480, 270, p.data_ptr() + r * per * 8, 0, shard_count=2, shard_index=r)\n"
+            "torch.cuda.synchronize(); res['packed'] = p.cpu().numpy()\n"
+            "np.savez(sys.argv[1], **res)") % (U.ROOT, os.path.join(U.ROOT, "tests"))
+    frames = {}
+    for tag, env in (("par", {"GI_R_PAR": "1"}), ("batch", {"GI_R_PAR": "2"}), ("flat", {"GI_R_PAR": "4"}),
+                     ("flat_overflow", {"GI_R_PAR": "4", "GI_RF_PER_SLOT": "1"})):
+        out = tmp_path / (tag + ".npz")
+        subprocess.run([sys.executable, "-c", code, str(out)], check=True, timeout=300, env=dict(os.environ, **env))
+        frames[tag] = dict(np.load(out))
+    torch = torch_cuda
+    sc = _scene("soup100000")
+    d = dev_scene("soup100000")
+    rgb, _ = d.render(cam_of(sc), sc.light, 1920, 1080)
+    per = gi.shard_tiles(480, 270, 2) * gi.TILE * gi.TILE * 3
+    p = torch.zeros(2 * per, dtype=torch.float64, device="cuda")
+    for r in range(2):
+        d.render_device(cam_of(sc), sc.light, 480, 270, p.data_ptr() + r * per * 8, 0, shard_count=2, shard_index=r)
+    torch.cuda.synchronize()
+    for tag, f in frames.items():
+        assert U.bits_equal(rgb, f["c4"]).all(), tag
+        assert U.bits_equal(p.cpu().numpy(), f["packed"]).all(), tag + " packed"
