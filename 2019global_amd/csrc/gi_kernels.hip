@@ -1006,9 +1006,13 @@ __global__ __launch_bounds__(256) void k_rf_hit(DevScene sc, CamDev cam, TileMap
     }
     if (STATS) wave_add_stats(stats, 0, 0, nprim, 0);
 }
-// per hitting pair: its entity's latest reachable appearance that beats the pixel's best rank
+// per hitting pair: its entity's latest reachable appearance that beats the pixel's best rank.
+// One wave per workgroup: the wave's LDS holds the node-test memo (RMemo, GI_R_MEMO entries) of each
+// of the 64 pixels of the region (tile) it works on -- the pixel's pairs share their root paths'
+// upper levels.
 template <bool STATS>
-__global__ __launch_bounds__(256) void k_rf_reach(DevScene sc, CamDev cam, TileMap m, RFlat f, unsigned long long* stats) {
+__global__ __launch_bounds__(64) void k_rf_reach(DevScene sc, CamDev cam, TileMap m, RFlat f, unsigned long long* stats) {
+    __shared__ int s_memo[GI_R_MEMO > 0 ? 64 * GI_R_MEMO : 1];
     if (*(volatile const unsigned*)f.cnt) return;
     const int lane = threadIdx.x & 63;
     const long long n_regions = m.n_local;
@@ -1016,16 +1020,23 @@ __global__ __launch_bounds__(256) void k_rf_reach(DevScene sc, CamDev cam, TileM
     uint32_t nnode = 0;
     for (long long r = gw; r < n_regions; r += n_w) {
         const unsigned n = f.hcnt[r];
+        if (n == 0) continue;
         const size_t base = (size_t)r * f.rs;
+        if (GI_R_MEMO > 0) {
+            __builtin_amdgcn_wave_barrier();
+            for (int k = 0; k < GI_R_MEMO; ++k) s_memo[lane * GI_R_MEMO + k] = -1;   // lane = pixel of the tile
+            __builtin_amdgcn_wave_barrier();
+        }
         for (unsigned i = lane; i < n; i += 64) {
             const unsigned slot = f.hits[2 * (base + i)];
             const int e = (int)f.hits[2 * (base + i) + 1];
+            const RMemo memo{GI_R_MEMO > 0 ? s_memo + (slot & 63) * GI_R_MEMO : nullptr};
             const V3 d = rf_dir(f, slot);
             const int a1 = sc.app_off[e + 1];
             for (int a = sc.app_off[e]; a < a1; ++a) {
                 const long long rk = sc.app_rank[a];
                 if (rk <= (long long)*(volatile unsigned long long*)(f.best + slot) - 1) break;
-                if (r_leaf_reachable(sc, sc.app_leaf[a], cam.pos, d, nnode)) {
+                if (r_leaf_reachable(sc, sc.app_leaf[a], cam.pos, d, nnode, memo)) {
                     atomicMax(f.best + slot, (unsigned long long)(rk + 1));
                     break;
                 }
@@ -2561,8 +2572,8 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
                 if (stats) hipLaunchKernelGGL((k_rf_hit<true, false>), fgrid, block, 0, stream, sc, cam, m, f, st);
                 else hipLaunchKernelGGL((k_rf_hit<false, false>), fgrid, block, 0, stream, sc, cam, m, f, st);
             }
-            if (stats) hipLaunchKernelGGL(k_rf_reach<true>, fgrid, block, 0, stream, sc, cam, m, f, st);
-            else hipLaunchKernelGGL(k_rf_reach<false>, fgrid, block, 0, stream, sc, cam, m, f, st);
+            if (stats) hipLaunchKernelGGL(k_rf_reach<true>, dim3(4 * fgrid.x), dim3(64), 0, stream, sc, cam, m, f, st);
+            else hipLaunchKernelGGL(k_rf_reach<false>, dim3(4 * fgrid.x), dim3(64), 0, stream, sc, cam, m, f, st);
             if (sc.r_tri_only && GI_R_TRI) {
                 if (stats) hipLaunchKernelGGL((k_rf_shade<true, true>), pgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, f, st);
                 else hipLaunchKernelGGL((k_rf_shade<false, true>), pgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, f, st);
