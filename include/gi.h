@@ -105,7 +105,7 @@ typedef enum gi_mode {
 #define GI_FLAG_R_DFS 2u   /* Mode R: walk the whole reference octree in reverse DFS order instead of
                               reconstructing the candidate list (same result; A/B and tests) */
 #define GI_FLAG_TIME 4u    /* record HIP events around the frame's dominant kernel (k_mode_r / k_mode_x; the
-                              wavefront form: its whole sequence of bounce kernels) on the render's
+                              wavefront form and Mode R's flat phases: their whole sequence) on the render's
                               stream; averaged by gi_scene_kernel_ms */
 #define GI_FLAG_X_NO_SHADOW 8u   /* Mode X, test only: no shadow rays (every light is visible).  With
                                     depth 1 and spp 1 this reduces Mode X to the reference's own
