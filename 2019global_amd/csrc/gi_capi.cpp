@@ -137,7 +137,8 @@ int ensure_xscratch(gi_scene* s, int w, int h, const gi_opts* o) {
             (void)hipFree(x.rf_dir);
             (void)hipFree(x.rf_rcnt);
             (void)hipFree(x.rf_hcnt);
-            x.rf_rcnt = x.rf_hcnt = nullptr;
+            (void)hipFree(x.rf_coff);
+            x.rf_rcnt = x.rf_hcnt = x.rf_coff = nullptr;
             x.rf_pairs = nullptr;
             x.rf_best = nullptr;
             x.rf_dir = nullptr;
@@ -147,7 +148,8 @@ int ensure_xscratch(gi_scene* s, int w, int h, const gi_opts* o) {
                 (e = hipMalloc((void**)&x.rf_best, (size_t)need * sizeof(unsigned long long))) != hipSuccess ||
                 (e = hipMalloc((void**)&x.rf_dir, (size_t)need * 3 * sizeof(double))) != hipSuccess ||
                 (e = hipMalloc((void**)&x.rf_rcnt, (size_t)(need / 64) * sizeof(unsigned))) != hipSuccess ||
-                (e = hipMalloc((void**)&x.rf_hcnt, (size_t)(need / 64) * sizeof(unsigned))) != hipSuccess)
+                (e = hipMalloc((void**)&x.rf_hcnt, (size_t)(need / 64) * sizeof(unsigned))) != hipSuccess ||
+                (e = hipMalloc((void**)&x.rf_coff, (size_t)(need / 64 + 1) * sizeof(unsigned))) != hipSuccess)
                 return hip_fail(e, "hipMalloc (flat Mode R)");
             if (!x.rf_cnt && (e = hipMalloc((void**)&x.rf_cnt, 8 * sizeof(unsigned))) != hipSuccess)
                 return hip_fail(e, "hipMalloc (flat Mode R counters)");
@@ -319,6 +321,7 @@ void destroy_scene(gi_scene* s) noexcept {
     (void)hipFree(s->xs.rf_dir);
     (void)hipFree(s->xs.rf_rcnt);
     (void)hipFree(s->xs.rf_hcnt);
+    (void)hipFree(s->xs.rf_coff);
     (void)hipFree(s->xs.rf_cnt);
     (void)hipHostFree(s->xs.h_nlist);
     for (int i = 0; i < KTimer::kRing; i++) {

@@ -872,6 +872,7 @@ struct RFlat {
     unsigned* cnt;              // word 0: overflow
     unsigned* rcnt;             // per region: pairs
     unsigned* hcnt;             // per region: hitting pairs
+    unsigned* coff;             // per region: its first 64-pair chunk of hits (k_rf_scan); [n_regions]: the total
     double* dir;                // per pixel slot: its primary direction (k_rf_walk writes, the others read)
     unsigned rs;                // pairs per region
 };
@@ -1006,10 +1007,36 @@ __global__ __launch_bounds__(256) void k_rf_hit(DevScene sc, CamDev cam, TileMap
     }
     if (STATS) wave_add_stats(stats, 0, 0, nprim, 0);
 }
+// the regions' hits in chunks of 64: coff = exclusive prefix of ceil(hcnt / 64) (one workgroup)
+__global__ __launch_bounds__(1024) void k_rf_scan(TileMap m, RFlat f) {
+    if (*(volatile const unsigned*)f.cnt) return;
+    __shared__ unsigned s_part[1024];
+    const int t = threadIdx.x;
+    const long long n = m.n_local, per = (n + 1023) / 1024;
+    const long long b0 = min(n, t * per), b1 = min(n, b0 + per);
+    unsigned sum = 0;
+    for (long long r = b0; r < b1; ++r) sum += (f.hcnt[r] + 63u) / 64u;
+    s_part[t] = sum;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {   // inclusive scan of the 1024 partial sums
+        const unsigned v = t >= off ? s_part[t - off] : 0u;
+        __syncthreads();
+        s_part[t] += v;
+        __syncthreads();
+    }
+    unsigned run = t ? s_part[t - 1] : 0u;
+    for (long long r = b0; r < b1; ++r) {
+        f.coff[r] = run;
+        run += (f.hcnt[r] + 63u) / 64u;
+    }
+    if (t == 1023) f.coff[n] = s_part[1023];
+}
 // per hitting pair: its entity's latest reachable appearance that beats the pixel's best rank.
+// Persistent waves take 64-pair chunks of hits in turn (k_rf_scan's offsets; a chunk's region by a
+// binary search), so a region with many hits -- the soup core's tiles -- is shared by several waves.
 // One wave per workgroup: the wave's LDS holds the node-test memo (RMemo, GI_R_MEMO entries) of each
 // of the 64 pixels of the region (tile) it works on -- the pixel's pairs share their root paths'
-// upper levels.
+// upper levels; it restarts when the wave's next chunk is in another region.
 template <bool STATS>
 __global__ __launch_bounds__(64) void k_rf_reach(DevScene sc, CamDev cam, TileMap m, RFlat f, unsigned long long* stats) {
     __shared__ int s_memo[GI_R_MEMO > 0 ? 64 * GI_R_MEMO : 1];
@@ -1017,17 +1044,27 @@ __global__ __launch_bounds__(64) void k_rf_reach(DevScene sc, CamDev cam, TileMa
     const int lane = threadIdx.x & 63;
     const long long n_regions = m.n_local;
     const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_w = ((long long)gridDim.x * blockDim.x) >> 6;
+    const long long n_chunks = f.coff[n_regions];
     uint32_t nnode = 0;
-    for (long long r = gw; r < n_regions; r += n_w) {
+    long long cur = -1;
+    for (long long c = gw; c < n_chunks; c += n_w) {
+        long long lo = 0, hi = n_regions - 1;   // the last region whose first chunk is <= c
+        while (lo < hi) {
+            const long long mid = (lo + hi + 1) >> 1;
+            if ((long long)f.coff[mid] <= c) lo = mid;
+            else hi = mid - 1;
+        }
+        const long long r = lo;
         const unsigned n = f.hcnt[r];
-        if (n == 0) continue;
         const size_t base = (size_t)r * f.rs;
-        if (GI_R_MEMO > 0) {
+        if (GI_R_MEMO > 0 && r != cur) {
             __builtin_amdgcn_wave_barrier();
             for (int k = 0; k < GI_R_MEMO; ++k) s_memo[lane * GI_R_MEMO + k] = -1;   // lane = pixel of the tile
             __builtin_amdgcn_wave_barrier();
         }
-        for (unsigned i = lane; i < n; i += 64) {
+        cur = r;
+        const unsigned i = (unsigned)(c - (long long)f.coff[r]) * 64u + (unsigned)lane;
+        if (i < n) {
             const unsigned slot = f.hits[2 * (base + i)];
             const int e = (int)f.hits[2 * (base + i) + 1];
             const RMemo memo{GI_R_MEMO > 0 ? s_memo + (slot & 63) * GI_R_MEMO : nullptr};
@@ -2557,7 +2594,7 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
         }
         mark(ev_begin);
         if (split && env.r_par == 4 && xs.rf_pairs && xs.rf_slots >= m.n_local * (kTile * kTile)) {   // flat phases
-            const RFlat f{xs.rf_pairs, xs.rf_pairs, xs.rf_best, xs.rf_cnt, xs.rf_rcnt, xs.rf_hcnt, xs.rf_dir,
+            const RFlat f{xs.rf_pairs, xs.rf_pairs, xs.rf_best, xs.rf_cnt, xs.rf_rcnt, xs.rf_hcnt, xs.rf_coff, xs.rf_dir,
                           (unsigned)(xs.rf_cap / xs.rf_slots * 64)};
             const dim3 pgrid((unsigned)((m.n_local * (kTile * kTile) + 255) / 256)), fgrid(4096);
             hipError_t e1 = hipMemsetAsync(xs.rf_cnt, 0, sizeof(unsigned), stream);
@@ -2572,6 +2609,7 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
                 if (stats) hipLaunchKernelGGL((k_rf_hit<true, false>), fgrid, block, 0, stream, sc, cam, m, f, st);
                 else hipLaunchKernelGGL((k_rf_hit<false, false>), fgrid, block, 0, stream, sc, cam, m, f, st);
             }
+            hipLaunchKernelGGL(k_rf_scan, dim3(1), dim3(1024), 0, stream, m, f);
             if (stats) hipLaunchKernelGGL(k_rf_reach<true>, dim3(4 * fgrid.x), dim3(64), 0, stream, sc, cam, m, f, st);
             else hipLaunchKernelGGL(k_rf_reach<false>, dim3(4 * fgrid.x), dim3(64), 0, stream, sc, cam, m, f, st);
             if (sc.r_tri_only && GI_R_TRI) {

@@ -247,6 +247,7 @@ struct XScratch {
     unsigned* rf_cnt = nullptr;
     unsigned* rf_rcnt = nullptr;
     unsigned* rf_hcnt = nullptr;
+    unsigned* rf_coff = nullptr;   // per tile + 1: the first 64-hit chunk of its region (k_rf_scan)
     long long rf_cap = 0, rf_slots = 0;
 };
 
