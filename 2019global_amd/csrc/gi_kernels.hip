@@ -913,10 +913,8 @@ __global__ __launch_bounds__(256) void k_rf_walk(DevScene sc, CamDev cam, TileMa
     for (;;) {
         if (ok) {
             while (ai < sc.n_r_always && nb < GI_RF_BUF) buf[nb++] = sc.r_always[ai++];   // every ray's ImpSpheres
-            while (pcur < pend && nb < GI_RF_BUF) {
-                const int e = sc.rc_ent[pcur++];
-                if (sc.app_off[e] != sc.app_off[e + 1]) buf[nb++] = e;
-            }
+            // (every line-BVH entity appears in some leaf list: build_rcand boxes only those)
+            while (pcur < pend && nb < GI_RF_BUF) buf[nb++] = sc.rc_ent[pcur++];
             if (pcur >= pend && walking) {   // one step of the whole walk
                 const uint32_t msk = lvl_get(mlo, mhi, level);
                 const int c = __builtin_ctz(msk);
