@@ -51,15 +51,17 @@ FLAG_X_WF = 16   # Mode X: the wavefront form (one launch per bounce over compac
 FLAG_X_MEGA = 32   # Mode X: the persistent path-state kernel k_mode_x
 FLAG_X_SEG = 64   # Mode X: the segment-synchronous persistent form k_seg (no form flag: chosen per launch)
 X_FORMS = ("k_mode_x", "k_wf_bounce", "k_seg")   # gi_scene_x_form's values
+R_KERNELS = ("k_mode_r", "k_rf_walk", "k_mode_r_batch")   # gi_scene_r_kernel's (1: the flat phases)
 STAT_RAYS, STAT_NODES, STAT_PRIMS, STAT_PIXELS, STAT_X_PATH_MAX = 0, 1, 2, 3, 4
 STAT_X_ITERS, STAT_X_TRAV, STAT_X_HANDLE, STAT_X_HLANES, STAT_X_HCLOSE, STAT_X_HSHADOW = 5, 6, 7, 8, 9, 10
 STAT_X_CYC_TRAV, STAT_X_CYC_HIT, STAT_X_CYC_NEXT, STAT_X_CYC_ALL = 11, 12, 13, 14
 STAT_X_RESOLVED = 15
 STAT_X_IT_NODE, STAT_X_LN_NODE, STAT_X_IT_LEAF, STAT_X_LN_LEAF = 16, 17, 18, 19
 STAT_X_IT_RS, STAT_X_LN_RS, STAT_X_IT_ST, STAT_X_LN_ST = 20, 21, 22, 23
-STATS_N = 24
+STAT_R_PAIRS, STAT_R_OVF_TILES = 24, 25
+STATS_N = 26
 TILE = 8
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 
 class GIError(RuntimeError):
@@ -107,7 +109,7 @@ TILE_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ct
 
 EXPORTS = ["gi_abi_version", "gi_last_error", "gi_camera_init", "gi_scene_create", "gi_scene_destroy",
            "gi_scene_get_info", "gi_render", "gi_render_device", "gi_shard_tiles", "gi_unshard_device",
-           "gi_trace_ray", "gi_kat_expbox", "gi_scene_kernel_ms", "gi_scene_x_form", "gi_octree_create", "gi_octree_destroy",
+           "gi_trace_ray", "gi_kat_expbox", "gi_scene_kernel_ms", "gi_scene_x_form", "gi_scene_r_kernel", "gi_octree_create", "gi_octree_destroy",
            "gi_octree_intersect", "gi_multi_create", "gi_multi_destroy", "gi_multi_info", "gi_multi_render", "gi_device_count",
            "gi_device_list", "gi_build_id", "gi_obj_parse"]
 
@@ -147,6 +149,7 @@ def lib():
         L.gi_kat_expbox.argtypes = [i32, dp, ctypes.POINTER(ctypes.c_int32)]
         L.gi_scene_kernel_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int64)]
         L.gi_scene_x_form.argtypes = [vp, ctypes.POINTER(Opts), ctypes.POINTER(ctypes.c_int32)]
+        L.gi_scene_r_kernel.argtypes = [vp, ctypes.POINTER(Opts), ctypes.POINTER(ctypes.c_int32)]
         L.gi_octree_create.argtypes = [ctypes.POINTER(SceneDesc), ctypes.POINTER(vp)]
         L.gi_octree_destroy.argtypes = [vp]
         L.gi_octree_destroy.restype = None
@@ -491,6 +494,15 @@ class DeviceScene:
         f = ctypes.c_int32()
         _check(lib().gi_scene_x_form(self._h, ctypes.byref(o), ctypes.byref(f)), "gi_scene_x_form")
         return X_FORMS[f.value]
+
+    def r_kernel(self, flags=0) -> str:
+        """The Mode R kernel a render would run: "k_mode_r" (one lane per pixel), "k_rf_walk" (the flat
+        phases k_rf_*, their overflowed tiles by k_mode_r_batch) or "k_mode_r_batch" (the whole frame)
+        -- gi_scene_r_kernel."""
+        o = self.opts(MODE_R, 1, 1, 0, flags=flags)
+        k = ctypes.c_int32()
+        _check(lib().gi_scene_r_kernel(self._h, ctypes.byref(o), ctypes.byref(k)), "gi_scene_r_kernel")
+        return R_KERNELS[k.value]
 
     def kernel_ms(self):
         """(average ms, launches) of the dominant kernel over the renders issued with FLAG_TIME since

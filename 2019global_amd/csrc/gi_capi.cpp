@@ -24,8 +24,11 @@ long long shard_tiles(int w, int h, int shard_count);
 hipError_t x_launch_config(const DevScene& sc, int device, XLaunchCfg& cfg);
 int x_form_choice(const DevScene& sc, const XLaunchCfg& xc, const gi_opts& o);
 long long x_wf_chunk();
-int x_env_r_par();
 int x_env_rf_per_slot();
+int r_kernel_choice(const DevScene& sc, const gi_opts& o);
+unsigned rf_own_pairs();
+unsigned rf_page_pairs();
+unsigned rf_max_pages();
 hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev& cam, V3 light, int w, int h, int y0,
                          const gi_opts& o, double* rgb, uint8_t* rgb8, const XScratch& xs, KTimer* kt,
                          hipStream_t stream);
@@ -111,50 +114,55 @@ hipError_t upload(gi_scene* s, const std::vector<T>& v, const T** out) {
     return hipSuccess;
 }
 
+void free_rflat(XScratch& x) {
+    for (void* p : {(void*)x.rf_pairs, (void*)x.rf_pt, (void*)x.rf_best, (void*)x.rf_dir, (void*)x.rf_cnt, (void*)x.rf_ovf,
+                    (void*)x.rf_rcnt, (void*)x.rf_hcnt, (void*)x.rf_coff})
+        (void)hipFree(p);
+    x.rf_pairs = x.rf_pt = x.rf_cnt = x.rf_ovf = x.rf_rcnt = x.rf_hcnt = x.rf_coff = nullptr;
+    x.rf_best = nullptr;
+    x.rf_dir = nullptr;
+    x.rf_pages = 0;
+    x.rf_slots = 0;
+    x.rf_bytes = 0;
+}
+
 // Mode X work buffers for a frame of w x h pixels cut into this call's shard (k_x_classify's list,
 // k_mode_x's per-sample radiance for spp > 1); grown, never shrunk.  hipFree synchronises with
 // work still using them.
 int ensure_xscratch(gi_scene* s, int w, int h, const gi_opts* o) {
     const long long need = shard_tiles(w, h, o->shard_count) * GI_TILE * GI_TILE;
     hipError_t e;
-    if (o->mode == GI_MODE_R) {   // the heavy-pixel list of k_mode_r_split (every pixel slot at most;
-                                  // large scenes only: without the list the split kernel has no budget)
+    if (o->mode == GI_MODE_R) {
+        // the flat Mode R phases' buffers, only when this launch runs them (r_kernel_choice == 1).
+        // Pairs are one word: per tile its own GI_RF_S0 (8 per pixel slot), plus a shared pool of
+        // GI_RF_PER_SLOT (16) per pixel slot in pages; with the per-slot directions and best ranks a
+        // 1080p frame takes 0.28 GB (R-C4 writes 5.0 M pairs: 20 MB).  A tile whose candidates do not
+        // fit is rendered by k_mode_r_batch; if the buffers cannot be had at all, the whole frame is.
         XScratch& x = s->xs;
-        if (s->dev.n_ents > 4096 && x.rcap < need) {
-            (void)hipFree(x.rheavy);
-            x.rheavy = nullptr;
-            x.rcap = 0;
-            if ((e = hipMalloc((void**)&x.rheavy, (size_t)need * 2 * sizeof(long long))) != hipSuccess)
-                return hip_fail(e, "hipMalloc (heavy-pixel list)");
-            x.rcap = need;
-        }
-        // the flat Mode R pipeline's buffers (GI_R_PAR=4): 128 candidate pairs per pixel slot of a
-        // tile's region (GI_RF_PER_SLOT; 1 GB per 1080p frame); a tile with more makes the frame fall
-        // back to k_mode_r_batch on the device (the overflow word)
-        if (s->dev.n_ents > 4096 && x_env_r_par() == 4 && x.rf_slots < need) {
-            (void)hipFree(x.rf_pairs);
-            (void)hipFree(x.rf_best);
-            (void)hipFree(x.rf_dir);
-            (void)hipFree(x.rf_rcnt);
-            (void)hipFree(x.rf_hcnt);
-            (void)hipFree(x.rf_coff);
-            x.rf_rcnt = x.rf_hcnt = x.rf_coff = nullptr;
-            x.rf_pairs = nullptr;
-            x.rf_best = nullptr;
-            x.rf_dir = nullptr;
-            x.rf_cap = x.rf_slots = 0;
-            const long long cap = (long long)x_env_rf_per_slot() * need;
-            if ((e = hipMalloc((void**)&x.rf_pairs, (size_t)cap * 2 * sizeof(unsigned))) != hipSuccess ||
-                (e = hipMalloc((void**)&x.rf_best, (size_t)need * sizeof(unsigned long long))) != hipSuccess ||
-                (e = hipMalloc((void**)&x.rf_dir, (size_t)need * 3 * sizeof(double))) != hipSuccess ||
-                (e = hipMalloc((void**)&x.rf_rcnt, (size_t)(need / 64) * sizeof(unsigned))) != hipSuccess ||
-                (e = hipMalloc((void**)&x.rf_hcnt, (size_t)(need / 64) * sizeof(unsigned))) != hipSuccess ||
-                (e = hipMalloc((void**)&x.rf_coff, (size_t)(need / 64 + 1) * sizeof(unsigned))) != hipSuccess)
-                return hip_fail(e, "hipMalloc (flat Mode R)");
-            if (!x.rf_cnt && (e = hipMalloc((void**)&x.rf_cnt, 8 * sizeof(unsigned))) != hipSuccess)
-                return hip_fail(e, "hipMalloc (flat Mode R counters)");
-            x.rf_cap = cap;
+        if (r_kernel_choice(s->dev, *o) == 1 && x.rf_slots < need) {
+            free_rflat(x);
+            const long long tiles = need / 64;
+            const long long pages = (long long)x_env_rf_per_slot() * need / (long long)rf_page_pairs();
+            const size_t pairs = (size_t)tiles * rf_own_pairs() + (size_t)pages * rf_page_pairs();
+            const bool ok =
+                hipMalloc((void**)&x.rf_pairs, pairs * sizeof(unsigned)) == hipSuccess &&
+                hipMalloc((void**)&x.rf_pt, (size_t)tiles * rf_max_pages() * sizeof(unsigned)) == hipSuccess &&
+                hipMalloc((void**)&x.rf_best, (size_t)need * sizeof(unsigned long long)) == hipSuccess &&
+                hipMalloc((void**)&x.rf_dir, (size_t)need * 3 * sizeof(double)) == hipSuccess &&
+                hipMalloc((void**)&x.rf_cnt, 8 * sizeof(unsigned)) == hipSuccess &&
+                hipMalloc((void**)&x.rf_ovf, (size_t)tiles * sizeof(unsigned)) == hipSuccess &&
+                hipMalloc((void**)&x.rf_rcnt, (size_t)tiles * sizeof(unsigned)) == hipSuccess &&
+                hipMalloc((void**)&x.rf_hcnt, (size_t)tiles * sizeof(unsigned)) == hipSuccess &&
+                hipMalloc((void**)&x.rf_coff, (size_t)(tiles + 1) * sizeof(unsigned)) == hipSuccess;
+            if (!ok) {
+                (void)hipGetLastError();   // (clears the sticky allocation error) -- rendered by k_mode_r_batch
+                free_rflat(x);
+                return GI_OK;
+            }
+            x.rf_pages = (unsigned)pages;
             x.rf_slots = need;
+            x.rf_bytes = pairs * sizeof(unsigned) + (size_t)tiles * (rf_max_pages() + 4) * sizeof(unsigned) +
+                         (size_t)need * (sizeof(unsigned long long) + 3 * sizeof(double));
         }
         return GI_OK;
     }
@@ -315,14 +323,7 @@ void destroy_scene(gi_scene* s) noexcept {
         (void)hipFree(s->xs.wid[q]);
     }
     (void)hipFree(s->xs.wcnt);
-    (void)hipFree(s->xs.rheavy);
-    (void)hipFree(s->xs.rf_pairs);
-    (void)hipFree(s->xs.rf_best);
-    (void)hipFree(s->xs.rf_dir);
-    (void)hipFree(s->xs.rf_rcnt);
-    (void)hipFree(s->xs.rf_hcnt);
-    (void)hipFree(s->xs.rf_coff);
-    (void)hipFree(s->xs.rf_cnt);
+    free_rflat(s->xs);
     (void)hipHostFree(s->xs.h_nlist);
     for (int i = 0; i < KTimer::kRing; i++) {
         if (s->kt.ev0[i]) (void)hipEventDestroy(static_cast<hipEvent_t>(s->kt.ev0[i]));
@@ -698,6 +699,15 @@ int gi_scene_x_form(gi_scene* s, const gi_opts* o, int32_t* form) {
         if (!s || !o || !form) return fail(GI_ERR_ARG, "null argument");
         std::lock_guard<std::mutex> lk(s->mu);
         *form = x_form_choice(s->dev, s->xcfg, *o);
+        return GI_OK;
+    });
+}
+
+int gi_scene_r_kernel(gi_scene* s, const gi_opts* o, int32_t* kernel) {
+    return guard([&]() -> int {
+        if (!s || !o || !kernel) return fail(GI_ERR_ARG, "null argument");
+        std::lock_guard<std::mutex> lk(s->mu);
+        *kernel = r_kernel_choice(s->dev, *o);
         return GI_OK;
     });
 }

@@ -284,12 +284,10 @@ __device__ __forceinline__ uint32_t children_mask_line(const XWNode* nd, F3 of, 
 }
 
 // The same 8 tests spread over the NSUB (>= 8) lanes of a pixel group that walk one line
-// (k_mode_r_split): lane sub tests child sub & 7 only -- its six bounds are one float each, and the
-// group's 8 lanes read 8 consecutive floats of each plane array -- and a ballot gathers the mask, the
-// same in every lane.  Per child the arithmetic is children_mask_line's, so the mask is identical.
-#ifndef GI_R_COOP
-#define GI_R_COOP 1   // cooperative line-BVH node tests in k_mode_r_split / k_mode_r_heavy
-#endif
+// (k_mode_r_batch's top two levels): lane sub tests child sub & 7 only -- its six bounds are one float
+// each, and the group's 8 lanes read 8 consecutive floats of each plane array -- and a ballot gathers
+// the mask, the same in every lane.  Per child the arithmetic is children_mask_line's, so the mask is
+// identical.
 template <int NSUB>
 __device__ __forceinline__ uint32_t children_mask_line_coop(const XWNode* nd, F3 of, F3 ivf, float tau, int sub) {
     const int c = sub & 7;
@@ -306,7 +304,7 @@ __device__ __forceinline__ uint32_t children_mask_line_coop(const XWNode* nd, F3
     return (uint32_t)((b >> base) & 0xFFull);
 }
 
-// Per-ray memo of node-test results (k_mode_r_split): the candidates' root paths share their upper
+// Per-ray memo of node-test results (k_mode_r_batch, k_rf_reach): the candidates' root paths share their upper
 // levels -- every path starts at the root -- and an exact ExpBox node test is ~12 fp32/fp64 triangle
 // solves, so a ray that walks many appearances' paths would repeat the same tests.  Direct-mapped,
 // RMEMO entries per ray in LDS, shared by the NSUB lanes of the pixel (one ray, so a result found
@@ -410,20 +408,13 @@ __device__ __forceinline__ void trace_mode_r_cand(const DevScene& sc, V3 o, V3 d
     }
 }
 
-// Mode R with a pixel's candidates split over NSUB lanes (large scenes).  The frame time of
-// k_mode_r on the 100k soup is a few pixels' serial work -- their lines cross ~100 entity boxes,
-// and a single 8x8 tile of them takes 5-6 ms alone on the GPU -- so here NSUB adjacent lanes take
-// one pixel: all of them walk the pixel's line BVH and make the same decisions, and the k-th
-// candidate met is considered by lane k mod NSUB only.  The walk depends on what was found only
-// through the rank pruning (rc_maxkey <= best), and it prunes only on the GROUP-maximised best
-// rank: group_max runs after the r_always candidates and after every leaf, and best changes nowhere
-// else between two pruning checks, so every lane of the group holds the same best at every check
-// and the lanes stay in step (the group shuffles rely on it).  At the end the lane holding the
-// highest rank -- the reference's last hitting reachable candidate, A.1; every candidate is
-// considered by exactly one lane, so the maximum is the same -- shades the pixel.
-#ifndef GI_R_NSUB
-#define GI_R_NSUB 8   // lanes per pixel in k_mode_r_split (a power of two <= 32)
-#endif
+// Mode R for large scenes (more than 4096 entities).  A one-lane-per-pixel walk (k_mode_r) spends
+// the 100k soup's frame on a few pixels' serial work -- their lines cross ~100 entity boxes -- so
+// these scenes run the flat phases below (k_rf_*), chip-wide and dense, and k_mode_r_batch renders
+// the tiles whose candidates do not fit the flat phases' buffers.  Both answer as trace_mode_r_cand:
+// the hitting candidate of highest reachable list rank (A.1), bit for bit.
+
+// maximum over the NSUB lanes of a pixel group
 template <int NSUB>
 __device__ __forceinline__ long long group_max(long long v) {
 #pragma unroll
@@ -433,74 +424,11 @@ __device__ __forceinline__ long long group_max(long long v) {
     }
     return v;
 }
-// best0: the pruning bound to start from (-1: none; the heavy-pixel pass restarts a pixel from the
-// rank its first pass had found, minus one, so that candidate is met again).  budget > 0: the walk
-// gives up (returns true, with best = the group's best so far) once the group has met more than
-// `budget` candidates -- decided after a leaf, where every lane holds the same count and best.
-template <int NSUB, bool TRI>
-__device__ __forceinline__ bool trace_mode_r_split(const DevScene& sc, V3 o, V3 d, float tau, int sub, RResult& r,
-                                                   long long& mine, uint32_t& nnode, uint32_t& nprim, RMemo memo,
-                                                   long long& best, unsigned budget) {
-    r.ent = -1;
-    mine = -1;
-    // best: the group's best rank so far (pruning bound)
-    unsigned k = 0;        // candidates met so far (the same count in every lane of the group)
-    auto consider = [&](int e) {
-        if ((int)(k++ % NSUB) != sub) return;
-        const long long before = best;
-        r_consider<TRI>(sc, e, o, d, best, r, nnode, nprim, memo);
-        if (best != before) mine = best;
-    };
-    for (int i = 0; i < sc.n_r_always; ++i) consider(sc.r_always[i]);
-    best = group_max<NSUB>(best);
-    const XWNode* W = sc.rc_nodes;
-    const F3 of = f3((float)o.x, (float)o.y, (float)o.z);
-    const F3 ivf = inv_dir(d);   // clamped to +-1e30: finite plane distances, near / far by sign
-    uint64_t mlo = 0, mhi = 0;
-    int node = 0, level = 0;
-    constexpr bool COOP = GI_R_COOP != 0 && NSUB >= 8;
-    const uint32_t rm = COOP ? children_mask_line_coop<NSUB>(W, of, ivf, tau, sub) : children_mask_line(W, of, ivf, tau);
-    lvl_set(mlo, mhi, 0, rm);
-    bool going = rm != 0;
-    while (going) {
-        const uint32_t msk = lvl_get(mlo, mhi, level);
-        const int c = __builtin_ctz(msk);
-        lvl_set(mlo, mhi, level, msk & (msk - 1));
-        const XWNode* nd = W + node;
-        const int ch = nd->child[c];
-        // rank order (gi_bvh.cpp build_rcand): a slot whose highest rank is <= the group's best --
-        // the same value in all NSUB lanes here -- and its later siblings hold no better candidate
-        if (sc.rc_maxkey[node * 8 + c] <= best) {
-            lvl_set(mlo, mhi, level, 0);
-        } else if (ch < 0) {
-            const int cnt = nd->cnt[c];
-            for (int j = 0; j < cnt; ++j) consider(sc.rc_ent[~ch + j]);
-            best = group_max<NSUB>(best);
-            if (budget && k > budget) return true;
-        } else {
-            const uint32_t cm = COOP ? children_mask_line_coop<NSUB>(W + ch, of, ivf, tau, sub)
-                                     : children_mask_line(W + ch, of, ivf, tau);
-            if (cm) {
-                node = ch;
-                ++level;
-                lvl_set(mlo, mhi, level, cm);
-            }
-        }
-        uint32_t rest = lvl_get(mlo, mhi, level);
-        while (rest == 0 && level > 0) {
-            --level;
-            node = level == 0 ? 0 : W[node].parent;
-            rest = lvl_get(mlo, mhi, level);
-        }
-        going = rest != 0;
-    }
-    return false;
-}
 
-// the pixel from a group's walk: the lowest sub-lane holding the group's highest rank (ranks are
+// the pixel from a group's candidates: the lowest sub-lane holding the group's highest rank (ranks are
 // unique: one lane at most) shades it; none: black
 template <int NSUB, bool TRI>
-__device__ __forceinline__ void r_split_write(const DevScene& sc, V3 d, V3 light, const RResult& r, long long mine,
+__device__ __forceinline__ void r_group_write(const DevScene& sc, V3 d, V3 light, const RResult& r, long long mine,
                                               int sub, long long idx, double* rgb, uint8_t* rgb8) {
     const long long gmax = group_max<NSUB>(mine);
     const unsigned long long m_win = __ballot(mine == gmax);
@@ -521,73 +449,16 @@ __device__ __forceinline__ void r_split_write(const DevScene& sc, V3 d, V3 light
     }
 }
 
-// Mode R with the line-BVH WALK itself split over a pixel's 8 lanes (GI_R_PAR; k_mode_r_par).  The
-// heavy-pixel experiments show a slow pixel's time is its serial walk -- a chain of dependent node
-// loads that k_mode_r_split's 8 lanes all repeat -- so here the group walks the top two levels
-// together (cooperative node tests) and lists the hit nodes / leaves below them in rank order (at
-// most 64 items); item i is then walked by lane i mod 8 alone (its own stackless walk of that
-// subtree).  Pruning: every lane reads the group's best rank from LDS before each slot (ranks only
-// rise, and only ranks of hitting reachable candidates are posted), so a slot whose bound is <= it
-// holds no better candidate; each candidate is considered by the one lane walking its leaf.  The
-// answer -- the highest reachable hitting rank, shaded by the lane holding it -- is the same.
-#ifndef GI_R_PAR
-// Mode R large scenes: 1 k_mode_r_par instead of k_mode_r_split (R-C4 5.47 -> 4.41 ms, R-C3 equal),
-// 2 k_mode_r_batch (3.19 ms), 4 the flat phases k_rf_* (2.58 ms)
-#define GI_R_PAR 4
-#endif
-#ifndef GI_R_PAR_DYN
-#define GI_R_PAR_DYN 1   // k_mode_r_par: items taken from a per-group LDS counter (0: item i by lane i mod 8)
-#endif
-#ifndef GI_R_MIN_WAVES
-#define GI_R_MIN_WAVES 1   // minimum waves per SIMD asked of the register allocator (Mode R kernels)
-#endif
+// a candidate considered by one lane of the group: on a better reachable hit, the group's best rank
+// (LDS, atomic max) is raised
 template <bool TRI>
-__device__ __forceinline__ void r_par_consider(const DevScene& sc, int e, V3 o, V3 d, unsigned long long* gb, long long& best,
-                                               long long& mine, RResult& r, uint32_t& nnode, uint32_t& nprim, RMemo memo) {
+__device__ __forceinline__ void r_group_consider(const DevScene& sc, int e, V3 o, V3 d, unsigned long long* gb, long long& best,
+                                                 long long& mine, RResult& r, uint32_t& nnode, uint32_t& nprim, RMemo memo) {
     const long long before = best;
     r_consider<TRI>(sc, e, o, d, best, r, nnode, nprim, memo);
     if (best != before) {
         mine = best;
         atomicMax(gb, (unsigned long long)(best + 1));
-    }
-}
-// one lane's walk of the subtree below wide node `root` (its hit children m0), leaves considered
-template <bool TRI>
-__device__ __forceinline__ void r_par_walk(const DevScene& sc, int root, uint32_t m0, F3 of, F3 ivf, float tau, V3 o, V3 d,
-                                           unsigned long long* gb, long long& best, long long& mine, RResult& r,
-                                           uint32_t& nnode, uint32_t& nprim, RMemo memo) {
-    const XWNode* W = sc.rc_nodes;
-    uint64_t mlo = 0, mhi = 0;
-    int node = root, level = 0;
-    lvl_set(mlo, mhi, 0, m0);
-    bool going = m0 != 0;
-    while (going) {
-        const uint32_t msk = lvl_get(mlo, mhi, level);
-        const int c = __builtin_ctz(msk);
-        lvl_set(mlo, mhi, level, msk & (msk - 1));
-        const XWNode* nd = W + node;
-        const int ch = nd->child[c];
-        best = max(best, (long long)*(volatile unsigned long long*)gb - 1);   // the group's best so far
-        if (sc.rc_maxkey[node * 8 + c] <= best) {
-            lvl_set(mlo, mhi, level, 0);
-        } else if (ch < 0) {
-            const int cnt = nd->cnt[c];
-            for (int j = 0; j < cnt; ++j) r_par_consider<TRI>(sc, sc.rc_ent[~ch + j], o, d, gb, best, mine, r, nnode, nprim, memo);
-        } else {
-            const uint32_t cm = children_mask_line(W + ch, of, ivf, tau);
-            if (cm) {
-                node = ch;
-                ++level;
-                lvl_set(mlo, mhi, level, cm);
-            }
-        }
-        uint32_t rest = lvl_get(mlo, mhi, level);
-        while (rest == 0 && level > 0) {
-            --level;
-            node = level == 0 ? root : W[node].parent;
-            rest = lvl_get(mlo, mhi, level);
-        }
-        going = rest != 0;
     }
 }
 // the items of a pixel's walk: the root's hit slots, an interior one replaced by its own hit slots
@@ -616,85 +487,17 @@ __device__ __forceinline__ int r_items(const XWNode* W, F3 of, F3 ivf, float tau
     __builtin_amdgcn_wave_barrier();
     return n;
 }
-template <bool STATS, bool TRI>
-__global__ __launch_bounds__(256, GI_R_MIN_WAVES) void k_mode_r_par(DevScene sc, CamDev cam, V3 light, TileMap m, double* rgb,
-                                                     uint8_t* rgb8, unsigned long long* stats, float tau) {
-    constexpr int NSUB = 8;
-    const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    const long long ps = g / NSUB;
-    const int sub = (int)(g % NSUB), grp = threadIdx.x / NSUB;
-    __shared__ int s_memo[GI_R_MEMO > 0 ? (256 / NSUB) * GI_R_MEMO : 1];
-    __shared__ unsigned long long s_best[256 / NSUB];   // the group's best rank + 1 (0: none)
-    __shared__ int s_item[256 / NSUB][64];              // (node << 3) | slot, in rank order
-    RMemo memo{GI_R_MEMO > 0 ? s_memo + grp * GI_R_MEMO : nullptr};
-    if (GI_R_MEMO > 0)
-        for (int k = sub; k < GI_R_MEMO; k += NSUB) memo.e[k] = -1;
-    __shared__ unsigned s_next[256 / NSUB];             // GI_R_PAR_DYN: the group's next item
-    if (sub == 0) {
-        s_best[grp] = 0ull;
-        s_next[grp] = 0u;
-    }
-    __builtin_amdgcn_wave_barrier();
-    const long long lt = ps >> 6;
-    long long idx = -1;
-    int x = 0, y = 0;
-    const bool ok = lt < m.n_local && slot_pixel(m, lt, (int)(ps & 63), idx, x, y);
-    y += m.y0;
-    uint32_t nnode = 0, nprim = 0;
-    if (ok) {
-        const V3 o = cam.pos;
-        const V3 d = normalize(primary_dir(cam, (double)x, (double)y));
-        unsigned long long* gb = s_best + grp;
-        RResult r;
-        r.ent = -1;
-        long long best = -1, mine = -1;
-        for (int i = sub; i < sc.n_r_always; i += NSUB) r_par_consider<TRI>(sc, sc.r_always[i], o, d, gb, best, mine, r, nnode, nprim, memo);
-        const XWNode* W = sc.rc_nodes;
-        const F3 of = f3((float)o.x, (float)o.y, (float)o.z);
-        const F3 ivf = inv_dir(d);
-        const int n = r_items<NSUB>(W, of, ivf, tau, sub, s_item[grp]);
-#if GI_R_PAR_DYN
-        // items handed out in rank order from the group's LDS counter: a lane that finishes a short
-        // walk takes the next item instead of waiting behind a long one of its own
-        for (;;) {
-            const int i = (int)atomicAdd(s_next + grp, 1u);
-            if (i >= n) break;
-#else
-        for (int i = sub; i < n; i += NSUB) {   // lane sub walks items sub, sub + 8, ...
-#endif
-            const int it = s_item[grp][i];
-            const int node = it >> 3, c = it & 7;
-            best = max(best, (long long)*(volatile unsigned long long*)gb - 1);
-            if (sc.rc_maxkey[node * 8 + c] <= best) continue;
-            const int ch = W[node].child[c];
-            if (ch < 0) {
-                const int cnt = W[node].cnt[c];
-                for (int j = 0; j < cnt; ++j) r_par_consider<TRI>(sc, sc.rc_ent[~ch + j], o, d, gb, best, mine, r, nnode, nprim, memo);
-            } else {
-                const uint32_t cm = children_mask_line(W + ch, of, ivf, tau);
-                r_par_walk<TRI>(sc, ch, cm, of, ivf, tau, o, d, gb, best, mine, r, nnode, nprim, memo);
-            }
-        }
-        r_split_write<NSUB, TRI>(sc, d, light, r, mine, sub, idx, rgb, rgb8);
-    } else if (sub == 0 && idx >= 0 && m.shard_count > 1) {   // padding slot of a packed tile
-        if (rgb) { rgb[3 * idx] = 0; rgb[3 * idx + 1] = 0; rgb[3 * idx + 2] = 0; }
-        if (rgb8) { rgb8[3 * idx] = 0; rgb8[3 * idx + 1] = 0; rgb8[3 * idx + 2] = 0; }
-    }
-    if (STATS) {
-        const bool px = ok && sub == 0;
-        wave_add_stats(stats, px ? 1 : 0, nnode, nprim, px ? 1 : 0);
-    }
-}
 
-// Mode R in rounds (GI_R_PAR=2; k_mode_r_batch).  k_mode_r_par's lanes run a candidate's exact tests
-// (ent_hit, the reachability node tests: fp64, ~55% of its VALU instructions) in the middle of their
-// own walks, so each test runs with the few lanes whose walks are at a leaf just then (VALU lane
-// utilisation 0.09 on R-C4).  Here every lane of the wave alternates two phases: a walk phase of at
-// most GI_R_BATCH_STEPS node steps, which only queues the entities of the leaves it meets (those
-// whose highest rank beats the group's best) in the lane's own LDS segment, and a test phase in which
-// the pixel's 8 lanes share the group's queued candidates (compacted, then candidate j by lane j mod
-// 8) -- the tests of all 8 pixels of the wave in one dense block.  Pruning and the answer are
-// k_mode_r_par's: the highest reachable hitting rank, every candidate considered by one lane.
+// Mode R in rounds, 8 lanes per pixel (k_mode_r_batch; the flat phases' fallback).  The group walks
+// the line BVH's top two levels together into <= 64 items in rank order; every lane then alternates a
+// walk phase of at most GI_R_BATCH_STEPS node steps over the items it takes from the group's LDS
+// counter, which only queues the entities of the leaves it meets (those whose highest rank beats the
+// group's best) in the lane's LDS segment, and a test phase in which the pixel's 8 lanes share the
+// group's queued candidates (compacted, candidate j by lane j mod 8) -- the exact tests of a wave's 8
+// pixels in one dense block.  Pruning only skips slots whose bound is <= a rank found, and every
+// candidate is considered by one lane, so the answer is the highest reachable hitting rank.
+// Work items are 32 pixel slots (one per 8-lane group of the workgroup): the whole frame
+// (tiles == nullptr) or both halves of each of the *n_tiles listed tiles.
 #ifndef GI_R_BATCH_STEPS
 #define GI_R_BATCH_STEPS 16   // node steps a lane's walk takes per round (R-C4: 2 4.04, 4 3.56, 8 3.41,
                              // 16 3.19, 32 3.33 ms)
@@ -703,15 +506,11 @@ __global__ __launch_bounds__(256, GI_R_MIN_WAVES) void k_mode_r_par(DevScene sc,
 #define GI_R_BATCH_SEG 8     // candidates a lane queues per round (4 and 16: equal or slower)
 #endif
 template <bool STATS, bool TRI>
-__global__ __launch_bounds__(256, GI_R_MIN_WAVES) void k_mode_r_batch(DevScene sc, CamDev cam, V3 light, TileMap m, double* rgb,
-                                                       uint8_t* rgb8, unsigned long long* stats, float tau,
-                                                       const unsigned* only_if) {
-    // only_if: the flat pipeline's counters -- run only when its candidate list overflowed
-    if (only_if && *(volatile const unsigned*)only_if == 0) return;
+__global__ __launch_bounds__(256) void k_mode_r_batch(DevScene sc, CamDev cam, V3 light, TileMap m, double* rgb,
+                                                      uint8_t* rgb8, unsigned long long* stats, float tau,
+                                                      const unsigned* tiles, const unsigned* n_tiles) {
     constexpr int NSUB = 8, SEG = GI_R_BATCH_SEG;   // lanes per pixel; queued candidates per lane and round
-    const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    const long long ps = g / NSUB;
-    const int sub = (int)(g % NSUB), grp = threadIdx.x / NSUB;
+    const int sub = (int)(threadIdx.x % NSUB), grp = threadIdx.x / NSUB;
     __shared__ int s_memo[GI_R_MEMO > 0 ? (256 / NSUB) * GI_R_MEMO : 1];
     __shared__ unsigned long long s_best[256 / NSUB];   // the group's best rank + 1 (0: none)
     __shared__ int s_item[256 / NSUB][64];              // (node << 3) | slot, in rank order
@@ -719,175 +518,200 @@ __global__ __launch_bounds__(256, GI_R_MIN_WAVES) void k_mode_r_batch(DevScene s
     __shared__ int s_seg[256 / NSUB][NSUB * SEG];       // each lane's queued candidates (SEG slots)
     __shared__ int s_cand[256 / NSUB][NSUB * SEG];      // the group's candidates of the round, compacted
     RMemo memo{GI_R_MEMO > 0 ? s_memo + grp * GI_R_MEMO : nullptr};
-    if (GI_R_MEMO > 0)
-        for (int k = sub; k < GI_R_MEMO; k += NSUB) memo.e[k] = -1;
-    if (sub == 0) {
-        s_best[grp] = 0ull;
-        s_next[grp] = 0u;
-    }
-    __builtin_amdgcn_wave_barrier();
-    const long long lt = ps >> 6;
-    long long idx = -1;
-    int x = 0, y = 0;
-    const bool ok = lt < m.n_local && slot_pixel(m, lt, (int)(ps & 63), idx, x, y);
-    y += m.y0;
-    uint32_t nnode = 0, nprim = 0;
-    if (ok) {
-        const V3 o = cam.pos;
-        const V3 d = normalize(primary_dir(cam, (double)x, (double)y));
-        unsigned long long* gb = s_best + grp;
-        RResult r;
-        r.ent = -1;
-        long long best = -1, mine = -1;
-        for (int i = sub; i < sc.n_r_always; i += NSUB) r_par_consider<TRI>(sc, sc.r_always[i], o, d, gb, best, mine, r, nnode, nprim, memo);
-        const XWNode* W = sc.rc_nodes;
-        const F3 of = f3((float)o.x, (float)o.y, (float)o.z);
-        const F3 ivf = inv_dir(d);
-        const int n = r_items<NSUB>(W, of, ivf, tau, sub, s_item[grp]);
-        int* seg = s_seg[grp] + sub * SEG;
-        int* cand = s_cand[grp];
-        // the lane's walk: (root, node, level, masks) while walking; a leaf's entities [pcur, pend)
-        // still to queue; done once the group's items are all taken
-        bool walking = false, done = false;
-        int root = 0, node = 0, level = 0, pcur = 0, pend = 0;
-        uint64_t mlo = 0, mhi = 0;
-        for (;;) {
-            // ---- walk phase: queue up to SEG candidates within GI_R_BATCH_STEPS node steps
-            int nq = 0, steps = 0;
-            while (nq < SEG) {
-                best = max(best, (long long)*(volatile unsigned long long*)gb - 1);
-                if (pcur < pend) {   // the current leaf's entities: those that can still win
-                    const int e = sc.rc_ent[pcur++];
-                    const int a0 = sc.app_off[e];
-                    if (a0 != sc.app_off[e + 1] && sc.app_rank[a0] > best) seg[nq++] = e;
-                    continue;
-                }
-                if (steps >= GI_R_BATCH_STEPS || done) break;
-                ++steps;
-                if (!walking) {      // the group's next item
-                    const int i = (int)atomicAdd(s_next + grp, 1u);
-                    if (i >= n) {
-                        done = true;
-                        break;
+    const long long n_items = tiles ? 2ll * (long long)*n_tiles : (m.n_local * (kTile * kTile) + 31) / 32;
+    uint32_t nnode = 0, nprim = 0, npx = 0;
+    for (long long item = blockIdx.x; item < n_items; item += gridDim.x) {   // uniform over the workgroup
+        const long long ps = (tiles ? (long long)tiles[item >> 1] * 64 + (item & 1) * 32 : item * 32) + grp;
+        if (GI_R_MEMO > 0)
+            for (int k = sub; k < GI_R_MEMO; k += NSUB) memo.e[k] = -1;
+        if (sub == 0) {
+            s_best[grp] = 0ull;
+            s_next[grp] = 0u;
+        }
+        __builtin_amdgcn_wave_barrier();
+        const long long lt = ps >> 6;
+        long long idx = -1;
+        int x = 0, y = 0;
+        const bool ok = lt < m.n_local && slot_pixel(m, lt, (int)(ps & 63), idx, x, y);
+        y += m.y0;
+        if (ok) {
+            if (sub == 0) ++npx;
+            const V3 o = cam.pos;
+            const V3 d = normalize(primary_dir(cam, (double)x, (double)y));
+            unsigned long long* gb = s_best + grp;
+            RResult r;
+            r.ent = -1;
+            long long best = -1, mine = -1;
+            for (int i = sub; i < sc.n_r_always; i += NSUB) r_group_consider<TRI>(sc, sc.r_always[i], o, d, gb, best, mine, r, nnode, nprim, memo);
+            const XWNode* W = sc.rc_nodes;
+            const F3 of = f3((float)o.x, (float)o.y, (float)o.z);
+            const F3 ivf = inv_dir(d);
+            const int n = r_items<NSUB>(W, of, ivf, tau, sub, s_item[grp]);
+            int* seg = s_seg[grp] + sub * SEG;
+            int* cand = s_cand[grp];
+            // the lane's walk: (root, node, level, masks) while walking; a leaf's entities [pcur, pend)
+            // still to queue; done once the group's items are all taken
+            bool walking = false, done = false;
+            int root = 0, node = 0, level = 0, pcur = 0, pend = 0;
+            uint64_t mlo = 0, mhi = 0;
+            for (;;) {
+                // ---- walk phase: queue up to SEG candidates within GI_R_BATCH_STEPS node steps
+                int nq = 0, steps = 0;
+                while (nq < SEG) {
+                    best = max(best, (long long)*(volatile unsigned long long*)gb - 1);
+                    if (pcur < pend) {   // the current leaf's entities: those that can still win
+                        const int e = sc.rc_ent[pcur++];
+                        const int a0 = sc.app_off[e];
+                        if (a0 != sc.app_off[e + 1] && sc.app_rank[a0] > best) seg[nq++] = e;
+                        continue;
                     }
-                    const int it = s_item[grp][i];
-                    const int in = it >> 3, ic = it & 7;
-                    if (sc.rc_maxkey[in * 8 + ic] <= best) continue;
-                    const int ch = W[in].child[ic];
-                    if (ch < 0) {
+                    if (steps >= GI_R_BATCH_STEPS || done) break;
+                    ++steps;
+                    if (!walking) {      // the group's next item
+                        const int i = (int)atomicAdd(s_next + grp, 1u);
+                        if (i >= n) {
+                            done = true;
+                            break;
+                        }
+                        const int it = s_item[grp][i];
+                        const int in = it >> 3, ic = it & 7;
+                        if (sc.rc_maxkey[in * 8 + ic] <= best) continue;
+                        const int ch = W[in].child[ic];
+                        if (ch < 0) {
+                            pcur = ~ch;
+                            pend = ~ch + W[in].cnt[ic];
+                        } else {
+                            ++nnode;
+                            const uint32_t cm = children_mask_line(W + ch, of, ivf, tau);
+                            if (cm) {
+                                root = node = ch;
+                                level = 0;
+                                mlo = mhi = 0;
+                                lvl_set(mlo, mhi, 0, cm);
+                                walking = true;
+                            }
+                        }
+                        continue;
+                    }
+                    // one step of the item's subtree walk (stackless, rank order)
+                    const uint32_t msk = lvl_get(mlo, mhi, level);
+                    const int c = __builtin_ctz(msk);
+                    lvl_set(mlo, mhi, level, msk & (msk - 1));
+                    const XWNode* nd = W + node;
+                    const int ch = nd->child[c];
+                    if (sc.rc_maxkey[node * 8 + c] <= best) {
+                        lvl_set(mlo, mhi, level, 0);
+                    } else if (ch < 0) {
                         pcur = ~ch;
-                        pend = ~ch + W[in].cnt[ic];
+                        pend = ~ch + nd->cnt[c];
                     } else {
                         ++nnode;
                         const uint32_t cm = children_mask_line(W + ch, of, ivf, tau);
                         if (cm) {
-                            root = node = ch;
-                            level = 0;
-                            mlo = mhi = 0;
-                            lvl_set(mlo, mhi, 0, cm);
-                            walking = true;
+                            node = ch;
+                            ++level;
+                            lvl_set(mlo, mhi, level, cm);
                         }
                     }
-                    continue;
-                }
-                // one step of the walk (r_par_walk's)
-                const uint32_t msk = lvl_get(mlo, mhi, level);
-                const int c = __builtin_ctz(msk);
-                lvl_set(mlo, mhi, level, msk & (msk - 1));
-                const XWNode* nd = W + node;
-                const int ch = nd->child[c];
-                if (sc.rc_maxkey[node * 8 + c] <= best) {
-                    lvl_set(mlo, mhi, level, 0);
-                } else if (ch < 0) {
-                    pcur = ~ch;
-                    pend = ~ch + nd->cnt[c];
-                } else {
-                    ++nnode;
-                    const uint32_t cm = children_mask_line(W + ch, of, ivf, tau);
-                    if (cm) {
-                        node = ch;
-                        ++level;
-                        lvl_set(mlo, mhi, level, cm);
+                    uint32_t rest = lvl_get(mlo, mhi, level);
+                    while (rest == 0 && level > 0) {
+                        --level;
+                        node = level == 0 ? root : W[node].parent;
+                        rest = lvl_get(mlo, mhi, level);
                     }
+                    walking = rest != 0;
                 }
-                uint32_t rest = lvl_get(mlo, mhi, level);
-                while (rest == 0 && level > 0) {
-                    --level;
-                    node = level == 0 ? root : W[node].parent;
-                    rest = lvl_get(mlo, mhi, level);
-                }
-                walking = rest != 0;
-            }
-            // ---- the group's queue, compacted (inclusive prefix of the lanes' counts)
-            int incl = nq;
+                // ---- the group's queue, compacted (inclusive prefix of the lanes' counts)
+                int incl = nq;
 #pragma unroll
-            for (int off = 1; off < NSUB; off <<= 1) {
-                const int t = __shfl_up(incl, off, NSUB);
-                if (sub >= off) incl += t;
+                for (int off = 1; off < NSUB; off <<= 1) {
+                    const int t = __shfl_up(incl, off, NSUB);
+                    if (sub >= off) incl += t;
+                }
+                const int total = __shfl(incl, NSUB - 1, NSUB);
+                for (int k = 0; k < nq; ++k) cand[incl - nq + k] = seg[k];
+                __builtin_amdgcn_wave_barrier();
+                // ---- test phase: candidate j by lane j mod 8
+                for (int j = sub; j < total; j += NSUB) {
+                    best = max(best, (long long)*(volatile unsigned long long*)gb - 1);
+                    r_group_consider<TRI>(sc, cand[j], o, d, gb, best, mine, r, nnode, nprim, memo);
+                }
+                __builtin_amdgcn_wave_barrier();
+                // the wave leaves the loop once none of its lanes has anything left (groups stay in step)
+                if (__ballot(!(done && !walking && pcur >= pend)) == 0) break;
             }
-            const int total = __shfl(incl, NSUB - 1, NSUB);
-            for (int k = 0; k < nq; ++k) cand[incl - nq + k] = seg[k];
-            __builtin_amdgcn_wave_barrier();
-            // ---- test phase: candidate j by lane j mod 8
-            for (int j = sub; j < total; j += NSUB) {
-                best = max(best, (long long)*(volatile unsigned long long*)gb - 1);
-                r_par_consider<TRI>(sc, cand[j], o, d, gb, best, mine, r, nnode, nprim, memo);
-            }
-            __builtin_amdgcn_wave_barrier();
-            // the wave leaves the loop once none of its lanes has anything left (groups stay in step)
-            if (__ballot(!(done && !walking && pcur >= pend)) == 0) break;
+            r_group_write<NSUB, TRI>(sc, d, light, r, mine, sub, idx, rgb, rgb8);
+        } else if (sub == 0 && idx >= 0 && m.shard_count > 1) {   // padding slot of a packed tile
+            if (rgb) { rgb[3 * idx] = 0; rgb[3 * idx + 1] = 0; rgb[3 * idx + 2] = 0; }
+            if (rgb8) { rgb8[3 * idx] = 0; rgb8[3 * idx + 1] = 0; rgb8[3 * idx + 2] = 0; }
         }
-        r_split_write<NSUB, TRI>(sc, d, light, r, mine, sub, idx, rgb, rgb8);
-    } else if (sub == 0 && idx >= 0 && m.shard_count > 1) {   // padding slot of a packed tile
-        if (rgb) { rgb[3 * idx] = 0; rgb[3 * idx + 1] = 0; rgb[3 * idx + 2] = 0; }
-        if (rgb8) { rgb8[3 * idx] = 0; rgb8[3 * idx + 1] = 0; rgb8[3 * idx + 2] = 0; }
+        __builtin_amdgcn_wave_barrier();   // the group's LDS state is reset for the next item
     }
-    if (STATS) {
-        const bool px = ok && sub == 0;
-        wave_add_stats(stats, px ? 1 : 0, nnode, nprim, px ? 1 : 0);
-    }
+    if (STATS) wave_add_stats(stats, npx, nnode, nprim, npx);
 }
 
-// Flat Mode R (GI_R_PAR=4; VERDICT r03's chip-wide phases).  k_rf_walk: one lane per pixel slot
-// walks the whole line BVH (no rank pruning) and appends a (slot, entity) pair for every entity of
-// every leaf its line crosses; k_rf_hit: ent_hit over the pairs, the hitting ones kept; k_rf_reach:
-// per hitting pair, the entity's appearances latest first against the pixel's best rank so far
-// (atomic max), the first reachable one raising it; k_rf_shade: per pixel, the entity of the best
-// rank (r_leaf_of_rank) tested again for its hit point and normal, shaded.  The answer -- the
-// highest reachable hitting rank -- is the other kernels'.  No global counter: the walk's wave for
-// tile t owns region t of the pair buffer (per_slot x 64 pairs; through per-lane LDS buffers, the
-// wave keeping its own fill), rcnt[t] its pairs; k_rf_hit compacts a region's hitting pairs in place
-// of its pairs (hcnt[t]); persistent waves take regions in turn.  A region that fills raises the overflow word:
-// k_rf_hit / k_rf_reach / k_rf_shade then do nothing and k_mode_r_batch, guarded by the same word,
-// renders the frame.  (A first version appended through one device-wide counter: its per-wave
-// atomics serialised, k_rf_hit waited 95% of its cycles.)
+// Flat Mode R (VERDICT r03's chip-wide phases; the default for large scenes).  k_rf_walk: one lane per
+// pixel slot walks the whole line BVH (no rank pruning) and stores a (slot, entity) pair for every
+// entity of every leaf its line crosses; k_rf_hit: ent_hit over the pairs, the hitting ones kept;
+// k_rf_scan + k_rf_reach: per hitting pair, the entity's appearances latest first against the pixel's
+// best rank so far (atomic max), the first reachable one raising it; k_rf_shade: per pixel, the
+// entity of the best rank (r_leaf_of_rank) tested again for its hit point and normal, shaded.  The
+// answer -- the highest reachable hitting rank -- is k_mode_r's.
+// Storage, no device-wide append counter (a first version appended every wave's pairs through one:
+// the atomics serialised, k_rf_hit waited 95% of its cycles): the walk's wave for tile t owns tile
+// t's region -- GI_RF_S0 pairs of its own, then pool pages of GI_RF_PAGE pairs taken with one atomic
+// per page run (only tiles with many candidates take any), at most GI_RF_KMAX; rcnt[t] its pairs.  A
+// pair is one word, (slot in the tile << 26) | entity.  k_rf_hit compacts a region's hitting pairs in
+// place; persistent waves take regions in turn.  A tile that needs more pages than it may take, or
+// finds the pool empty, is marked overflowed (rcnt = kRfOvf) and listed; the other phases skip it and
+// k_mode_r_batch, launched behind them over that list, renders exactly those tiles.
 #ifndef GI_RF_BUF
 #define GI_RF_BUF 16   // k_rf_walk: pairs a lane buffers in LDS before the wave flushes
 #endif
+#define GI_RF_S0 512u     // pairs of a tile's own region (8 per pixel slot)
+#define GI_RF_PAGE 512u   // pairs per pool page
+#define GI_RF_KMAX 64u    // pool pages a tile may take (so at most 33,280 pairs per tile)
+constexpr unsigned kRfOvf = 0xFFFFFFFFu;
+constexpr unsigned kRfEntMask = (1u << 26) - 1u;   // scenes of more entities run k_mode_r_batch
 struct RFlat {
-    unsigned* pairs;            // n_regions x rs pairs (slot, entity)
-    unsigned* hits;             // = pairs: each region's hitting pairs compacted in place (a hit is
-                                //   written at or before its pair's position, after the wave read it)
+    unsigned* pairs;            // n_regions x GI_RF_S0: each tile's own region
+    unsigned* pool;             // n_pages x GI_RF_PAGE
+    unsigned* pt;               // per tile: GI_RF_KMAX pool page ids (those taken)
     unsigned long long* best;   // per pixel slot: best rank + 1
-    unsigned* cnt;              // word 0: overflow
-    unsigned* rcnt;             // per region: pairs
-    unsigned* hcnt;             // per region: hitting pairs
-    unsigned* coff;             // per region: its first 64-pair chunk of hits (k_rf_scan); [n_regions]: the total
+    unsigned* cnt;              // [0] pool pages taken, [1] overflowed tiles
+    unsigned* ovf;              // the overflowed tiles (cnt[1] of them)
+    unsigned* rcnt;             // per tile: pairs, or kRfOvf
+    unsigned* hcnt;             // per tile: hitting pairs
+    unsigned* coff;             // per tile: its first 64-pair chunk of hits (k_rf_scan); [n_regions]: the total
     double* dir;                // per pixel slot: its primary direction (k_rf_walk writes, the others read)
-    unsigned rs;                // pairs per region
+    unsigned n_pages;
 };
 __device__ __forceinline__ V3 rf_dir(const RFlat& f, unsigned slot) {
     const double* q = f.dir + 3 * (size_t)slot;
     return v3(q[0], q[1], q[2]);
 }
+// the page index (0 .. GI_RF_KMAX-1) holding pair i of a region beyond its own GI_RF_S0 (0 below)
+__device__ __forceinline__ int rf_page(unsigned i) {
+    return i < GI_RF_S0 ? 0 : (int)min((i - GI_RF_S0) / GI_RF_PAGE, GI_RF_KMAX - 1u);
+}
+// pair i of region r; pg: the id of its pool page (rf_page(i)-th of the region's pages)
+__device__ __forceinline__ unsigned* rf_pair(const RFlat& f, long long r, unsigned i, unsigned pg) {
+    return i < GI_RF_S0 ? f.pairs + (size_t)r * GI_RF_S0 + i : f.pool + (size_t)pg * GI_RF_PAGE + (i - GI_RF_S0) % GI_RF_PAGE;
+}
+// lane k: the id of region r's k-th pool page (only regions beyond their own pairs have any)
+__device__ __forceinline__ unsigned rf_pages_of(const RFlat& f, long long r, unsigned n, int lane) {
+    return (n > GI_RF_S0 && (unsigned)lane < GI_RF_KMAX) ? f.pt[(size_t)r * GI_RF_KMAX + lane] : 0u;
+}
 template <bool STATS>
 __global__ __launch_bounds__(256) void k_rf_walk(DevScene sc, CamDev cam, TileMap m, float tau, RFlat f,
                                                  unsigned long long* stats) {
     __shared__ int s_buf[256][GI_RF_BUF];
+    __shared__ unsigned s_pt[4][GI_RF_KMAX];   // the wave's pool pages
     const long long slot = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     const long long region = slot >> 6;
     const int lane = threadIdx.x & 63;
     int* buf = s_buf[threadIdx.x];
+    unsigned* pt = s_pt[threadIdx.x >> 6];
     long long idx = -1;
     int x = 0, y = 0;
     const bool in = slot < m.n_local * 64;
@@ -897,8 +721,8 @@ __global__ __launch_bounds__(256) void k_rf_walk(DevScene sc, CamDev cam, TileMa
     const XWNode* W = sc.rc_nodes;
     uint64_t mlo = 0, mhi = 0;
     int node = 0, level = 0, pcur = 0, pend = 0, ai = 0, nb = 0;
-    unsigned fill = 0;   // the wave's pairs in its region so far (the same in every lane)
-    bool walking = false;
+    unsigned fill = 0, npg = 0;   // the wave's pairs and pool pages so far (the same in every lane)
+    bool walking = false, ovf = false;
     F3 of = f3(0, 0, 0), ivf = f3(1, 1, 1);
     if (ok) {
         const V3 d = normalize(primary_dir(cam, (double)x, (double)(y + m.y0)));
@@ -910,6 +734,7 @@ __global__ __launch_bounds__(256) void k_rf_walk(DevScene sc, CamDev cam, TileMa
         lvl_set(mlo, mhi, 0, rm);
         walking = rm != 0;
     }
+    const unsigned tag = (unsigned)(slot & 63) << 26;
     for (;;) {
         if (ok) {
             while (ai < sc.n_r_always && nb < GI_RF_BUF) buf[nb++] = sc.r_always[ai++];   // every ray's ImpSpheres
@@ -952,53 +777,77 @@ __global__ __launch_bounds__(256) void k_rf_walk(DevScene sc, CamDev cam, TileMa
                 if (lane >= off) incl += t;
             }
             const unsigned tot = (unsigned)__shfl(incl, 63);
-            for (int k = 0; k < nb; ++k) {
-                const unsigned j = fill + (unsigned)(incl - nb + k);
-                if (j < f.rs) {
-                    const size_t at = (size_t)region * f.rs + j;
-                    f.pairs[2 * at] = (unsigned)slot;
-                    f.pairs[2 * at + 1] = (unsigned)buf[k];
+            const unsigned end = fill + tot;
+            const unsigned need = end > GI_RF_S0 ? (end - GI_RF_S0 + GI_RF_PAGE - 1) / GI_RF_PAGE : 0u;
+            if (need > npg) {   // pool pages for the pairs beyond the tile's own region: one atomic
+                unsigned b = 0;
+                if (lane == 0 && need <= GI_RF_KMAX) b = atomicAdd(f.cnt, need - npg);
+                b = __shfl(b, 0);
+                if (need > GI_RF_KMAX || b + (need - npg) > f.n_pages) {
+                    ovf = true;   // (pages taken past the pool's end are simply unused)
                 } else {
-                    f.cnt[0] = 1u;
+                    if ((unsigned)lane >= npg && (unsigned)lane < need) {
+                        pt[lane] = b + (unsigned)lane - npg;
+                        f.pt[(size_t)region * GI_RF_KMAX + lane] = b + (unsigned)lane - npg;
+                    }
+                    npg = need;
+                    __builtin_amdgcn_wave_barrier();
                 }
             }
-            fill += tot;
+            if (!ovf) {
+                for (int k = 0; k < nb; ++k) {
+                    const unsigned j = fill + (unsigned)(incl - nb + k);
+                    *rf_pair(f, region, j, pt[rf_page(j)]) = tag | (unsigned)buf[k];
+                }
+            }
+            fill = end;
             nb = 0;
         }
-        if (m_more == 0) break;
+        if (m_more == 0 || ovf) break;
     }
-    if (in && lane == 0) f.rcnt[region] = min(fill, f.rs);
-    if (STATS) wave_add_stats(stats, 0, nnode, 0, 0);
+    if (in && lane == 0) {
+        f.rcnt[region] = ovf ? kRfOvf : fill;
+        if (ovf) f.ovf[atomicAdd(f.cnt + 1, 1u)] = (unsigned)region;
+    }
+    if (STATS) {
+        wave_add_stats(stats, 0, nnode, 0, 0);
+        if (in && lane == 0) {
+            atomicAdd(stats + GI_STAT_R_PAIRS, (unsigned long long)fill);
+            if (ovf) atomicAdd(stats + GI_STAT_R_OVF_TILES, 1ull);
+        }
+    }
 }
 // the pairs' exact entity tests; each region's hitting pairs compacted in place of the region
 template <bool STATS, bool TRI>
 __global__ __launch_bounds__(256) void k_rf_hit(DevScene sc, CamDev cam, TileMap m, RFlat f, unsigned long long* stats) {
-    if (*(volatile const unsigned*)f.cnt) return;
     const int lane = threadIdx.x & 63;
     const long long n_regions = m.n_local;
     const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_w = ((long long)gridDim.x * blockDim.x) >> 6;
     uint32_t nprim = 0;
     for (long long r = gw; r < n_regions; r += n_w) {
         const unsigned n = f.rcnt[r];
-        const size_t base = (size_t)r * f.rs;
+        if (n == kRfOvf) {   // k_mode_r_batch renders this tile
+            if (lane == 0) f.hcnt[r] = 0;
+            continue;
+        }
+        const unsigned pg = rf_pages_of(f, r, n, lane);
         unsigned kept = 0;
         for (unsigned i0 = 0; i0 < n; i0 += 64) {
             const unsigned i = i0 + lane;
+            const unsigned pin = __shfl(pg, rf_page(i));
             bool hit = false;
-            unsigned slot = 0, e = 0;
+            unsigned pr = 0;
             if (i < n) {
-                slot = f.pairs[2 * (base + i)];
-                e = f.pairs[2 * (base + i) + 1];
+                pr = *rf_pair(f, r, i, pin);
+                const unsigned slot = (unsigned)r * 64u + (pr >> 26);
                 const V3 d = rf_dir(f, slot);
                 V3 P, N;
-                hit = ent_hit<TRI>(sc, sc.ents[e], cam.pos, d, P, N, nprim) && sq3(P - cam.pos) < DBL_MAX;   // raytracer.h:58-65
+                hit = ent_hit<TRI>(sc, sc.ents[pr & kRfEntMask], cam.pos, d, P, N, nprim) && sq3(P - cam.pos) < DBL_MAX;   // raytracer.h:58-65
             }
             const unsigned long long mh = __ballot(hit);
-            if (hit) {
-                const size_t at = base + kept + (unsigned)__popcll(mh & ((1ull << lane) - 1));
-                f.hits[2 * at] = slot;
-                f.hits[2 * at + 1] = e;
-            }
+            const unsigned k = kept + (unsigned)__popcll(mh & ((1ull << lane) - 1));
+            const unsigned pout = __shfl(pg, rf_page(k));
+            if (hit) *rf_pair(f, r, k, pout) = pr;   // at or before its own position, already read
             kept += (unsigned)__popcll(mh);
         }
         if (lane == 0) f.hcnt[r] = kept;
@@ -1007,7 +856,6 @@ __global__ __launch_bounds__(256) void k_rf_hit(DevScene sc, CamDev cam, TileMap
 }
 // the regions' hits in chunks of 64: coff = exclusive prefix of ceil(hcnt / 64) (one workgroup)
 __global__ __launch_bounds__(1024) void k_rf_scan(TileMap m, RFlat f) {
-    if (*(volatile const unsigned*)f.cnt) return;
     __shared__ unsigned s_part[1024];
     const int t = threadIdx.x;
     const long long n = m.n_local, per = (n + 1023) / 1024;
@@ -1038,13 +886,13 @@ __global__ __launch_bounds__(1024) void k_rf_scan(TileMap m, RFlat f) {
 template <bool STATS>
 __global__ __launch_bounds__(64) void k_rf_reach(DevScene sc, CamDev cam, TileMap m, RFlat f, unsigned long long* stats) {
     __shared__ int s_memo[GI_R_MEMO > 0 ? 64 * GI_R_MEMO : 1];
-    if (*(volatile const unsigned*)f.cnt) return;
     const int lane = threadIdx.x & 63;
     const long long n_regions = m.n_local;
     const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_w = ((long long)gridDim.x * blockDim.x) >> 6;
     const long long n_chunks = f.coff[n_regions];
     uint32_t nnode = 0;
     long long cur = -1;
+    unsigned pg = 0;
     for (long long c = gw; c < n_chunks; c += n_w) {
         long long lo = 0, hi = n_regions - 1;   // the last region whose first chunk is <= c
         while (lo < hi) {
@@ -1054,18 +902,22 @@ __global__ __launch_bounds__(64) void k_rf_reach(DevScene sc, CamDev cam, TileMa
         }
         const long long r = lo;
         const unsigned n = f.hcnt[r];
-        const size_t base = (size_t)r * f.rs;
-        if (GI_R_MEMO > 0 && r != cur) {
-            __builtin_amdgcn_wave_barrier();
-            for (int k = 0; k < GI_R_MEMO; ++k) s_memo[lane * GI_R_MEMO + k] = -1;   // lane = pixel of the tile
-            __builtin_amdgcn_wave_barrier();
+        if (r != cur) {
+            pg = rf_pages_of(f, r, n, lane);
+            if (GI_R_MEMO > 0) {
+                __builtin_amdgcn_wave_barrier();
+                for (int k = 0; k < GI_R_MEMO; ++k) s_memo[lane * GI_R_MEMO + k] = -1;   // lane = pixel of the tile
+                __builtin_amdgcn_wave_barrier();
+            }
         }
         cur = r;
         const unsigned i = (unsigned)(c - (long long)f.coff[r]) * 64u + (unsigned)lane;
+        const unsigned pin = __shfl(pg, rf_page(i));
         if (i < n) {
-            const unsigned slot = f.hits[2 * (base + i)];
-            const int e = (int)f.hits[2 * (base + i) + 1];
-            const RMemo memo{GI_R_MEMO > 0 ? s_memo + (slot & 63) * GI_R_MEMO : nullptr};
+            const unsigned pr = *rf_pair(f, r, i, pin);
+            const unsigned slot = (unsigned)r * 64u + (pr >> 26);
+            const int e = (int)(pr & kRfEntMask);
+            const RMemo memo{GI_R_MEMO > 0 ? s_memo + (pr >> 26) * GI_R_MEMO : nullptr};
             const V3 d = rf_dir(f, slot);
             const int a1 = sc.app_off[e + 1];
             for (int a = sc.app_off[e]; a < a1; ++a) {
@@ -1080,12 +932,12 @@ __global__ __launch_bounds__(64) void k_rf_reach(DevScene sc, CamDev cam, TileMa
     }
     if (STATS) wave_add_stats(stats, 0, nnode, 0, 0);
 }
-// per pixel: the best rank's entity, shaded
+// per pixel: the best rank's entity, shaded (overflowed tiles: left to k_mode_r_batch)
 template <bool STATS, bool TRI>
 __global__ __launch_bounds__(256) void k_rf_shade(DevScene sc, CamDev cam, V3 light, TileMap m, double* rgb, uint8_t* rgb8,
                                                   RFlat f, unsigned long long* stats) {
-    if (*(volatile const unsigned*)f.cnt) return;
     const long long slot = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (slot < m.n_local * 64 && f.rcnt[slot >> 6] == kRfOvf) return;   // (uniform: a wave is one tile)
     long long idx = -1;
     int x = 0, y = 0;
     const bool ok = slot < m.n_local * 64 && slot_pixel(m, slot >> 6, (int)(slot & 63), idx, x, y);
@@ -1111,102 +963,6 @@ __global__ __launch_bounds__(256) void k_rf_shade(DevScene sc, CamDev cam, V3 li
         if (rgb8) { rgb8[3 * idx] = 0; rgb8[3 * idx + 1] = 0; rgb8[3 * idx + 2] = 0; }
     }
     if (STATS) wave_add_stats(stats, ok ? 1 : 0, 0, nprim, ok ? 1 : 0);
-}
-
-// pixels whose first pass gave up (k_mode_r_split with a budget): (pixel slot, rank found) pairs
-struct RHeavy {
-    long long* list;   // 2 per entry
-    unsigned* n;
-    unsigned budget;   // 0: no budget (the first pass finishes every pixel)
-};
-
-
-#ifndef GI_R_BUDGET
-// candidates a pixel's 8 lanes may meet in k_mode_r_split before the pixel is handed to
-// k_mode_r_heavy (a whole wave per pixel); 0: never
-#define GI_R_BUDGET 0
-#endif
-#ifndef GI_R_TRI
-#define GI_R_TRI 1   // k_mode_r_split specialised for scenes of ImpTriangles only (DevScene::r_tri_only)
-#endif
-#ifndef GI_R_MIN_WAVES
-#define GI_R_MIN_WAVES 1   // minimum waves per SIMD asked of the register allocator (k_mode_r_split)
-#endif
-template <bool STATS, int NSUB, bool TRI>
-__global__ __launch_bounds__(256, GI_R_MIN_WAVES) void k_mode_r_split(DevScene sc, CamDev cam, V3 light, TileMap m, double* rgb,
-                                                       uint8_t* rgb8, unsigned long long* stats, float tau, RHeavy hv) {
-    const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    const long long ps = g / NSUB;   // pixel slot (tile order)
-    const int sub = (int)(g % NSUB);
-    // the ray's node-test memo: GI_R_MEMO entries per pixel group, cleared by its lanes
-    __shared__ int s_memo[GI_R_MEMO > 0 ? (256 / NSUB) * GI_R_MEMO : 1];
-    RMemo memo{GI_R_MEMO > 0 ? s_memo + (threadIdx.x / NSUB) * GI_R_MEMO : nullptr};
-    if (GI_R_MEMO > 0) {
-        for (int k = sub; k < GI_R_MEMO; k += NSUB) memo.e[k] = -1;
-        __builtin_amdgcn_wave_barrier();   // a group's lanes are in one wave (NSUB <= 64)
-    }
-    const long long lt = ps >> 6;
-    long long idx = -1;
-    int x = 0, y = 0;
-    const bool ok = lt < m.n_local && slot_pixel(m, lt, (int)(ps & 63), idx, x, y);
-    y += m.y0;
-    uint32_t nnode = 0, nprim = 0;
-    if (ok) {
-        const V3 o = cam.pos;
-        const V3 d = normalize(primary_dir(cam, (double)x, (double)y));   // Ray ctor (ray.h:6)
-        RResult r;
-        long long mine, best = -1;
-        const bool gave_up = trace_mode_r_split<NSUB, TRI>(sc, o, d, tau, sub, r, mine, nnode, nprim, memo, best, hv.budget);
-        if (gave_up) {   // a heavy pixel: k_mode_r_heavy finishes it with a whole wave
-            if (sub == 0) {
-                const unsigned i = atomicAdd(hv.n, 1u);
-                hv.list[2 * i] = ps;
-                hv.list[2 * i + 1] = best;
-            }
-        } else {
-            r_split_write<NSUB, TRI>(sc, d, light, r, mine, sub, idx, rgb, rgb8);
-        }
-    } else if (sub == 0 && idx >= 0 && m.shard_count > 1) {   // padding slot of a packed tile
-        if (rgb) { rgb[3 * idx] = 0; rgb[3 * idx + 1] = 0; rgb[3 * idx + 2] = 0; }
-        if (rgb8) { rgb8[3 * idx] = 0; rgb8[3 * idx + 1] = 0; rgb8[3 * idx + 2] = 0; }
-    }
-    if (STATS) {
-        const bool px = ok && sub == 0;
-        wave_add_stats(stats, px ? 1 : 0, nnode, nprim, px ? 1 : 0);
-    }
-}
-
-// Heavy pixels of the budgeted first pass: one wave (64 lanes) per pixel, candidates dealt over its
-// 64 lanes, the walk restarted with the first pass's rank minus one as the pruning bound (its
-// candidate is met again; nothing of lower rank can win).  Waves loop over the list.
-template <bool STATS, bool TRI>
-__global__ __launch_bounds__(256, GI_R_MIN_WAVES) void k_mode_r_heavy(DevScene sc, CamDev cam, V3 light, TileMap m, double* rgb,
-                                                       uint8_t* rgb8, unsigned long long* stats, float tau, RHeavy hv) {
-    __shared__ int s_memo[GI_R_MEMO > 0 ? 4 * GI_R_MEMO : 1];
-    RMemo memo{GI_R_MEMO > 0 ? s_memo + (threadIdx.x >> 6) * GI_R_MEMO : nullptr};
-    const int sub = (int)(threadIdx.x & 63);
-    const unsigned n = *hv.n;
-    uint32_t nnode = 0, nprim = 0;
-    for (unsigned i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < n; i += (gridDim.x * blockDim.x) >> 6) {
-        const long long ps = hv.list[2 * i];
-        long long best = hv.list[2 * i + 1] - 1;
-        if (GI_R_MEMO > 0) {
-            for (int k = sub; k < GI_R_MEMO; k += 64) memo.e[k] = -1;
-            __builtin_amdgcn_wave_barrier();
-        }
-        long long idx = -1;
-        int x = 0, y = 0;
-        slot_pixel(m, ps >> 6, (int)(ps & 63), idx, x, y);
-        y += m.y0;
-        const V3 o = cam.pos;
-        const V3 d = normalize(primary_dir(cam, (double)x, (double)y));
-        RResult r;
-        long long mine;
-        trace_mode_r_split<64, TRI>(sc, o, d, tau, sub, r, mine, nnode, nprim, memo, best, 0);
-        r_split_write<64, TRI>(sc, d, light, r, mine, sub, idx, rgb, rgb8);
-        __builtin_amdgcn_wave_barrier();
-    }
-    if (STATS) wave_add_stats(stats, 0, nnode, nprim, 0);
 }
 
 template <bool STATS>
@@ -2464,11 +2220,11 @@ long long shard_tiles(int w, int h, int shard_count) { return make_map(w, h, sha
 // overrides the shading-handler threshold, GI_X_FLAGS the schedule flags, GI_X_MAX_RUN the largest
 // work-unit run length (scenes of cheap background samples such as the main.cpp scene prefer 8).
 struct XEnv {
-    int lds = 1, h8 = 0, xf = -1, run_log2 = 0, help = 1, spread = -1, r_split = -1, leaf8 = 0, wf = -1;
-    int r_budget = GI_R_BUDGET;       // Mode R heavy-pixel hand-off (GI_R_BUDGET, candidates; 0: off)
-    int r_par = GI_R_PAR;             // Mode R walk split over the pixel's lanes (GI_R_PAR=0/1; 2: in rounds; 4: flat)
+    int lds = 1, h8 = 0, xf = -1, run_log2 = 0, help = 1, spread = -1, leaf8 = 0, wf = -1;
+    int r_flat = -1;                  // Mode R kernels (GI_R_FLAT): 1 the flat phases for every scene, 0 k_mode_r
+                                      // for every scene, 2 k_mode_r_batch for the whole frame (tests); -1 by size
     long long wf_chunk = 8ll << 20;   // wavefront Mode X: units (pixel samples) per chunk = queue capacity
-    int rf_per_slot = 128;            // flat Mode R: candidate pairs per pixel slot of a tile's region (GI_RF_PER_SLOT)
+    int rf_per_slot = 16;             // flat Mode R: pool pairs per pixel slot of the frame (GI_RF_PER_SLOT)
 };
 const XEnv& x_env() {
     static XEnv env;
@@ -2479,10 +2235,8 @@ const XEnv& x_env() {
         if (const char* v = std::getenv("GI_X_FLAGS")) env.xf = std::atoi(v);
         if (const char* v = std::getenv("GI_X_HELP")) env.help = std::atoi(v) != 0;
         if (const char* v = std::getenv("GI_X_SPREAD")) env.spread = std::atoi(v);
-        if (const char* v = std::getenv("GI_R_SPLIT")) env.r_split = std::atoi(v);
-        if (const char* v = std::getenv("GI_R_BUDGET")) env.r_budget = std::max(0, std::atoi(v));
-        if (const char* v = std::getenv("GI_R_PAR")) env.r_par = std::atoi(v);
-        if (const char* v = std::getenv("GI_RF_PER_SLOT")) env.rf_per_slot = std::max(1, std::min(1024, std::atoi(v)));
+        if (const char* v = std::getenv("GI_R_FLAT")) env.r_flat = std::atoi(v);
+        if (const char* v = std::getenv("GI_RF_PER_SLOT")) env.rf_per_slot = std::max(0, std::min(1024, std::atoi(v)));
         if (const char* v = std::getenv("GI_X_LEAF8")) env.leaf8 = std::max(0, std::min(8, std::atoi(v)));
         if (const char* v = std::getenv("GI_X_WF")) env.wf = std::atoi(v);
         if (const char* v = std::getenv("GI_X_WF_CHUNK")) env.wf_chunk = std::max(1ll << 16, std::min(1ll << 30, std::atoll(v)));
@@ -2525,8 +2279,21 @@ int x_form_choice(const DevScene& sc, const XLaunchCfg& xc, const gi_opts& o) {
     return (xc.kv >= 2 || (size_t)sc.n_xwnodes * sizeof(XWNode) <= ((size_t)1 << 20)) ? 2 : 0;
 }
 long long x_wf_chunk() { return x_env().wf_chunk; }
-int x_env_r_par() { return x_env().r_par; }
 int x_env_rf_per_slot() { return x_env().rf_per_slot; }
+unsigned rf_own_pairs() { return GI_RF_S0; }
+unsigned rf_page_pairs() { return GI_RF_PAGE; }
+unsigned rf_max_pages() { return GI_RF_KMAX; }
+// Mode R kernel of a launch: 0 k_mode_r (one lane per pixel; small scenes, the reverse-DFS flag, an
+// octree that never split), 1 the flat phases (scenes of more than 4096 entities; their overflowed
+// tiles through k_mode_r_batch), 2 k_mode_r_batch for the whole frame (GI_R_FLAT=2, tests; and
+// scenes of 2^26 entities or more, beyond the flat phases' one-word pairs)
+int r_kernel_choice(const DevScene& sc, const gi_opts& o) {
+    if (o.mode != GI_MODE_R || (o.flags & GI_FLAG_R_DFS) || sc.n_rnodes <= 1) return 0;
+    const XEnv& env = x_env();
+    const bool large = env.r_flat >= 0 ? env.r_flat != 0 : sc.n_ents > 4096;
+    if (!large) return 0;
+    return (env.r_flat == 2 || (unsigned)sc.n_ents > kRfEntMask) ? 2 : 1;
+}
 
 hipError_t x_launch_config(const DevScene& sc, int device, XLaunchCfg& cfg) {
     const bool lds = x_env().lds != 0 && sc.x_lds_bytes > 0;
@@ -2580,84 +2347,38 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
         // an octree that never split is one leaf: its list scanned backwards (first success) is
         // already the least work
         const int dfs = ((o.flags & GI_FLAG_R_DFS) || sc.n_rnodes <= 1) ? 1 : 0;
-        // large scenes: a pixel's candidates split over 8 lanes (k_mode_r_split); GI_R_SPLIT=0 / 1
-        // forces either
-        const XEnv& env = x_env();
-        const bool split = !dfs && (env.r_split >= 0 ? env.r_split != 0 : sc.n_ents > 4096);
-        // heavy-pixel hand-off (k_mode_r_heavy): the budget from GI_R_BUDGET, when the scratch list exists
-        RHeavy hv{xs.rheavy, sc.work + 2, xs.rheavy ? (unsigned)env.r_budget : 0u};
-        if (split && hv.budget) {
-            const hipError_t e0 = hipMemsetAsync(sc.work + 2, 0, sizeof(unsigned), stream);
-            if (e0 != hipSuccess) return e0;
-        }
+        const int rk = r_kernel_choice(sc, o);
+        const bool tri = sc.r_tri_only != 0;   // ImpTriangle-only scenes: the other entity kinds' code dropped
         mark(ev_begin);
-        if (split && env.r_par == 4 && xs.rf_pairs && xs.rf_slots >= m.n_local * (kTile * kTile)) {   // flat phases
-            const RFlat f{xs.rf_pairs, xs.rf_pairs, xs.rf_best, xs.rf_cnt, xs.rf_rcnt, xs.rf_hcnt, xs.rf_coff, xs.rf_dir,
-                          (unsigned)(xs.rf_cap / xs.rf_slots * 64)};
+        if (rk == 1 && xs.rf_pairs && xs.rf_slots >= m.n_local * (kTile * kTile)) {   // flat phases
+            const RFlat f{xs.rf_pairs, xs.rf_pairs + (size_t)(xs.rf_slots / 64) * GI_RF_S0, xs.rf_pt, xs.rf_best, xs.rf_cnt,
+                          xs.rf_ovf, xs.rf_rcnt, xs.rf_hcnt, xs.rf_coff, xs.rf_dir, xs.rf_pages};
             const dim3 pgrid((unsigned)((m.n_local * (kTile * kTile) + 255) / 256)), fgrid(4096);
-            hipError_t e1 = hipMemsetAsync(xs.rf_cnt, 0, sizeof(unsigned), stream);
+            hipError_t e1 = hipMemsetAsync(xs.rf_cnt, 0, 2 * sizeof(unsigned), stream);
             if (e1 != hipSuccess) return e1;
-            const dim3 sgrid((unsigned)((m.n_local * (kTile * kTile) * 8 + 255) / 256));
+            // the overflowed tiles' fallback: half a tile per workgroup item, a grid that returns at once
+            // when the list is empty
+            const dim3 bgrid((unsigned)std::min<long long>(2 * m.n_local, 2048));
             if (stats) hipLaunchKernelGGL(k_rf_walk<true>, pgrid, block, 0, stream, sc, cam, m, tau, f, st);
             else hipLaunchKernelGGL(k_rf_walk<false>, pgrid, block, 0, stream, sc, cam, m, tau, f, st);
-            if (sc.r_tri_only && GI_R_TRI) {
-                if (stats) hipLaunchKernelGGL((k_rf_hit<true, true>), fgrid, block, 0, stream, sc, cam, m, f, st);
-                else hipLaunchKernelGGL((k_rf_hit<false, true>), fgrid, block, 0, stream, sc, cam, m, f, st);
-            } else {
-                if (stats) hipLaunchKernelGGL((k_rf_hit<true, false>), fgrid, block, 0, stream, sc, cam, m, f, st);
-                else hipLaunchKernelGGL((k_rf_hit<false, false>), fgrid, block, 0, stream, sc, cam, m, f, st);
-            }
-            hipLaunchKernelGGL(k_rf_scan, dim3(1), dim3(1024), 0, stream, m, f);
-            if (stats) hipLaunchKernelGGL(k_rf_reach<true>, dim3(4 * fgrid.x), dim3(64), 0, stream, sc, cam, m, f, st);
-            else hipLaunchKernelGGL(k_rf_reach<false>, dim3(4 * fgrid.x), dim3(64), 0, stream, sc, cam, m, f, st);
-            if (sc.r_tri_only && GI_R_TRI) {
-                if (stats) hipLaunchKernelGGL((k_rf_shade<true, true>), pgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, f, st);
-                else hipLaunchKernelGGL((k_rf_shade<false, true>), pgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, f, st);
-                // the candidate buffer overflowed: the batch kernel renders the frame instead
-                if (stats) hipLaunchKernelGGL((k_mode_r_batch<true, true>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, xs.rf_cnt);
-                else hipLaunchKernelGGL((k_mode_r_batch<false, true>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, xs.rf_cnt);
-            } else {
-                if (stats) hipLaunchKernelGGL((k_rf_shade<true, false>), pgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, f, st);
-                else hipLaunchKernelGGL((k_rf_shade<false, false>), pgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, f, st);
-                if (stats) hipLaunchKernelGGL((k_mode_r_batch<true, false>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, xs.rf_cnt);
-                else hipLaunchKernelGGL((k_mode_r_batch<false, false>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, xs.rf_cnt);
-            }
-        } else if (split && env.r_par >= 2) {   // walk and candidate tests in rounds (k_mode_r_batch)
-            const dim3 sgrid((unsigned)((m.n_local * (kTile * kTile) * 8 + 255) / 256));
-            if (sc.r_tri_only && GI_R_TRI) {
-                if (stats) hipLaunchKernelGGL((k_mode_r_batch<true, true>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, nullptr);
-                else hipLaunchKernelGGL((k_mode_r_batch<false, true>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, nullptr);
-            } else {
-                if (stats) hipLaunchKernelGGL((k_mode_r_batch<true, false>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, nullptr);
-                else hipLaunchKernelGGL((k_mode_r_batch<false, false>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, nullptr);
-            }
-        } else if (split && env.r_par) {   // the walk split over the pixel's 8 lanes (k_mode_r_par)
-            const dim3 sgrid((unsigned)((m.n_local * (kTile * kTile) * 8 + 255) / 256));
-            if (sc.r_tri_only && GI_R_TRI) {
-                if (stats) hipLaunchKernelGGL((k_mode_r_par<true, true>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
-                else hipLaunchKernelGGL((k_mode_r_par<false, true>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
-            } else {
-                if (stats) hipLaunchKernelGGL((k_mode_r_par<true, false>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
-                else hipLaunchKernelGGL((k_mode_r_par<false, false>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau);
-            }
-        } else if (split) {
-            const dim3 sgrid((unsigned)((m.n_local * (kTile * kTile) * GI_R_NSUB + 255) / 256));
-            const dim3 hgrid(1024);   // k_mode_r_heavy: 4096 waves loop over the heavy pixels
-            if (sc.r_tri_only && GI_R_TRI) {
-                if (stats) hipLaunchKernelGGL((k_mode_r_split<true, GI_R_NSUB, true>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, hv);
-                else hipLaunchKernelGGL((k_mode_r_split<false, GI_R_NSUB, true>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, hv);
-                if (hv.budget) {
-                    if (stats) hipLaunchKernelGGL((k_mode_r_heavy<true, true>), hgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, hv);
-                    else hipLaunchKernelGGL((k_mode_r_heavy<false, true>), hgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, hv);
-                }
-            } else {
-                if (stats) hipLaunchKernelGGL((k_mode_r_split<true, GI_R_NSUB, false>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, hv);
-                else hipLaunchKernelGGL((k_mode_r_split<false, GI_R_NSUB, false>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, hv);
-                if (hv.budget) {
-                    if (stats) hipLaunchKernelGGL((k_mode_r_heavy<true, false>), hgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, hv);
-                    else hipLaunchKernelGGL((k_mode_r_heavy<false, false>), hgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, hv);
-                }
-            }
+#define GI_LAUNCH_RF(S, T)                                                                                                \
+    do {                                                                                                                  \
+        hipLaunchKernelGGL((k_rf_hit<S, T>), fgrid, block, 0, stream, sc, cam, m, f, st);                                 \
+        hipLaunchKernelGGL(k_rf_scan, dim3(1), dim3(1024), 0, stream, m, f);                                              \
+        hipLaunchKernelGGL(k_rf_reach<S>, dim3(4 * fgrid.x), dim3(64), 0, stream, sc, cam, m, f, st);                     \
+        hipLaunchKernelGGL((k_rf_shade<S, T>), pgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, f, st);             \
+        hipLaunchKernelGGL((k_mode_r_batch<S, T>), bgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau,        \
+                           (const unsigned*)xs.rf_ovf, (const unsigned*)(xs.rf_cnt + 1));                                 \
+    } while (0)
+            if (stats) { if (tri) GI_LAUNCH_RF(true, true); else GI_LAUNCH_RF(true, false); }
+            else { if (tri) GI_LAUNCH_RF(false, true); else GI_LAUNCH_RF(false, false); }
+#undef GI_LAUNCH_RF
+        } else if (rk) {   // k_mode_r_batch over the whole frame
+            const dim3 sgrid((unsigned)((m.n_local * (kTile * kTile) + 31) / 32));
+            if (stats) { if (tri) hipLaunchKernelGGL((k_mode_r_batch<true, true>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, nullptr, nullptr);
+                         else hipLaunchKernelGGL((k_mode_r_batch<true, false>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, nullptr, nullptr); }
+            else { if (tri) hipLaunchKernelGGL((k_mode_r_batch<false, true>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, nullptr, nullptr);
+                   else hipLaunchKernelGGL((k_mode_r_batch<false, false>), sgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, nullptr, nullptr); }
         } else if (stats) {
             hipLaunchKernelGGL(k_mode_r<true>, grid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau, dfs);
         } else {

@@ -189,7 +189,7 @@ struct DevScene {
     int32_t x_waves4;      // LDS-resident scene with light shading: k_mode_x at 4 waves per SIMD
     int32_t x_tri_only;    // every primitive a triangle, every entity ImpTriangle / ExpQuad / ExpCube /
                            // ExpBox (the 4-wave kinds): HBM-resident k_mode_x's TRI specialisation
-    int32_t r_tri_only;    // every entity an ImpTriangle: k_mode_r_split's TRI specialisation
+    int32_t r_tri_only;    // every entity an ImpTriangle: the Mode R kernels' TRI specialisation
     float root_lo[3], root_hi[3];   // Mode X: union of the root's fp32 child boxes (conservative)
     // Mode R candidate reconstruction (HostScene fields of the same names)
     const int32_t* app_off;
@@ -234,21 +234,23 @@ struct XScratch {
     unsigned* wcnt = nullptr;
     unsigned* h_nlist = nullptr;
     long long wcap = 0;
-    // Mode R heavy-pixel list of the budgeted split kernel: (pixel slot, rank) per entry, rcap entries
-    long long* rheavy = nullptr;
-    long long rcap = 0;
-    // flat Mode R (GI_R_PAR=4): candidate pairs (pixel slot, entity), rf_cap, in regions of
-    // rf_cap / rf_slots x 64 per tile, the hitting ones compacted in place; per tile the pairs / hits
-    // in its region, the best
-    // rank + 1 and the primary direction per pixel slot (rf_slots), and the overflow word
+    // flat Mode R (gi_kernels.hip k_rf_*): candidate pairs, one word each -- every tile's own region
+    // of GI_RF_S0, then the pool of rf_pages pages of GI_RF_PAGE (rf_pairs holds both); per tile its
+    // pool page ids (GI_RF_KMAX), its pairs / hits and its first chunk of hits; per pixel slot the best
+    // rank + 1 and the primary direction; the counters (pool pages taken, overflowed tiles) and the
+    // overflowed tiles' list.  Sized for rf_slots pixel slots.
     unsigned* rf_pairs = nullptr;
+    unsigned* rf_pt = nullptr;
     unsigned long long* rf_best = nullptr;
-    double* rf_dir = nullptr;   // per pixel slot: the primary direction (3 doubles), written by the walk
+    double* rf_dir = nullptr;
     unsigned* rf_cnt = nullptr;
+    unsigned* rf_ovf = nullptr;
     unsigned* rf_rcnt = nullptr;
     unsigned* rf_hcnt = nullptr;
-    unsigned* rf_coff = nullptr;   // per tile + 1: the first 64-hit chunk of its region (k_rf_scan)
-    long long rf_cap = 0, rf_slots = 0;
+    unsigned* rf_coff = nullptr;
+    unsigned rf_pages = 0;
+    long long rf_slots = 0;
+    size_t rf_bytes = 0;
 };
 
 // Mode X launch configuration, computed once per scene when it is created (gi_capi.cpp, on the

@@ -331,9 +331,9 @@ __device__ __forceinline__ bool x_segment(const DevScene& sc, const WFView& v, c
         ws.cyc_s += c1 - c0;
         c0 = c1;
     }
-    if (GI_WF_PSL && act) {
-        L = v3(v.pl[0], v.pl[256], v.pl[512]);
-        T = v3(v.pl[768], v.pl[1024], v.pl[1280]);
+    if (GI_WF_PSL) {   // every lane: a lane without a path never uses them, so L and T are dead during
+        L = v3(v.pl[0], v.pl[256], v.pl[512]);      // the traversals (conditioned on act, the register copies
+        T = v3(v.pl[768], v.pl[1024], v.pl[1280]);  // stayed live for inactive lanes and were spilled)
     }
     // ---- shading (local = ambient, + diffuse + specular when lit)
     bool cont = false;

@@ -87,7 +87,7 @@ def pmc_summary(workload: str, kernel: str = ""):
             continue
         if d.get("workload") != workload or not d.get("counters_per_launch"):
             continue
-        if kernel and not any(kernel + suf in d.get("kernel", "") for suf in ("<", "_split<", "_par<", "_batch<")):
+        if kernel and kernel + "<" not in d.get("kernel", ""):   # (the flat Mode R summary names all its kernels)
             continue
         rnd = os.path.basename(p)[1:3]
         if best is None or rnd > best[0]:
@@ -427,13 +427,14 @@ def main():
         # root-box pretest resolve without traversal (each adds exactly +0) are counted apart
         rays_traced = rays_frame - resolved
         form = dev.x_form(mode, spp, depth) if mode == 1 else None   # the Mode X form this launch ran
+        rkern = dev.r_kernel() if mode == 0 else None                 # Mode R: its kernel (k_rf_walk: the flat phases)
         value = rays_traced * args.steps / elapsed / 1e6
         # algorithmic bytes per launch of the dominant kernel (this rank's launch; N=1: the frame)
         node_bytes = dev.info()["x_node_bytes"] if mode == 1 else NODE_BYTES[0]
         alg = (st[gi.STAT_NODES] * node_bytes + st[gi.STAT_PRIMS] * PRIM_BYTES[mode] +
                st[gi.STAT_PIXELS] * 27) / world
         achieved = alg / (kern_ms * 1e-3) / 1e9
-        ceil = counter_ceilings(args.workload, kern_ms, form if mode == 1 else "k_mode_r") if world == 1 else None
+        ceil = counter_ceilings(args.workload, kern_ms, form if mode == 1 else rkern) if world == 1 else None
         traffic = ceil.get("hbm_counter_bytes") if ceil else None
         out = {
             "metric": "Mray/s + ms/frame at 1920x1080, depth 8; %HBM roofline",
@@ -461,7 +462,7 @@ def main():
             # primary (w*h*spp) and total (primary + bounce + shadow) rays per second
             "mray_s_primary": round(w * h * spp * args.steps / elapsed / 1e6, 3),
             "mray_s_all_rays": round(rays_frame * args.steps / elapsed / 1e6, 3),
-            "roofline": {"bound": "hbm", "kernel": (form if mode == 1 else "k_mode_r"),
+            "roofline": {"bound": "hbm", "kernel": (form if mode == 1 else rkern),
                          "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "alg_bytes_per_launch": int(alg),
@@ -483,6 +484,10 @@ def main():
                       "unit": "TFLOP/s", "frac": ceil["f64_valu_frac"],
                       "achieved_note": "f64 FLOPs per launch (PMC SQ_INSTS_VALU_FLOPS_FP64 x 64 lanes x VALU "
                                        "lane utilisation, pmc_source) / live kernel time", **hbm_part})
+        if rkern == "k_rf_walk":   # the flat phases' candidate pairs and the tiles left to k_mode_r_batch
+            out["roofline"]["kernel_note"] = "flat phases k_rf_walk/hit/scan/reach/shade + k_mode_r_batch over overflowed tiles"
+            out["rf_pairs"] = st[gi.STAT_R_PAIRS]
+            out["rf_overflow_tiles"] = st[gi.STAT_R_OVF_TILES]
         if frame_check is not None:
             out["frame_check"] = frame_check
             if args.dist_backend != "nccl":

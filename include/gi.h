@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GI_ABI_VERSION 9
+#define GI_ABI_VERSION 10
 
 typedef enum gi_status {
     GI_OK = 0,
@@ -162,7 +162,10 @@ typedef struct gi_opts {
 #define GI_STAT_X_LN_RS 21
 #define GI_STAT_X_IT_ST 22
 #define GI_STAT_X_LN_ST 23
-#define GI_STATS_N 24
+#define GI_STAT_R_PAIRS 24      /* Mode R flat phases: candidate pairs (pixel, entity) the walk stored */
+#define GI_STAT_R_OVF_TILES 25  /* Mode R flat phases: tiles whose candidates did not fit the pair
+                                   buffer, rendered by the fallback kernel (k_mode_r_batch) instead */
+#define GI_STATS_N 26
 
 #define GI_TILE 8             /* shard granularity: 8x8 pixel tiles, dealt round-robin to ranks */
 
@@ -246,6 +249,11 @@ int gi_scene_kernel_ms(gi_scene* scene, float* avg_ms, int64_t* n);
  * path-state kernel k_mode_x, 1 = the wavefront form (k_wf_bounce once per bounce), 2 = the
  * segment-synchronous form (k_seg); Mode R: 0. */
 int gi_scene_x_form(gi_scene* scene, const gi_opts* opts, int32_t* form);
+/* Mode R kernel a render of `scene` with `opts` would run (ABI 10; bench labels, tests): 0 = k_mode_r
+ * (one lane per pixel: small scenes, GI_FLAG_R_DFS), 1 = the flat phases (k_rf_walk, k_rf_hit,
+ * k_rf_scan, k_rf_reach, k_rf_shade; scenes of more than 4096 entities; their overflowed tiles by
+ * k_mode_r_batch), 2 = k_mode_r_batch for the whole frame.  Mode X: 0. */
+int gi_scene_r_kernel(gi_scene* scene, const gi_opts* opts, int32_t* kernel);
 
 /* ---- host-side reference octree (no device needed) --------------------------------------------
  * gi_octree_create builds the reference octree from the same descriptors as gi_scene_create (push

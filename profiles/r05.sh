@@ -1,0 +1,99 @@
+#!/bin/bash
+# Round-5 GPU runs, one entry point (run from gpurun: paths relative to $GRAFT_REPO_ROOT).
+#   profiles/r05.sh suites [forms]             GPU suite with the default form choice, then with each
+#                                              Mode X form forced (GI_X_WF=0 persistent, 1 wavefront,
+#                                              2 segment-synchronous; default "2 1 0")
+#   profiles/r05.sh formab <wls,> <spec> ...   the Mode X forms per workload and kernel variant, every
+#                                              form's frame checked bit for bit against the first
+#                                              (FORMS=mega,wf,seg selects the forms)
+#   profiles/r05.sh rab <spec> ...             Mode R: parity subset, then R-C4 / R-C3 bench lines
+#   profiles/r05.sh benchq <wls,> [steps]      quick bench lines (kernel ms, schedule block)
+#   profiles/r05.sh tk <pytest -k expr> [wls,]  GPU tests selected by -k, then quick bench lines
+#   profiles/r05.sh evidence 1|2|forms         1: GPU suite + rocprofv3 stats/PMC of the default kernels
+#                                              (C3 C2 C4 R-C4 C5, or $WLS); 2: shard probes, bench lines
+#                                              of every workload, the C3 bench with its CPU baseline, the
+#                                              N = 8 gloo rehearsal; forms: the forced-form profiles (C3
+#                                              under k_mode_x and the wavefront form, C5 under the
+#                                              wavefront and segment forms)
+# A <spec> is <variant>[:ENV=v,...]: variant "default" = 2019global_amd/libgi.so, else
+# 2019global_amd/_variants/libgi_<variant>.so (python -m 2019global_amd.build --variant NAME DEFINES).
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+lib() { if [ "$1" = default ]; then echo $GRAFT_REPO_ROOT/2019global_amd/libgi.so; else echo $GRAFT_REPO_ROOT/2019global_amd/_variants/libgi_$1.so; fi; }
+what=$1; shift
+case $what in
+suites)
+  O=gpurun_out/r05suite; mkdir -p $O
+  for F in default ${1:-2 1 0}; do
+    if [ $F = default ]; then E=""; else E="GI_X_WF=$F"; fi
+    env $E timeout -k 10 400 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/suite_$F.log 2>&1; rc=$?
+    echo "suite $F: $(tail -1 $O/suite_$F.log)"
+    [ $rc -eq 0 ] || { grep -E "^FAILED|Error" $O/suite_$F.log | head -5; exit 1; }
+  done ;;
+formab)
+  O=gpurun_out/r05form; mkdir -p $O
+  WL=${1//,/ }; shift
+  for SPEC in "$@"; do
+    V=${SPEC%%:*}; E=""; [[ "$SPEC" == *:* ]] && E=${SPEC#*:}; E=${E//,/ }
+    T=${V}_$(echo "$E" | tr ' =' '_-')
+    env GI_LIB=$(lib $V) $E timeout -k 10 400 python3 -u profiles/wf_probe.py --steps 3 --warmup 1 --forms ${FORMS:-mega,wf,seg} $WL > $O/$T.jsonl 2> $O/$T.err || { echo "FAIL $SPEC"; tail -5 $O/$T.err; exit 1; }
+    python3 - "$O/$T.jsonl" "$SPEC" <<'PY'
+import json, sys
+for l in open(sys.argv[1]):
+    d = json.loads(l)
+    f = " ".join("%s %8.3f" % (k, d[k]["pass_ms"]) for k in ("mega", "wf", "seg") if k in d)
+    print("%-30s %-11s %s  identical %s" % (sys.argv[2], d["workload"], f, d.get("identical")), flush=True)
+PY
+  done ;;
+rab)
+  O=gpurun_out/r05rab; mkdir -p $O
+  for SPEC in "$@"; do
+    V=${SPEC%%:*}; E=""; [[ "$SPEC" == *:* ]] && E=${SPEC#*:}; E=${E//,/ }
+    T=${V}_$(echo "$E" | tr ' =' '_-')
+    env GI_LIB=$(lib $V) $E timeout -k 10 300 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 200 --timeout-method thread \
+      -k "soup100k or mode_r_vs_reference_golden or split or candidate_reconstruction or mode_r_entities or mode_r_random" > $O/parity_$T.log 2>&1 || { echo "PARITY FAIL $SPEC"; tail -15 $O/parity_$T.log; exit 1; }
+    echo "parity ok $SPEC: $(tail -1 $O/parity_$T.log)"
+    for W in R-C4 R-C3; do
+      env GI_LIB=$(lib $V) $E timeout -k 10 200 python3 bench.py --workload $W --steps 5 --warmup 1 --no-cpu-baseline --no-host-path > $O/${W}_$T.json 2> $O/${W}_$T.err || { echo "bench fail $SPEC $W"; tail -5 $O/${W}_$T.err; exit 1; }
+      python3 -c "import json; d=json.loads(open('$O/${W}_$T.json').read().strip().splitlines()[-1]); print('%-30s %-6s kernel %.4f ms  frame %.4f ms' % ('$SPEC', '$W', d['roofline']['kernel_ms'], d['ms_per_step']))"
+    done
+  done ;;
+benchq)
+  O=gpurun_out/r05bq; mkdir -p $O
+  for W in ${1//,/ }; do
+    timeout -k 10 200 python3 bench.py --workload $W --steps ${2:-5} --warmup 1 --no-cpu-baseline --no-host-path > $O/bench_$W.json 2> $O/bench_$W.err || { echo "bench $W failed"; tail -5 $O/bench_$W.err; exit 1; }
+    python3 -c "import json; d=json.loads(open('$O/bench_$W.json').read().strip().splitlines()[-1]); print('$W', d['roofline']['kernel'], d['roofline']['kernel_ms'], d['ms_per_step'], d['value'], json.dumps(d.get('schedule')))"
+  done ;;
+tk)
+  O=gpurun_out/r05tk; mkdir -p $O
+  timeout -k 10 500 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$1" > $O/tests.log 2>&1 || { grep -E "FAILED|Error|error" $O/tests.log | head -20; tail -30 $O/tests.log; exit 1; }
+  tail -1 $O/tests.log
+  [ -n "$2" ] && bash $0 benchq $2
+  ;;
+evidence)
+  O=gpurun_out/r05ev; mkdir -p $O
+  case $1 in
+  1)
+    timeout -k 10 600 python3 -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -20 $O/gpu_tests.log; exit 1; }
+    tail -1 $O/gpu_tests.log
+    timeout -k 10 1000 bash profiles/profile.sh r05 ${WLS:-C3 C2 C4 R-C4 C5} > $O/prof.log 2>&1 || { tail -5 $O/prof.log; exit 1; } ;;
+  2)
+    for W in R-C4 C3 C4 C5; do
+      timeout -k 10 300 python3 profiles/shard_scaling.py --workload $W > $O/shard_$W.jsonl 2>&1 || { tail -5 $O/shard_$W.jsonl; exit 1; }
+      tail -1 $O/shard_$W.jsonl | cut -c1-300
+    done
+    for W in C2 C4 C5 R-C4 R-C3 R-main X-main X-zoo X-soup1000; do
+      timeout -k 10 300 python3 bench.py --workload $W --steps 5 --warmup 1 --no-cpu-baseline > $O/bench_$W.json 2> $O/bench_$W.err || { tail -5 $O/bench_$W.err; exit 1; }
+    done
+    timeout -k 10 300 python3 bench.py --workload C3 --steps 20 --warmup 2 > $O/bench_C3.json 2> $O/bench_C3.err || { tail -5 $O/bench_C3.err; exit 1; }
+    timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 8 --dist-backend gloo --workload C3 --steps 3 --warmup 1 > $O/rehearsal_n8_gloo.log 2>&1 || { tail -20 $O/rehearsal_n8_gloo.log; exit 1; }
+    tail -1 $O/rehearsal_n8_gloo.log | cut -c1-300 ;;
+  forms)
+    GI_X_WF=0 timeout -k 10 600 bash profiles/profile.sh r05mega C3 > $O/prof_mega.log 2>&1 || { tail -5 $O/prof_mega.log; exit 1; }
+    GI_X_WF=1 timeout -k 10 900 bash profiles/profile.sh r05wf C3 C5 > $O/prof_wf.log 2>&1 || { tail -5 $O/prof_wf.log; exit 1; }
+    GI_X_WF=2 timeout -k 10 600 bash profiles/profile.sh r05seg C5 > $O/prof_seg.log 2>&1 || { tail -5 $O/prof_seg.log; exit 1; } ;;
+  esac
+  echo "evidence $1 done" ;;
+*)
+  sed -n 2,19p "$0"; exit 2 ;;
+esac

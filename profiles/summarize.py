@@ -12,9 +12,9 @@
 
     python profiles/summarize.py gpurun_out/prof_c3 C3 k_mode_x profiles/r01_c3_pmc.json [frames]
 
-kernel "auto": the dominant one (by total time) of k_mode_x / k_wf_bounce / k_seg / k_mode_r_par /
-k_mode_r_batch / k_mode_r_split / k_mode_r and the flat Mode R pipeline (k_rf_walk, k_rf_hit,
-k_rf_reach, k_rf_shade and its guarded k_mode_r_batch fallback launch), whose figures are the sums
+kernel "auto": the dominant one (by total time) of k_mode_x / k_wf_bounce / k_seg / k_mode_r_batch /
+k_mode_r and the flat Mode R pipeline (k_rf_walk, k_rf_hit, k_rf_scan, k_rf_reach, k_rf_shade and its
+k_mode_r_batch launch over the overflowed tiles), whose figures are the sums
 over its kernels per frame (frames = k_rf_walk's timed calls).  The wavefront form (k_wf_bounce)
 launches once per bounce, so its figures are per FRAME too: `frames` (the bench's timed + warm-up
 frames) given, avg_launch_ns and every counter are the sums over the frame's dispatches (per PMC
@@ -27,7 +27,7 @@ import os
 import sys
 from collections import defaultdict
 
-SINGLE = ("k_mode_x", "k_wf_bounce", "k_seg", "k_mode_r_par", "k_mode_r_batch", "k_mode_r_split", "k_mode_r")
+SINGLE = ("k_mode_x", "k_wf_bounce", "k_seg", "k_mode_r_batch", "k_mode_r")
 
 
 def finish(workload, out, stats, name, launch_ns, per, avg):

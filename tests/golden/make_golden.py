@@ -163,9 +163,54 @@ def make_kat():
     print("kat", kat)
 
 
+# Whole large Mode R frames: R-C3 (Cornell) and R-C4 (the 100k soup) at
+# 1920x1080, every pixel through the compiled reference, in row bands over parallel processes.  The
+# fixture is digests only: the sha256 of the whole RGB888 frame and of each RGB888 row (the exact bar),
+# plus per row the fp64 radiance's channel sums over its non-NaN pixels and its NaN count (compared
+# within 1e-5 relative: device acos / sin / pow may differ from libm by an ulp).
+WHOLE = [("cornell", 1920, 1080), ("soup100000", 1920, 1080)]
+
+
+def _band(args):
+    scn, w, h, y0, y1 = args
+    return y0, U.ref_render(scn, w, h, window=(0, y0, w, y1), stride=1)
+
+
+def whole_frame_digest(rgb: np.ndarray, q: np.ndarray) -> dict:
+    """rgb: (h, w, 3) fp64, q: (h, w, 3) uint8 -- the digests both the fixture and the GPU test use."""
+    h = q.shape[0]
+    nan = np.isnan(rgb).any(axis=2)
+    sums = np.where(nan[:, :, None], 0.0, rgb).sum(axis=1)   # (h, 3)
+    return dict(rgb8_sha256=hashlib.sha256(np.ascontiguousarray(q).tobytes()).hexdigest(),
+                row_rgb8_sha256=[hashlib.sha256(np.ascontiguousarray(q[y]).tobytes()).hexdigest()[:16] for y in range(h)],
+                row_sum=sums.tolist(), row_nan=nan.sum(axis=1).astype(int).tolist())
+
+
+def make_whole_frames(jobs: int = 8, band: int = 8):
+    from multiprocessing import Pool
+    for scene, w, h in WHOLE:
+        sc = scene_by_name(scene)
+        scn = sc.to_scn()
+        rgb = np.zeros((h, w, 3), np.float64)
+        q = np.zeros((h, w, 3), np.uint8)
+        hits = 0
+        with Pool(jobs) as pool:
+            for y0, r in pool.imap_unordered(_band, [(scn, w, h, y, min(h, y + band)) for y in range(0, h, band)]):
+                rgb[r["y"], r["x"]] = r["rgb"]
+                q[r["y"], r["x"]] = r["q"].reshape(-1, 3)
+                hits += int((r["hit"] >= 0).sum())
+        d = whole_frame_digest(rgb, q)
+        d.update(scene=scene, w=w, h=h, mode="R", scene_sha256=sc.digest(), hits=hits)
+        json.dump(d, open(os.path.join(HERE, f"whole_{scene}_{w}x{h}.json"), "w"))
+        print("whole", scene, w, h, d["rgb8_sha256"], int(sum(d["row_nan"])), "NaN pixels")
+
+
 if __name__ == "__main__":
     if not U.have_ref():
         sys.exit("oracle/_ref/ref_harness missing: run `make -C oracle ref` where /root/reference exists")
+    if sys.argv[1:] == ["whole"]:   # the whole 1080p Mode R frames only (minutes over 8 processes)
+        make_whole_frames()
+        sys.exit(0)
     json.dump({"soup100000_vertices_sha256": S.soup_digest(100000, 2019),
                "soup1000_vertices_sha256": S.soup_digest(1000, 2019)},
               open(os.path.join(HERE, "soup_digest.json"), "w"), indent=1)

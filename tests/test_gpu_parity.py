@@ -917,11 +917,13 @@ def test_mode_x_shadow_handoff_frame_identical(torch_cuda, tmp_path):
         assert U.bits_equal(rgb, ref[name]).all(), name
 
 
-def test_mode_r_split_candidates_frame_identical(torch_cuda, tmp_path):
-    """Mode R with a pixel's candidates split over 8 lanes (k_mode_r_split, chosen for scenes of
-    more than 4096 entities; GI_R_SPLIT=1 forces it, read once per process: a child process renders)
-    gives the same frames bit for bit as one lane per pixel on every small scene -- spheres (tested
-    by every ray), all entity classes, and the sharded packed layout."""
+@pytest.mark.parametrize("kernel", ["1", "2"])
+def test_mode_r_large_scene_kernels_on_small_scenes(torch_cuda, tmp_path, kernel):
+    """The Mode R kernels for scenes of more than 4096 entities -- the flat phases (GI_R_FLAT=1) and
+    the 8-lanes-per-pixel fallback k_mode_r_batch over the whole frame (GI_R_FLAT=2), forced onto the
+    small scenes (read once per process: a child process renders) -- give the same frames bit for
+    bit as k_mode_r's one lane per pixel: spheres (tested by every ray), all entity classes, and the
+    sharded packed layout."""
     import subprocess
     import sys
     cases = (("main", 200, 200, 1), ("zoo", 160, 160, 1), ("cornell", 128, 128, 1), ("soup1000", 160, 160, 3))
@@ -938,7 +940,7 @@ def test_mode_r_split_candidates_frame_identical(torch_cuda, tmp_path):
             "        for r in range(n): d.render_device(cam, sc.light, w, h, p.data_ptr() + r * per * 8, 0, shard_count=n, shard_index=r)\n"
             "        torch.cuda.synchronize(); res[name + '_packed'] = p.cpu().numpy()\n"
             "np.savez(%r, **res)") % (U.ROOT, os.path.join(U.ROOT, "tests"), cases, str(out))
-    subprocess.run([sys.executable, "-c", code], check=True, timeout=300, env=dict(os.environ, GI_R_SPLIT="1"))
+    subprocess.run([sys.executable, "-c", code], check=True, timeout=300, env=dict(os.environ, GI_R_FLAT=kernel))
     ref = np.load(out)
     torch = torch_cuda
     for name, w, h, n in cases:
@@ -1014,12 +1016,12 @@ def test_mode_x_forms_bit_identical(torch_cuda, name, w, h, spp, depth, shard):
 
 
 def test_mode_r_kernels_frame_identical(torch_cuda, tmp_path):
-    """The Mode R kernels for large scenes -- the walk split over a pixel's lanes (GI_R_PAR=1,
-    k_mode_r_par), walk / test rounds (2, k_mode_r_batch) and the flat phases (4: k_rf_walk, k_rf_hit,
-    k_rf_reach, k_rf_shade), also with a candidate buffer too small for the frame (GI_RF_PER_SLOT=1:
-    the device falls back to k_mode_r_batch) -- render the whole R-C4 frame (the 100k soup, 1920x1080)
-    and a 2-way sharded, packed 480x270 frame of it bit for bit alike (read once per process: child
-    processes render)."""
+    """The Mode R kernels for large scenes render the whole R-C4 frame (the 100k soup, 1920x1080) and
+    a 2-way sharded, packed 480x270 frame of it bit for bit alike: the flat phases (default), the
+    fallback k_mode_r_batch over the whole frame (GI_R_FLAT=2), and the flat phases with no pool
+    (GI_RF_PER_SLOT=0: every tile with more than its own 512 candidate pairs overflows and only those
+    tiles are rendered by k_mode_r_batch -- counted in GI_STAT_R_OVF_TILES, some but not all).  Read
+    once per process: child processes render."""
     import subprocess
     import sys
     code = ("import sys, numpy as np, torch; sys.path.insert(0, %r); sys.path.insert(0, %r); import oracle_util as U; "
@@ -1027,14 +1029,17 @@ def test_mode_r_kernels_frame_identical(torch_cuda, tmp_path):
             "sc = S.named_scene('soup100000'); d = gi.DeviceScene.from_scene(sc)\n"
             "cam = gi.Camera(sc.cam_pos, sc.cam_look, sc.focal)\n"
             "res['c4'] = d.render(cam, sc.light, 1920, 1080)[0]\n"
+            "st = torch.zeros(gi.STATS_N, dtype=torch.int64, device='cuda')\n"
+            "buf = torch.zeros(1920 * 1080 * 3, dtype=torch.float64, device='cuda')\n"
+            "d.render_device(cam, sc.light, 1920, 1080, buf.data_ptr(), 0, stats_ptr=st.data_ptr())\n"
+            "torch.cuda.synchronize(); res['stats'] = st.cpu().numpy(); res['c4_stats'] = buf.cpu().numpy()\n"
             "per = gi.shard_tiles(480, 270, 2) * gi.TILE * gi.TILE * 3\n"
             "p = torch.zeros(2 * per, dtype=torch.float64, device='cuda')\n"
             "for r in range(2): d.render_device(cam, sc.light, 480, 270, p.data_ptr() + r * per * 8, 0, shard_count=2, shard_index=r)\n"
             "torch.cuda.synchronize(); res['packed'] = p.cpu().numpy()\n"
             "np.savez(sys.argv[1], **res)") % (U.ROOT, os.path.join(U.ROOT, "tests"))
     frames = {}
-    for tag, env in (("par", {"GI_R_PAR": "1"}), ("batch", {"GI_R_PAR": "2"}), ("flat", {"GI_R_PAR": "4"}),
-                     ("flat_overflow", {"GI_R_PAR": "4", "GI_RF_PER_SLOT": "1"})):
+    for tag, env in (("flat", {}), ("batch", {"GI_R_FLAT": "2"}), ("flat_overflow", {"GI_RF_PER_SLOT": "0"})):
         out = tmp_path / (tag + ".npz")
         subprocess.run([sys.executable, "-c", code, str(out)], check=True, timeout=300, env=dict(os.environ, **env))
         frames[tag] = dict(np.load(out))
@@ -1049,4 +1054,11 @@ def test_mode_r_kernels_frame_identical(torch_cuda, tmp_path):
     torch.cuda.synchronize()
     for tag, f in frames.items():
         assert U.bits_equal(rgb, f["c4"]).all(), tag
+        assert U.bits_equal(rgb.reshape(-1), f["c4_stats"]).all(), tag + " (stats launch)"
         assert U.bits_equal(p.cpu().numpy(), f["packed"]).all(), tag + " packed"
+    tiles = gi.shard_tiles(1920, 1080, 1)
+    assert frames["flat"]["stats"][gi.STAT_R_OVF_TILES] == 0
+    assert 0 < frames["flat_overflow"]["stats"][gi.STAT_R_OVF_TILES] < tiles
+    assert frames["flat"]["stats"][gi.STAT_R_PAIRS] > 0
+    print("R-C4 pairs", int(frames["flat"]["stats"][gi.STAT_R_PAIRS]), "overflowed tiles without a pool",
+          int(frames["flat_overflow"]["stats"][gi.STAT_R_OVF_TILES]), "of", tiles)
