@@ -49,10 +49,20 @@ namespace {
 #endif
 #ifndef GI_WF_PSL
 // a path's L and T wait out the two traversals in a per-lane LDS slot (column layout, 6 x 256 fp64 per
-// workgroup) instead of VGPRs: the 4-wave kernel stays within 128 VGPRs
+// workgroup) instead of VGPRs: the 4-wave kernel stays within 128 VGPRs.  k_seg also keeps the path's
+// RNG key, its output index and sample, and its bounce there (fields 6, 7, 8), read where they are
+// used: carried in VGPRs across the traversals they were spilled to scratch (136 -> 56 B per lane)
 #define GI_WF_PSL 1
 #endif
-constexpr size_t kWfSlotBytes = GI_WF_PSL ? 6 * 256 * sizeof(double) : 0;
+constexpr size_t kWfSlotBytes = GI_WF_PSL ? 9 * 256 * sizeof(double) : 0;
+// a path's identity where the shading needs it: RNG key, sample, bounce
+struct PathId {
+    uint64_t key;
+    unsigned smp;
+    int b;
+};
+__device__ __forceinline__ void slot_put_u64(double* pl, int f, uint64_t v) { reinterpret_cast<uint64_t*>(pl)[f * 256] = v; }
+__device__ __forceinline__ uint64_t slot_get_u64(const double* pl, int f) { return reinterpret_cast<const uint64_t*>(pl)[f * 256]; }
 
 // one queue of path records: field f (o.xyz, d.xyz, L.xyz, T.xyz) of entry j at r[f * cap + j]
 struct WFQ {
@@ -286,9 +296,9 @@ __device__ __forceinline__ void wf_wave_steps(uint32_t n, uint64_t& it, uint64_t
     }
     if ((threadIdx.x & 63) == 0) { it += mx; ln += sm; }
 }
-template <bool STATS, bool LDS, bool SH, bool TRI, bool CN>
+template <bool STATS, bool LDS, bool SH, bool TRI, bool CN, typename KeyF>
 __device__ __forceinline__ bool x_segment(const DevScene& sc, const WFView& v, const V3& light, int depth, bool no_shadow, bool act,
-                                          int b, uint64_t key, unsigned smp, V3& o, V3& d, V3& L, V3& T,
+                                          const KeyF& id_of, V3& o, V3& d, V3& L, V3& T,
                                           uint32_t& nnode, uint32_t& nprim, uint32_t& nrays, WFSegStats& ws) {
     uint32_t st_steps = 0;
     uint64_t c0 = STATS ? clock64() : 0;
@@ -356,6 +366,10 @@ __device__ __forceinline__ bool x_segment(const DevScene& sc, const WFView& v, c
             loc = (la + ldf) + ls;
         }
         L = L + vmul(T, v3(smin(loc.x, 1.0), smin(loc.y, 1.0), smin(loc.z, 1.0)));
+        const PathId id = id_of();   // (k_seg: from the lane's slot)
+        const uint64_t key = id.key;
+        const unsigned smp = id.smp;
+        const int b = id.b;
         if (b != depth - 1) {
             if (e.refl > 0.0 && mx_u01k(key, smp, b, 4) < e.refl) {   // mirror: T unchanged
                 d = normalize(d - N * (2.0 * dot(d, N)));
@@ -464,7 +478,7 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
             }
         }
         WFSegStats ws;
-        const bool cont = x_segment<false, LDS, SH, TRI, CN>(sc, v, light, depth, no_shadow, act, b, key, smp, o, d, L, T,
+        const bool cont = x_segment<false, LDS, SH, TRI, CN>(sc, v, light, depth, no_shadow, act, [&] { return PathId{key, smp, b}; }, o, d, L, T,
                                                              nnode, nprim, nrays, ws);
         // ---- live paths to the next bounce's queue: one atomic per wave, entries in lane order
         const unsigned long long mc = __ballot(cont);
@@ -618,6 +632,9 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
                     if (GI_WF_PSL) {
                         v.pl[0] = 0.0; v.pl[256] = 0.0; v.pl[512] = 0.0;
                         v.pl[768] = 1.0; v.pl[1024] = 1.0; v.pl[1280] = 1.0;
+                        slot_put_u64(v.pl, 6, key);
+                        slot_put_u64(v.pl, 7, (uint64_t)(uint32_t)idx | ((uint64_t)smp << 32));   // (idx < 2^32: work-list index or pixel)
+                        slot_put_u64(v.pl, 8, 0ull);
                     }
                 }
             }
@@ -632,11 +649,19 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
             const unsigned long long ml = __ballot(live);
             if (lane == 0) { ++ws.segs; ws.live += __popcll(ml); }
         }
-        const bool cont = x_segment<STATS, LDS, SH, TRI, CN>(sc, v, light, depth, no_shadow, live, b, key, smp, o, d, L, T,
-                                                             nnode, nprim, nrays, ws);
+        const bool cont = x_segment<STATS, LDS, SH, TRI, CN>(
+            sc, v, light, depth, no_shadow, live,
+            [&] { return GI_WF_PSL ? PathId{slot_get_u64(v.pl, 6), (unsigned)(slot_get_u64(v.pl, 7) >> 32), (int)slot_get_u64(v.pl, 8)}
+                                   : PathId{key, smp, b}; },
+            o, d, L, T, nnode, nprim, nrays, ws);
         if (live) {
             if (cont) {
-                ++b;
+                if (GI_WF_PSL) slot_put_u64(v.pl, 8, slot_get_u64(v.pl, 8) + 1);
+                else ++b;
+            } else if (GI_WF_PSL) {
+                const uint64_t is = slot_get_u64(v.pl, 7);
+                wf_store(a.part, rgb, rgb8, spp, (long long)(uint32_t)is, (unsigned)(is >> 32), L);
+                live = false;
             } else {
                 wf_store(a.part, rgb, rgb8, spp, idx, smp, L);
                 live = false;

@@ -176,16 +176,6 @@ def _band(args):
     return y0, U.ref_render(scn, w, h, window=(0, y0, w, y1), stride=1)
 
 
-def whole_frame_digest(rgb: np.ndarray, q: np.ndarray) -> dict:
-    """rgb: (h, w, 3) fp64, q: (h, w, 3) uint8 -- the digests both the fixture and the GPU test use."""
-    h = q.shape[0]
-    nan = np.isnan(rgb).any(axis=2)
-    sums = np.where(nan[:, :, None], 0.0, rgb).sum(axis=1)   # (h, 3)
-    return dict(rgb8_sha256=hashlib.sha256(np.ascontiguousarray(q).tobytes()).hexdigest(),
-                row_rgb8_sha256=[hashlib.sha256(np.ascontiguousarray(q[y]).tobytes()).hexdigest()[:16] for y in range(h)],
-                row_sum=sums.tolist(), row_nan=nan.sum(axis=1).astype(int).tolist())
-
-
 def make_whole_frames(jobs: int = 8, band: int = 8):
     from multiprocessing import Pool
     for scene, w, h in WHOLE:
@@ -199,7 +189,7 @@ def make_whole_frames(jobs: int = 8, band: int = 8):
                 rgb[r["y"], r["x"]] = r["rgb"]
                 q[r["y"], r["x"]] = r["q"].reshape(-1, 3)
                 hits += int((r["hit"] >= 0).sum())
-        d = whole_frame_digest(rgb, q)
+        d = U.whole_frame_digest(rgb, q)
         d.update(scene=scene, w=w, h=h, mode="R", scene_sha256=sc.digest(), hits=hits)
         json.dump(d, open(os.path.join(HERE, f"whole_{scene}_{w}x{h}.json"), "w"))
         print("whole", scene, w, h, d["rgb8_sha256"], int(sum(d["row_nan"])), "NaN pixels")

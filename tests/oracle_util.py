@@ -4,6 +4,7 @@ build time), and read/write golden fixtures.  Test infrastructure only."""
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import importlib
 import os
 import struct
@@ -195,6 +196,19 @@ def ref_boxes(recs: np.ndarray) -> np.ndarray:
             f.write(np.ascontiguousarray(recs, "<f8").tobytes())
         subprocess.run([REF_HARNESS, "boxes", rp, op], check=True)
         return np.frombuffer(open(op, "rb").read(), dtype="<i4").copy()
+
+
+def whole_frame_digest(rgb: np.ndarray, q: np.ndarray) -> dict:
+    """Digests of a whole frame (tests/golden/whole_*.json, make_golden.py `whole`): rgb (h, w, 3) fp64
+    radiance, q (h, w, 3) RGB888.  The sha256 of the RGB888 frame and of each of its rows (the exact
+    bar), and per row the fp64 channel sums over its non-NaN pixels and its NaN count (compared within
+    1e-5 relative: the device's acos / sin / pow may differ from libm by an ulp)."""
+    h = q.shape[0]
+    nan = np.isnan(rgb).any(axis=2)
+    sums = np.where(nan[:, :, None], 0.0, rgb).sum(axis=1)   # (h, 3)
+    return dict(rgb8_sha256=hashlib.sha256(np.ascontiguousarray(q).tobytes()).hexdigest(),
+                row_rgb8_sha256=[hashlib.sha256(np.ascontiguousarray(q[y]).tobytes()).hexdigest()[:16] for y in range(h)],
+                row_sum=sums.tolist(), row_nan=nan.sum(axis=1).astype(int).tolist())
 
 
 def bits_equal(a: np.ndarray, b: np.ndarray) -> np.ndarray:

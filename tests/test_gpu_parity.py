@@ -90,6 +90,24 @@ def test_mode_r_vs_reference_golden(torch_cuda, name):
     print(f"{name}: {exact * 100:.3f}% pixels bit-identical to the reference")
 
 
+@pytest.mark.parametrize("scene", ["cornell", "soup100000"])
+def test_mode_r_whole_frame_vs_reference(torch_cuda, scene):
+    """R-C3 (Cornell) and R-C4 (the 100k soup) at 1920x1080, EVERY pixel against the compiled
+    reference (tests/golden/whole_<scene>_1920x1080.json, make_golden.py `whole`): the RGB888 frame
+    (Image::setPixel, image.h:14-16) hashes equal row by row and as a whole -- the exact bar -- and
+    each row's fp64 radiance sums per channel agree within 1e-5 relative, its NaN count exactly."""
+    g = json.load(open(os.path.join(GOLD, f"whole_{scene}_1920x1080.json")))
+    sc = _scene(scene)
+    assert sc.digest() == g["scene_sha256"]
+    rgb, rgb8 = dev_scene(scene).render(cam_of(sc), sc.light, g["w"], g["h"])
+    d = U.whole_frame_digest(rgb, rgb8)
+    bad = [y for y in range(g["h"]) if d["row_rgb8_sha256"][y] != g["row_rgb8_sha256"][y]]
+    assert not bad, f"{scene}: RGB888 rows differ from the reference: {bad[:10]} ({len(bad)} rows)"
+    assert d["rgb8_sha256"] == g["rgb8_sha256"]
+    assert d["row_nan"] == g["row_nan"]
+    assert_rel(np.array(d["row_sum"]), np.array(g["row_sum"]), f"{scene} row sums")
+
+
 @pytest.mark.parametrize("scene,w,h", [("zoo", 160, 160), ("only_expsphere", 96, 96), ("only_expcone", 96, 96)])
 def test_mode_r_entities_vs_oracle_all_pixels(torch_cuda, scene, w, h):
     """Every pixel, including those whose texel the reference reads out of bounds: the device and
