@@ -29,6 +29,7 @@ int r_kernel_choice(const DevScene& sc, const gi_opts& o);
 unsigned rf_own_pairs();
 unsigned rf_page_pairs();
 unsigned rf_max_pages();
+unsigned rf_seg_pairs();
 hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev& cam, V3 light, int w, int h, int y0,
                          const gi_opts& o, double* rgb, uint8_t* rgb8, const XScratch& xs, KTimer* kt,
                          hipStream_t stream);
@@ -116,9 +117,9 @@ hipError_t upload(gi_scene* s, const std::vector<T>& v, const T** out) {
 
 void free_rflat(XScratch& x) {
     for (void* p : {(void*)x.rf_pairs, (void*)x.rf_pt, (void*)x.rf_best, (void*)x.rf_dir, (void*)x.rf_cnt, (void*)x.rf_ovf,
-                    (void*)x.rf_rcnt, (void*)x.rf_hcnt, (void*)x.rf_coff})
+                    (void*)x.rf_rcnt, (void*)x.rf_soff, (void*)x.rf_shc, (void*)x.rf_sreg, (void*)x.rf_hoff})
         (void)hipFree(p);
-    x.rf_pairs = x.rf_pt = x.rf_cnt = x.rf_ovf = x.rf_rcnt = x.rf_hcnt = x.rf_coff = nullptr;
+    x.rf_pairs = x.rf_pt = x.rf_cnt = x.rf_ovf = x.rf_rcnt = x.rf_soff = x.rf_shc = x.rf_sreg = x.rf_hoff = nullptr;
     x.rf_best = nullptr;
     x.rf_dir = nullptr;
     x.rf_pages = 0;
@@ -144,6 +145,9 @@ int ensure_xscratch(gi_scene* s, int w, int h, const gi_opts* o) {
             const long long tiles = need / 64;
             const long long pages = (long long)x_env_rf_per_slot() * need / (long long)rf_page_pairs();
             const size_t pairs = (size_t)tiles * rf_own_pairs() + (size_t)pages * rf_page_pairs();
+            // segments of k_rf_hit: a tile's pairs cut every rf_seg_pairs(), so at most one per tile
+            // plus one per rf_seg_pairs() of the buffer
+            const size_t segs = (size_t)tiles + pairs / rf_seg_pairs() + 1;
             const bool ok =
                 hipMalloc((void**)&x.rf_pairs, pairs * sizeof(unsigned)) == hipSuccess &&
                 hipMalloc((void**)&x.rf_pt, (size_t)tiles * rf_max_pages() * sizeof(unsigned)) == hipSuccess &&
@@ -152,8 +156,10 @@ int ensure_xscratch(gi_scene* s, int w, int h, const gi_opts* o) {
                 hipMalloc((void**)&x.rf_cnt, 8 * sizeof(unsigned)) == hipSuccess &&
                 hipMalloc((void**)&x.rf_ovf, (size_t)tiles * sizeof(unsigned)) == hipSuccess &&
                 hipMalloc((void**)&x.rf_rcnt, (size_t)tiles * sizeof(unsigned)) == hipSuccess &&
-                hipMalloc((void**)&x.rf_hcnt, (size_t)tiles * sizeof(unsigned)) == hipSuccess &&
-                hipMalloc((void**)&x.rf_coff, (size_t)(tiles + 1) * sizeof(unsigned)) == hipSuccess;
+                hipMalloc((void**)&x.rf_soff, (size_t)(tiles + 1) * sizeof(unsigned)) == hipSuccess &&
+                hipMalloc((void**)&x.rf_shc, (size_t)segs * sizeof(unsigned)) == hipSuccess &&
+                hipMalloc((void**)&x.rf_sreg, (size_t)segs * sizeof(unsigned)) == hipSuccess &&
+                hipMalloc((void**)&x.rf_hoff, (size_t)(segs + 1) * sizeof(unsigned)) == hipSuccess;
             if (!ok) {
                 (void)hipGetLastError();   // (clears the sticky allocation error) -- rendered by k_mode_r_batch
                 free_rflat(x);
@@ -161,7 +167,7 @@ int ensure_xscratch(gi_scene* s, int w, int h, const gi_opts* o) {
             }
             x.rf_pages = (unsigned)pages;
             x.rf_slots = need;
-            x.rf_bytes = pairs * sizeof(unsigned) + (size_t)tiles * (rf_max_pages() + 4) * sizeof(unsigned) +
+            x.rf_bytes = pairs * sizeof(unsigned) + (size_t)tiles * (rf_max_pages() + 4) * sizeof(unsigned) + segs * 12 +
                          (size_t)need * (sizeof(unsigned long long) + 3 * sizeof(double));
         }
         return GI_OK;

@@ -296,9 +296,6 @@ __device__ __forceinline__ uint32_t children_mask(const XWNode* nd, F3 of, F3 iv
 // difference from decoding first is a few fp32 ulps of t, inside the 1e-5 * extent padding that
 // the host-checked decoded box already exceeds (the CPU checker runs this form).  Near / far
 // planes per axis as for XWNode.
-#ifndef GI_XC_PK
-#define GI_XC_PK 0   // quantised node test: two children per v_pk_fma_f32
-#endif
 __device__ __forceinline__ float xc_scale(int w, int a) {   // 2^e of axis a (e: signed byte a of w)
     const int e = (int)(int8_t)((w >> (8 * a)) & 0xFF);
     return __int_as_float((e + 127) << 23);
@@ -328,26 +325,6 @@ __device__ __forceinline__ uint32_t children_mask_q(int4 h, int4 q1, int4 q2, in
         fw[a][1] = neg ? lw[a][1] : hw[a][1];
     }
     uint32_t m = 0;
-#if GI_XC_PK
-    // children in pairs: one v_pk_fma_f32 gives two children's plane distances (the same fma per
-    // element, so the same mask)
-#pragma unroll
-    for (int c = 0; c < 8; c += 2) {
-        f32x2 tn = {0.0f, 0.0f}, tf = {tmax, tmax};
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const f32x2 s2 = {siv[a], siv[a]}, b2 = {base[a], base[a]};
-            const f32x2 qn = {xc_q(nw[a][0], nw[a][1], c), xc_q(nw[a][0], nw[a][1], c + 1)};
-            const f32x2 qf = {xc_q(fw[a][0], fw[a][1], c), xc_q(fw[a][0], fw[a][1], c + 1)};
-            const f32x2 t0 = __builtin_elementwise_fma(qn, s2, b2), t1 = __builtin_elementwise_fma(qf, s2, b2);
-            tn.x = fmaxf(tn.x, t0.x);
-            tn.y = fmaxf(tn.y, t0.y);
-            tf.x = fminf(tf.x, t1.x);
-            tf.y = fminf(tf.y, t1.y);
-        }
-        m |= (tn.x <= tf.x ? 1u << c : 0u) | (tn.y <= tf.y ? 2u << c : 0u);
-    }
-#else
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
         float tn = 0.0f, tf = tmax;
@@ -358,7 +335,6 @@ __device__ __forceinline__ uint32_t children_mask_q(int4 h, int4 q1, int4 q2, in
         }
         m |= tn <= tf ? 1u << c : 0u;
     }
-#endif
     return xor_permute8(m & (uint32_t)((h.w >> 24) & 0xFF), dmask);
 }
 template <bool AXIS>

@@ -314,7 +314,8 @@ __device__ __forceinline__ uint32_t children_mask_line_coop(const XWNode* nd, F3
 #define GI_R_MEMO 64   // entries per ray (power of two); 0 disables the memo
 #endif
 struct RMemo {
-    int* e;   // GI_R_MEMO entries of this ray, or nullptr
+    int* e;        // GI_R_MEMO entries of this ray, or nullptr
+    int tag = 0;   // k_rf_reach: (tile & 255) << 1 -- a row serves the same pixel slot of several tiles
 };
 __device__ __forceinline__ int r_memo_slot(int node) { return (int)(((unsigned)node * 2654435761u) >> 26) & (GI_R_MEMO - 1); }
 
@@ -329,13 +330,14 @@ __device__ __forceinline__ bool r_leaf_reachable(const DevScene& sc, int leaf, V
         if (GI_R_MEMO > 0 && memo.e) {
             int* slot = memo.e + r_memo_slot(ni);
             const int m = *slot;
-            if ((m >> 1) == ni) {
+            const int key = (ni << 9) | memo.tag;   // (the scenes using a memo have < 2^22 nodes)
+            if ((m & ~1) == key) {
                 if (!(m & 1)) return false;
                 continue;
             }
             ++nnode;
             const bool ok = box_hit(ld3(nd.mn), ld3(nd.mx), o, d);
-            *slot = (ni << 1) | (ok ? 1 : 0);
+            *slot = key | (ok ? 1 : 0);
             if (!ok) return false;
             continue;
         }
@@ -517,12 +519,13 @@ __global__ __launch_bounds__(256) void k_mode_r_batch(DevScene sc, CamDev cam, V
     __shared__ unsigned s_next[256 / NSUB];             // the group's next item
     __shared__ int s_seg[256 / NSUB][NSUB * SEG];       // each lane's queued candidates (SEG slots)
     __shared__ int s_cand[256 / NSUB][NSUB * SEG];      // the group's candidates of the round, compacted
-    RMemo memo{GI_R_MEMO > 0 ? s_memo + grp * GI_R_MEMO : nullptr};
+    // (memo keys are node << 9: scenes of 2^22 nodes or more run without the memo)
+    RMemo memo{(GI_R_MEMO > 0 && sc.n_rnodes < (1 << 22)) ? s_memo + grp * GI_R_MEMO : nullptr};
     const long long n_items = tiles ? 2ll * (long long)*n_tiles : (m.n_local * (kTile * kTile) + 31) / 32;
     uint32_t nnode = 0, nprim = 0, npx = 0;
     for (long long item = blockIdx.x; item < n_items; item += gridDim.x) {   // uniform over the workgroup
         const long long ps = (tiles ? (long long)tiles[item >> 1] * 64 + (item & 1) * 32 : item * 32) + grp;
-        if (GI_R_MEMO > 0)
+        if (memo.e)
             for (int k = sub; k < GI_R_MEMO; k += NSUB) memo.e[k] = -1;
         if (sub == 0) {
             s_best[grp] = 0ull;
@@ -681,8 +684,10 @@ struct RFlat {
     unsigned* cnt;              // [0] pool pages taken, [1] overflowed tiles
     unsigned* ovf;              // the overflowed tiles (cnt[1] of them)
     unsigned* rcnt;             // per tile: pairs, or kRfOvf
-    unsigned* hcnt;             // per tile: hitting pairs
-    unsigned* coff;             // per tile: its first 64-pair chunk of hits (k_rf_scan); [n_regions]: the total
+    unsigned* soff;             // per tile: its first segment of GI_RF_SEG pairs (k_rf_scan); [n_regions]: the total
+    unsigned* shc;              // per segment: its hitting pairs (compacted to the segment's start)
+    unsigned* sreg;             // per segment: its region
+    unsigned* hoff;             // per segment: the hits before it (k_rf_scan); [segments]: the total
     double* dir;                // per pixel slot: its primary direction (k_rf_walk writes, the others read)
     unsigned n_pages;
 };
@@ -702,109 +707,202 @@ __device__ __forceinline__ unsigned* rf_pair(const RFlat& f, long long r, unsign
 __device__ __forceinline__ unsigned rf_pages_of(const RFlat& f, long long r, unsigned n, int lane) {
     return (n > GI_RF_S0 && (unsigned)lane < GI_RF_KMAX) ? f.pt[(size_t)r * GI_RF_KMAX + lane] : 0u;
 }
+// k_rf_walk: a wave per tile walks the line BVH ONCE for all 64 of its pixels' lines.  The lines
+// of a tile's pixels lie in the convex cone (apex at the camera) over the tile's 4 corner directions
+// -- the primary direction is affine in the pixel coordinates (raytracer.h:41-43) -- so a node box
+// that misses both nappes of that cone (a necessary-condition test against its 4 side planes, in
+// fp64, the box widened by 2 tau) holds no pixel's candidate.  The wave pops up to 8 nodes per round
+// from its LDS stack and tests their 64 children together, one per lane; hit interior children are
+// pushed, hit leaf slots are then tested by every lane against its own line with the per-line slab
+// test of the per-pixel walk (child_hit_line, the same arithmetic), and a passing lane queues the
+// slot's entities.  Since a node's box contains its children's, the pairs are exactly those of a
+// per-pixel walk; a tile's loads are the same for all its lanes (broadcasts) instead of 64
+// divergent walks.  A stack that would exceed GI_RF_STK marks the tile overflowed (k_mode_r_batch).
+#define GI_RF_STK 512u   // traversal stack entries per wave (tile)
+__device__ __forceinline__ bool child_hit_line(const XWNode* nd, int c, F3 of, F3 ivf, float tau) {
+    const int sm = iv_signs(ivf);
+    const float nx = (sm & 1) ? nd->hi[0][c] : nd->lo[0][c], fx = (sm & 1) ? nd->lo[0][c] : nd->hi[0][c];
+    const float ny = (sm & 2) ? nd->hi[1][c] : nd->lo[1][c], fy = (sm & 2) ? nd->lo[1][c] : nd->hi[1][c];
+    const float nz = (sm & 4) ? nd->hi[2][c] : nd->lo[2][c], fz = (sm & 4) ? nd->lo[2][c] : nd->hi[2][c];
+    const float sx = (sm & 1) ? tau : -tau, sy = (sm & 2) ? tau : -tau, sz = (sm & 4) ? tau : -tau;
+    const float tn = fmaxf(fmaxf(((nx + sx) - of.x) * ivf.x, ((ny + sy) - of.y) * ivf.y), ((nz + sz) - of.z) * ivf.z);
+    const float tf = fminf(fminf(((fx - sx) - of.x) * ivf.x, ((fy - sy) - of.y) * ivf.y), ((fz - sz) - of.z) * ivf.z);
+    return (tn <= tf) & ((nd->exists >> c) & 1);
+}
+// may some line of the tile's double cone (side-plane normals n[4], through the camera c) meet the
+// box [lo - wd, hi + wd]?  Forward nappe: every side plane has part of the box on its inner side;
+// backward nappe: every side plane has part of it on its outer side.  Conservative (margin eps).
+__device__ __forceinline__ bool box_meets_cone(const float* lo, const float* hi, double wd, V3 c, const V3* n) {
+    const double l[3] = {(double)lo[0] - wd - c.x, (double)lo[1] - wd - c.y, (double)lo[2] - wd - c.z};
+    const double h[3] = {(double)hi[0] + wd - c.x, (double)hi[1] + wd - c.y, (double)hi[2] + wd - c.z};
+    const double ext = fmax(fmax(fabs(l[0]), fabs(h[0])), fmax(fmax(fabs(l[1]), fabs(h[1])), fmax(fabs(l[2]), fabs(h[2]))));
+    bool fwd = true, bwd = true;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+        const double nn[3] = {n[a].x, n[a].y, n[a].z};
+        double mx = 0.0, mn = 0.0, an = 0.0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const double u = nn[k] * l[k], v = nn[k] * h[k];
+            mx += fmax(u, v);
+            mn += fmin(u, v);
+            an += fabs(nn[k]);
+        }
+        const double eps = 1e-9 * an * ext;
+        fwd = fwd && mx >= -eps;
+        bwd = bwd && mn <= eps;
+    }
+    return fwd || bwd;
+}
 template <bool STATS>
 __global__ __launch_bounds__(256) void k_rf_walk(DevScene sc, CamDev cam, TileMap m, float tau, RFlat f,
                                                  unsigned long long* stats) {
     __shared__ int s_buf[256][GI_RF_BUF];
     __shared__ unsigned s_pt[4][GI_RF_KMAX];   // the wave's pool pages
+    __shared__ int s_stk[4][GI_RF_STK];        // the tile's traversal stack (line-BVH nodes)
+    __shared__ int s_leaf[4][64];              // a round's hit leaf slots: (node << 3) | slot
     const long long slot = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     const long long region = slot >> 6;
     const int lane = threadIdx.x & 63;
     int* buf = s_buf[threadIdx.x];
     unsigned* pt = s_pt[threadIdx.x >> 6];
+    int* stk = s_stk[threadIdx.x >> 6];
+    int* leaves = s_leaf[threadIdx.x >> 6];
     long long idx = -1;
     int x = 0, y = 0;
     const bool in = slot < m.n_local * 64;
     const bool ok = in && slot_pixel(m, slot >> 6, (int)(slot & 63), idx, x, y);
     if (in) f.best[slot] = 0ull;
+    if (__ballot(in) == 0) return;   // (a wave is one tile: all of it beyond the shard's tiles)
     uint32_t nnode = 0;
     const XWNode* W = sc.rc_nodes;
-    uint64_t mlo = 0, mhi = 0;
-    int node = 0, level = 0, pcur = 0, pend = 0, ai = 0, nb = 0;
+    int nb = 0;
     unsigned fill = 0, npg = 0;   // the wave's pairs and pool pages so far (the same in every lane)
-    bool walking = false, ovf = false;
-    F3 of = f3(0, 0, 0), ivf = f3(1, 1, 1);
+    bool ovf = false;
+    const unsigned tag = (unsigned)(slot & 63) << 26;
+    const F3 of = f3((float)cam.pos.x, (float)cam.pos.y, (float)cam.pos.z);
+    F3 ivf = f3(1, 1, 1);
     if (ok) {
         const V3 d = normalize(primary_dir(cam, (double)x, (double)(y + m.y0)));
-        double* q = f.dir + 3 * slot;
-        q[0] = d.x; q[1] = d.y; q[2] = d.z;
-        of = f3((float)cam.pos.x, (float)cam.pos.y, (float)cam.pos.z);
+        double* qd = f.dir + 3 * slot;
+        qd[0] = d.x; qd[1] = d.y; qd[2] = d.z;
         ivf = inv_dir(d);
-        const uint32_t rm = children_mask_line(W, of, ivf, tau);
-        lvl_set(mlo, mhi, 0, rm);
-        walking = rm != 0;
     }
-    const unsigned tag = (unsigned)(slot & 63) << 26;
-    for (;;) {
-        if (ok) {
-            while (ai < sc.n_r_always && nb < GI_RF_BUF) buf[nb++] = sc.r_always[ai++];   // every ray's ImpSpheres
-            // (every line-BVH entity appears in some leaf list: build_rcand boxes only those)
-            while (pcur < pend && nb < GI_RF_BUF) buf[nb++] = sc.rc_ent[pcur++];
-            if (pcur >= pend && walking) {   // one step of the whole walk
-                const uint32_t msk = lvl_get(mlo, mhi, level);
-                const int c = __builtin_ctz(msk);
-                lvl_set(mlo, mhi, level, msk & (msk - 1));
-                const XWNode* nd = W + node;
-                const int ch = nd->child[c];
-                if (ch < 0) {
-                    pcur = ~ch;
-                    pend = ~ch + nd->cnt[c];
-                } else {
-                    ++nnode;
-                    const uint32_t cm = children_mask_line(W + ch, of, ivf, tau);
-                    if (cm) {
-                        node = ch;
-                        ++level;
-                        lvl_set(mlo, mhi, level, cm);
-                    }
-                }
-                uint32_t rest = lvl_get(mlo, mhi, level);
-                while (rest == 0 && level > 0) {
-                    --level;
-                    node = level == 0 ? 0 : W[node].parent;
-                    rest = lvl_get(mlo, mhi, level);
-                }
-                walking = rest != 0;
-            }
-        }
-        const bool more = ok && (walking || pcur < pend || ai < sc.n_r_always);
-        const unsigned long long m_more = __ballot(more);
-        if (m_more == 0 || __ballot(nb > GI_RF_BUF / 2) != 0) {   // flush the wave's buffers into its region
-            int incl = nb;
+    // flush the wave's buffers into its region (pool pages taken as needed: one atomic)
+    auto flush = [&]() {
+        int incl = nb;
 #pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const int t = __shfl_up(incl, off);
-                if (lane >= off) incl += t;
-            }
-            const unsigned tot = (unsigned)__shfl(incl, 63);
-            const unsigned end = fill + tot;
-            const unsigned need = end > GI_RF_S0 ? (end - GI_RF_S0 + GI_RF_PAGE - 1) / GI_RF_PAGE : 0u;
-            if (need > npg) {   // pool pages for the pairs beyond the tile's own region: one atomic
-                unsigned b = 0;
-                if (lane == 0 && need <= GI_RF_KMAX) b = atomicAdd(f.cnt, need - npg);
-                b = __shfl(b, 0);
-                if (need > GI_RF_KMAX || b + (need - npg) > f.n_pages) {
-                    ovf = true;   // (pages taken past the pool's end are simply unused)
-                } else {
-                    if ((unsigned)lane >= npg && (unsigned)lane < need) {
-                        pt[lane] = b + (unsigned)lane - npg;
-                        f.pt[(size_t)region * GI_RF_KMAX + lane] = b + (unsigned)lane - npg;
-                    }
-                    npg = need;
-                    __builtin_amdgcn_wave_barrier();
-                }
-            }
-            if (!ovf) {
-                for (int k = 0; k < nb; ++k) {
-                    const unsigned j = fill + (unsigned)(incl - nb + k);
-                    *rf_pair(f, region, j, pt[rf_page(j)]) = tag | (unsigned)buf[k];
-                }
-            }
-            fill = end;
-            nb = 0;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int t = __shfl_up(incl, off);
+            if (lane >= off) incl += t;
         }
-        if (m_more == 0 || ovf) break;
+        const unsigned tot = (unsigned)__shfl(incl, 63);
+        const unsigned end = fill + tot;
+        const unsigned need = end > GI_RF_S0 ? (end - GI_RF_S0 + GI_RF_PAGE - 1) / GI_RF_PAGE : 0u;
+        if (need > npg && !ovf) {
+            unsigned b = 0;
+            if (lane == 0 && need <= GI_RF_KMAX) b = atomicAdd(f.cnt, need - npg);
+            b = __shfl(b, 0);
+            if (need > GI_RF_KMAX || b + (need - npg) > f.n_pages) {
+                ovf = true;   // (pages taken past the pool's end are simply unused)
+            } else {
+                if ((unsigned)lane >= npg && (unsigned)lane < need) {
+                    pt[lane] = b + (unsigned)lane - npg;
+                    f.pt[(size_t)region * GI_RF_KMAX + lane] = b + (unsigned)lane - npg;
+                }
+                npg = need;
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+        if (!ovf) {
+            for (int k = 0; k < nb; ++k) {
+                const unsigned j = fill + (unsigned)(incl - nb + k);
+                *rf_pair(f, region, j, pt[rf_page(j)]) = (unsigned)buf[k];
+            }
+        }
+        fill = end;
+        nb = 0;
+    };
+    // every ray's ImpSpheres (build_rcand keeps them out of the line BVH)
+    for (int k = 0; k < sc.n_r_always; ++k) {
+        if (__ballot(nb >= (int)GI_RF_BUF) != 0) flush();
+        if (ok) buf[nb++] = (int)(tag | (unsigned)sc.r_always[k]);
     }
+    // the tile's cone: corner directions from its pixels' extents (uniform)
+    int x0 = ok ? x : INT_MAX, x1 = ok ? x : INT_MIN, y0 = ok ? y : INT_MAX, y1 = ok ? y : INT_MIN;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        x0 = min(x0, __shfl_xor(x0, off));
+        x1 = max(x1, __shfl_xor(x1, off));
+        y0 = min(y0, __shfl_xor(y0, off));
+        y1 = max(y1, __shfl_xor(y1, off));
+    }
+    int sp = 0;   // stack entries (uniform)
+    V3 n[4];
+    if (x0 <= x1) {
+        const V3 da = primary_dir(cam, (double)x0, (double)(y0 + m.y0)), db = primary_dir(cam, (double)x1, (double)(y0 + m.y0));
+        const V3 dc = primary_dir(cam, (double)x1, (double)(y1 + m.y0)), dd = primary_dir(cam, (double)x0, (double)(y1 + m.y0));
+        const V3 mid = ((da + db) + (dc + dd)) * 0.25;
+        n[0] = cross(da, db);
+        n[1] = cross(db, dc);
+        n[2] = cross(dc, dd);
+        n[3] = cross(dd, da);
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+            if (dot(n[a], mid) < 0) n[a] = -n[a];
+        if (lane == 0) stk[0] = 0;   // the root
+        sp = 1;
+        __builtin_amdgcn_wave_barrier();
+    }
+    const double wd = 2.0 * (double)tau;
+    const V3 cp = cam.pos;
+    while (sp > 0 && !ovf) {
+        // ---- up to 8 nodes from the stack, their 64 children one per lane
+        const int nt = min(sp, 8);
+        const int j = lane >> 3, c = lane & 7;
+        int ch = 0;
+        bool hit = false;
+        if (j < nt) {
+            const int nd_i = stk[sp - 1 - j];
+            const XWNode* nd = W + nd_i;
+            if ((nd->exists >> c) & 1) {
+                const float lo[3] = {nd->lo[0][c], nd->lo[1][c], nd->lo[2][c]};
+                const float hi[3] = {nd->hi[0][c], nd->hi[1][c], nd->hi[2][c]};
+                hit = box_meets_cone(lo, hi, wd, cp, n);
+                ch = nd->child[c];
+                if (hit && ch < 0) ch = ~((nd_i << 3) | c);   // a leaf slot: (node << 3) | slot, negated
+            }
+            if (c == 0) ++nnode;
+        }
+        __builtin_amdgcn_wave_barrier();
+        sp -= nt;
+        const unsigned long long m_in = __ballot(hit && ch >= 0), m_lf = __ballot(hit && ch < 0);
+        const int n_in = __popcll(m_in), n_lf = __popcll(m_lf);
+        if ((unsigned)(sp + n_in) > GI_RF_STK) {
+            ovf = true;
+            break;
+        }
+        if (hit && ch >= 0) stk[sp + __popcll(m_in & ((1ull << lane) - 1))] = ch;
+        if (hit && ch < 0) leaves[__popcll(m_lf & ((1ull << lane) - 1))] = ~ch;
+        sp += n_in;
+        __builtin_amdgcn_wave_barrier();
+        // ---- the round's leaf slots against every lane's own line
+        for (int i = 0; i < n_lf; ++i) {
+            const int it = leaves[i];
+            const XWNode* nd = W + (it >> 3);
+            const int sl = it & 7;
+            const bool pass = ok && child_hit_line(nd, sl, of, ivf, tau);
+            const int e0 = ~nd->child[sl], cnt = nd->cnt[sl];   // (uniform: one leaf for the wave)
+            for (int k0 = 0; k0 < cnt; k0 += (int)GI_RF_BUF / 2) {
+                const int kk = min(cnt - k0, (int)GI_RF_BUF / 2);
+                if (__ballot(nb + kk > (int)GI_RF_BUF) != 0) flush();
+                if (pass)
+                    for (int k = 0; k < kk; ++k) buf[nb++] = (int)(tag | (unsigned)sc.rc_ent[e0 + k0 + k]);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    flush();
     if (in && lane == 0) {
         f.rcnt[region] = ovf ? kRfOvf : fill;
         if (ovf) f.ovf[atomicAdd(f.cnt + 1, 1u)] = (unsigned)region;
@@ -817,27 +915,46 @@ __global__ __launch_bounds__(256) void k_rf_walk(DevScene sc, CamDev cam, TileMa
         }
     }
 }
-// the pairs' exact entity tests; each region's hitting pairs compacted in place of the region
+// the last index k in [0, n) with off[k] <= v (off ascending from off[0] = 0)
+__device__ __forceinline__ long long rf_find(const unsigned* off, long long n, long long v) {
+    long long lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const long long mid = (lo + hi + 1) >> 1;
+        if ((long long)off[mid] <= v) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+// The pairs' exact entity tests, per segment of GI_RF_SEG pairs of a region (k_rf_scan numbers them),
+// its hitting pairs compacted to the segment's start.  Persistent waves take segments in turn, so the
+// thousands of pairs of a soup-core tile are tested by many waves at once, not by one in sequence.
+#ifndef GI_RF_SEG
+#define GI_RF_SEG 512u   // pairs per segment (8 chunks of 64)
+#endif
 template <bool STATS, bool TRI>
-__global__ __launch_bounds__(256) void k_rf_hit(DevScene sc, CamDev cam, TileMap m, RFlat f, unsigned long long* stats) {
+__global__ __launch_bounds__(64) void k_rf_hit(DevScene sc, CamDev cam, TileMap m, RFlat f, unsigned long long* stats) {
     const int lane = threadIdx.x & 63;
     const long long n_regions = m.n_local;
     const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_w = ((long long)gridDim.x * blockDim.x) >> 6;
+    const long long n_seg = f.soff[n_regions];
     uint32_t nprim = 0;
-    for (long long r = gw; r < n_regions; r += n_w) {
-        const unsigned n = f.rcnt[r];
-        if (n == kRfOvf) {   // k_mode_r_batch renders this tile
-            if (lane == 0) f.hcnt[r] = 0;
-            continue;
+    long long cur = -1;
+    unsigned pg = 0, n = 0;
+    for (long long sg = gw; sg < n_seg; sg += n_w) {
+        const long long r = rf_find(f.soff, n_regions, sg);
+        if (r != cur) {
+            n = f.rcnt[r];   // (overflowed tiles have no segment)
+            pg = rf_pages_of(f, r, n, lane);
+            cur = r;
         }
-        const unsigned pg = rf_pages_of(f, r, n, lane);
+        const unsigned p0 = (unsigned)(sg - (long long)f.soff[r]) * GI_RF_SEG, p1 = min(n, p0 + GI_RF_SEG);
         unsigned kept = 0;
-        for (unsigned i0 = 0; i0 < n; i0 += 64) {
+        for (unsigned i0 = p0; i0 < p1; i0 += 64) {
             const unsigned i = i0 + lane;
             const unsigned pin = __shfl(pg, rf_page(i));
             bool hit = false;
             unsigned pr = 0;
-            if (i < n) {
+            if (i < p1) {
                 pr = *rf_pair(f, r, i, pin);
                 const unsigned slot = (unsigned)r * 64u + (pr >> 26);
                 const V3 d = rf_dir(f, slot);
@@ -845,79 +962,104 @@ __global__ __launch_bounds__(256) void k_rf_hit(DevScene sc, CamDev cam, TileMap
                 hit = ent_hit<TRI>(sc, sc.ents[pr & kRfEntMask], cam.pos, d, P, N, nprim) && sq3(P - cam.pos) < DBL_MAX;   // raytracer.h:58-65
             }
             const unsigned long long mh = __ballot(hit);
-            const unsigned k = kept + (unsigned)__popcll(mh & ((1ull << lane) - 1));
+            const unsigned k = p0 + kept + (unsigned)__popcll(mh & ((1ull << lane) - 1));
             const unsigned pout = __shfl(pg, rf_page(k));
             if (hit) *rf_pair(f, r, k, pout) = pr;   // at or before its own position, already read
             kept += (unsigned)__popcll(mh);
         }
-        if (lane == 0) f.hcnt[r] = kept;
+        if (lane == 0) {
+            f.shc[sg] = kept;
+            f.sreg[sg] = (unsigned)r;
+        }
     }
     if (STATS) wave_add_stats(stats, 0, 0, nprim, 0);
 }
-// the regions' hits in chunks of 64: coff = exclusive prefix of ceil(hcnt / 64) (one workgroup)
-__global__ __launch_bounds__(1024) void k_rf_scan(TileMap m, RFlat f) {
-    __shared__ unsigned s_part[1024];
-    const int t = threadIdx.x;
-    const long long n = m.n_local, per = (n + 1023) / 1024;
-    const long long b0 = min(n, t * per), b1 = min(n, b0 + per);
-    unsigned sum = 0;
-    for (long long r = b0; r < b1; ++r) sum += (f.hcnt[r] + 63u) / 64u;
-    s_part[t] = sum;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {   // inclusive scan of the 1024 partial sums
-        const unsigned v = t >= off ? s_part[t - off] : 0u;
+// out[k] = sum of ceil(in[j] / div) over j < k, out[n] = the total (in[j] == kRfOvf counts 0); n from
+// the device (n_dev) or the host.  One workgroup: tiles of 8192 entries, a coalesced load of their
+// counts into LDS, 8 consecutive ones per thread, wave prefix sums by shuffles, the 16 wave totals, a
+// coalesced store (the first version -- 32 strided entries per thread -- took ~50 us for the 32,400
+// tiles of a 1080p frame; this one ~15 us).
+__global__ __launch_bounds__(1024) void k_rf_scan(const unsigned* in, unsigned* out, const unsigned* n_dev, long long n_host,
+                                                 unsigned div) {
+    __shared__ unsigned s_v[8192];
+    __shared__ unsigned s_w[16];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const long long n = n_dev ? (long long)*n_dev : n_host;
+    unsigned carry = 0;
+    for (long long base = 0; base < n; base += 8192) {
+        for (int k = t; k < 8192; k += 1024) {
+            const long long r = base + k;
+            const unsigned v = r < n ? in[r] : 0u;
+            s_v[k] = v == kRfOvf ? 0u : (v + div - 1u) / div;
+        }
         __syncthreads();
-        s_part[t] += v;
+        unsigned v[8], sum = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            v[k] = s_v[8 * t + k];
+            sum += v[k];
+        }
+        unsigned incl = sum;   // inclusive prefix over the wave's lanes
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const unsigned u = __shfl_up(incl, off);
+            if (lane >= off) incl += u;
+        }
+        if (lane == 63) s_w[wv] = incl;
+        __syncthreads();
+        unsigned before = carry, tot = 0;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) {
+            before += w < wv ? s_w[w] : 0u;
+            tot += s_w[w];
+        }
+        unsigned run = before + incl - sum;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            s_v[8 * t + k] = run;
+            run += v[k];
+        }
+        __syncthreads();
+        for (int k = t; k < 8192; k += 1024) {
+            const long long r = base + k;
+            if (r < n) out[r] = s_v[k];
+        }
+        carry += tot;
         __syncthreads();
     }
-    unsigned run = t ? s_part[t - 1] : 0u;
-    for (long long r = b0; r < b1; ++r) {
-        f.coff[r] = run;
-        run += (f.hcnt[r] + 63u) / 64u;
-    }
-    if (t == 1023) f.coff[n] = s_part[1023];
+    if (t == 0) out[n] = carry;
 }
 // per hitting pair: its entity's latest reachable appearance that beats the pixel's best rank.
-// Persistent waves take 64-pair chunks of hits in turn (k_rf_scan's offsets; a chunk's region by a
-// binary search), so a region with many hits -- the soup core's tiles -- is shared by several waves.
-// One wave per workgroup: the wave's LDS holds the node-test memo (RMemo, GI_R_MEMO entries) of each
-// of the 64 pixels of the region (tile) it works on -- the pixel's pairs share their root paths'
-// upper levels; it restarts when the wave's next chunk is in another region.
+// Persistent waves take chunks of 64 consecutive hits of the whole frame in turn (hoff numbers them
+// across the segments, so chunks are full; a chunk's first segment by a binary search, each lane's
+// from there), so the hits of a soup-core tile are shared by many waves.  One wave per workgroup:
+// its LDS holds a node-test memo (RMemo, GI_R_MEMO entries) per pixel slot of a tile, each entry
+// tagged with the tile (low 8 bits: a chunk spans fewer tiles), so lanes of different tiles never
+// read each other's results and the memo is never reset.
 template <bool STATS>
 __global__ __launch_bounds__(64) void k_rf_reach(DevScene sc, CamDev cam, TileMap m, RFlat f, unsigned long long* stats) {
     __shared__ int s_memo[GI_R_MEMO > 0 ? 64 * GI_R_MEMO : 1];
     const int lane = threadIdx.x & 63;
     const long long n_regions = m.n_local;
     const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_w = ((long long)gridDim.x * blockDim.x) >> 6;
-    const long long n_chunks = f.coff[n_regions];
+    const long long n_seg = f.soff[n_regions], n_hits = f.hoff[n_seg];
+    const bool use_memo = GI_R_MEMO > 0 && sc.n_rnodes < (1 << 22);
+    if (use_memo)
+        for (int k = 0; k < GI_R_MEMO; ++k) s_memo[lane * GI_R_MEMO + k] = -1;   // (matches no key)
+    __builtin_amdgcn_wave_barrier();
     uint32_t nnode = 0;
-    long long cur = -1;
-    unsigned pg = 0;
-    for (long long c = gw; c < n_chunks; c += n_w) {
-        long long lo = 0, hi = n_regions - 1;   // the last region whose first chunk is <= c
-        while (lo < hi) {
-            const long long mid = (lo + hi + 1) >> 1;
-            if ((long long)f.coff[mid] <= c) lo = mid;
-            else hi = mid - 1;
-        }
-        const long long r = lo;
-        const unsigned n = f.hcnt[r];
-        if (r != cur) {
-            pg = rf_pages_of(f, r, n, lane);
-            if (GI_R_MEMO > 0) {
-                __builtin_amdgcn_wave_barrier();
-                for (int k = 0; k < GI_R_MEMO; ++k) s_memo[lane * GI_R_MEMO + k] = -1;   // lane = pixel of the tile
-                __builtin_amdgcn_wave_barrier();
-            }
-        }
-        cur = r;
-        const unsigned i = (unsigned)(c - (long long)f.coff[r]) * 64u + (unsigned)lane;
-        const unsigned pin = __shfl(pg, rf_page(i));
-        if (i < n) {
-            const unsigned pr = *rf_pair(f, r, i, pin);
+    for (long long c = gw; 64 * c < n_hits; c += n_w) {
+        const long long i = 64 * c + lane;
+        long long sg = rf_find(f.hoff, n_seg, 64 * c);   // the chunk's first segment (uniform)
+        if (i < n_hits) {
+            while (sg + 1 < n_seg && (long long)f.hoff[sg + 1] <= i) ++sg;   // this lane's
+            const long long r = f.sreg[sg];
+            const unsigned p = (unsigned)(sg - (long long)f.soff[r]) * GI_RF_SEG + (unsigned)(i - (long long)f.hoff[sg]);
+            const unsigned pg = p < GI_RF_S0 ? 0u : f.pt[(size_t)r * GI_RF_KMAX + rf_page(p)];
+            const unsigned pr = *rf_pair(f, r, p, pg);
             const unsigned slot = (unsigned)r * 64u + (pr >> 26);
             const int e = (int)(pr & kRfEntMask);
-            const RMemo memo{GI_R_MEMO > 0 ? s_memo + (pr >> 26) * GI_R_MEMO : nullptr};
+            const RMemo memo{use_memo ? s_memo + (pr >> 26) * GI_R_MEMO : nullptr, (int)((r & 255) << 1)};
             const V3 d = rf_dir(f, slot);
             const int a1 = sc.app_off[e + 1];
             for (int a = sc.app_off[e]; a < a1; ++a) {
@@ -1009,7 +1151,7 @@ __global__ __launch_bounds__(256) void k_mode_r(DevScene sc, CamDev cam, V3 ligh
 // live lanes have a finished ray, or when none is still traversing, so it executes with a
 // well-filled EXEC mask.  The per-path operation sequence is exactly the oracle's (pixel_mode_x in
 // oracle/gi_oracle.cpp), so results are bit-identical whatever the schedule.
-enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD = 4, PH_DONEPX = 5, PH_HELP = 6, PH_SUB = 7 };
+enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD = 4, PH_DONEPX = 5, PH_HELP = 6 };
 
 #ifndef GI_X_START_BURST
 #define GI_X_START_BURST 16   // primary rays a lane may resolve by the root test per handler run
@@ -1017,27 +1159,11 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 #ifndef GI_X_PSL
 #define GI_X_PSL 1   // 4-wave LDS kernel: path values carried across the shadow ray kept in LDS
 #endif
-#ifndef GI_X_TRAV_UNROLL
-#define GI_X_TRAV_UNROLL 1   // traversal steps per loop iteration
-#endif
 #ifndef GI_X_PAIR
 #define GI_X_PAIR 1   // LDS-resident scenes: leaf records tested two at a time (interleaved fp64 chains)
 #endif
 #ifndef GI_X_HELP
 #define GI_X_HELP 1   // HBM-resident scenes: shadow rays handed to idle lanes of the wave (XHelp)
-#endif
-#ifndef GI_X_SUBS
-#define GI_X_SUBS 0   // handoff build: most closest-hit subtrees a lane has out with idle lanes (measured slower: C4
-                      // 1.65 -> 1.96 ms with 2 or 3, 2.17 with 4 -- the owner waits on subtrees it would have culled)
-#endif
-#ifndef GI_X_LEAFQ
-// quantised-node scenes, long launches: leaf tests postponed into leaf phases (LQ, mode_x_wave):
-// C5 245 -> 229 ms in round 2; with UL (one load round trip per step for node and leaf lanes) the
-// plain step is faster again (C5 182.5 ms without LQ against 196.5 ms with it), so LQ is off
-#define GI_X_LEAFQ 0
-#endif
-#ifndef GI_X_LEAFQ_LDS
-#define GI_X_LEAFQ_LDS 0   // LDS-resident scenes: leaf postponement as above (leaf tests two at a time)
 #endif
 #ifndef GI_X_TRI
 #define GI_X_TRI 1   // 4-wave LDS kernel: triangle-only primitive tests and texture mapping (TRI)
@@ -1046,18 +1172,6 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 // HBM-resident scenes: fetch the next pop's child reference a step ahead (PF): C4 1.94 -> 1.75-1.78 ms,
 // C5 199.7 -> 198.5 ms
 #define GI_X_PREFETCH 1
-#endif
-#ifndef GI_X_PREFETCH_LDS
-#define GI_X_PREFETCH_LDS 0   // the same for LDS-resident scenes
-#endif
-#ifndef GI_X_RECULL_LEAF_HBM
-// HBM-resident scenes: re-cull popped leaves (0: a leaf's fp64 tests run against the best t as they
-// stand -- C5 208 -> 199 ms, C4 1.89 -> 1.82 ms: the re-cull's node-record fetch and ~60 instructions
-// cost more than the leaf tests it saves)
-#define GI_X_RECULL_LEAF_HBM 0
-#endif
-#ifndef GI_X_RECULL_INT_HBM
-#define GI_X_RECULL_INT_HBM 0   // HBM-resident scenes: re-cull popped interior children too
 #endif
 #ifndef GI_X_MERGE
 // 4-wave LDS kernel: a step's interior-node test and a restarted ray's root test in one block
@@ -1068,9 +1182,6 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 // UL (mode_x_wave, quantised-node HBM scenes): a step's node-test and leaf-test lanes share one load
 // round trip -- C5 196.5 -> 182.5 ms (without leaf postponement), C4 ~-1% (noise band)
 #define GI_X_UNILOAD 1
-#endif
-#ifndef GI_X_LEAF8
-#define GI_X_LEAF8 3   // LQ: leaf phase once 3/8 of the traversing lanes hold a leaf (C5 sweep 1-8)
 #endif
 #ifndef GI_X_CLIMB_CLZ
 #define GI_X_CLIMB_CLZ 1   // NST climb: the target level by a leading-zero count (C5 -2%), not a loop
@@ -1139,27 +1250,10 @@ struct XWork {
 // and the frame, bit for bit -- are the oracle's.  Per lane in LDS (column layout, 256 lanes):
 // ray[7][256] (origin, direction, tmax), own[256] (owner lane within the wave, -1: none) and
 // res[256] (the owner's answer: 0 pending, 1 lit, 2 occluded).
-// Closest-hit subtrees (GI_X_SUBS): a lane tracing a closest-hit ray while its wave has idle lanes
-// gives a pending child of its shallowest unfinished level to one of them (at most GI_X_SUBS out at a
-// time).  The helper traverses that subtree from the owner's (t, primitive) best at the hand-over
-// and leaves its own best in the owner's slot; the owner, once its own traversal ends, takes the
-// (t, primitive) minimum over its own and its slots' answers.  The closest hit is that minimum over
-// every primitive whatever the order the boxes are visited in (culling is conservative), so the
-// frame is the same bit for bit.  own[] then carries the owner lane | 0x100 | slot << 9 | child << 12;
-// snode[256] / sbest[256] the subtree's node and the starting best primitive (the starting t in
-// ray[6]); per owner and slot: st[slot][256] (t), sp[slot][256] (primitive), sf[slot][256] (done);
-// sg[256]: per owner, the least t found so far by the ray's lanes (LDS atomic min), which every one
-// of them culls with.
 struct XHelp {
     double* ray;
     int* own;
     int* res;
-    int* snode;
-    int* sbest;
-    double* st;
-    double* sg;
-    int* sp;
-    int* sf;
 };
 __device__ __forceinline__ int nth_set_bit(unsigned long long m, unsigned n) {
     for (unsigned i = 0; i < n; ++i) m &= m - 1;
@@ -1169,7 +1263,7 @@ __device__ __forceinline__ int nth_set_bit(unsigned long long m, unsigned n) {
 // NST: the wide-node index of every level of the current traversal path lives in LDS (nst[level *
 // 256], one column per lane), so climbing out of exhausted levels is one ds_read instead of a chain
 // of dependent parent-pointer loads from HBM / L2 (one per level climbed).
-template <bool STATS, bool PAIR, bool PSL, bool NST, bool HELP, bool SH, bool LQ, bool TRI, typename NodeP,
+template <bool STATS, bool PAIR, bool PSL, bool NST, bool HELP, bool SH, bool TRI, typename NodeP,
           typename HotP, typename PrimP, typename EntP>
 __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H, PrimP XP, EntP EN, double* pslot,
                                             int* nst, XHelp hp_,
@@ -1214,11 +1308,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     }
     bool pend = false;       // this lane's last shadow ray is being traced by a helper
     bool any_gave = false;   // some lane of the wave handed a shadow ray over in the last iteration
-    int howner = 0;          // PH_HELP / PH_SUB: the owner lane
-    constexpr bool SUB = HELP && NST && GI_X_SUBS > 0;
-    int nsub = 0;            // SUB: slots of this lane's closest-hit ray handed out (answered or not)
-    int hslot = 0;           // PH_SUB: the owner's slot
-    int root0 = 0;           // the node of traversal level 0 (the root; PH_SUB: the subtree's parent)
+    int howner = 0;          // PH_HELP: the owner lane
     uint32_t nnode = 0, nprim = 0, nrays = 0, nres = 0, npx = 0, nsteps = 0;
     long long idx = -1;
     int x = 0, y = 0;
@@ -1230,18 +1320,15 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     V3 o = cam.pos, d = v3(1, 0, 0);
     int dmask = 0, best = -1, node = 0, level = 0;
     bool raying = false;
-    int poff = 0, pcnt = 0;   // LQ: the pending leaf (records H[poff .. poff + pcnt)), pcnt 0: none
-    bool pdone = false;       // LQ: the ray ends once its pending leaf is tested
-    // MERGE (LDS kernel, no LQ): the step's interior-node test and a restarted ray's root test share
-    // one children_mask call at the end of the step
-    constexpr bool MERGE = GI_X_MERGE != 0 && PAIR && PSL && !LQ && !NST;
-    // UL (quantised-node HBM scenes without leaf postponement): one load round trip per step for
-    // the node-test and leaf-test lanes together
-    constexpr bool UL = GI_X_UNILOAD != 0 && !PAIR && !LQ &&
+    // MERGE (LDS kernel): the step's interior-node test and a restarted ray's root test share one
+    // children_mask call at the end of the step
+    constexpr bool MERGE = GI_X_MERGE != 0 && PAIR && PSL && !NST;
+    // UL (quantised-node HBM scenes): one load round trip per step for the node-test and leaf-test
+    // lanes together
+    constexpr bool UL = GI_X_UNILOAD != 0 && !PAIR &&
                         std::is_same<std::remove_cv_t<std::remove_pointer_t<NodeP>>, XCNode>::value;
     bool desc = false, rs = false;   // MERGE: this step descends into xch / restarts at the root
     int xch = 0;
-    const int leaf8 = ((xflags >> 12) & 15) ? ((xflags >> 12) & 15) : GI_X_LEAF8;
     uint64_t mlo = 0, mhi = 0;
     double tbest = INFINITY, tmax = INFINITY;
     float tbest_f = INFINITY;
@@ -1266,7 +1353,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             ++nprim;
             const double t = x_prim_t<TRI>(rec.h, o, d, MX_TMIN);
             const int pi = rec.h.prim;
-            if (phase != PH_CLOSEST && phase != PH_SUB) {
+            if (phase != PH_CLOSEST) {
                 if (t < tmax) { best = pi; raying = false; return; }   // any hit occludes
             } else if (t < tbest || (t == tbest && pi < best)) {
                 tbest = t;
@@ -1285,7 +1372,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 const double ta = x_prim_t<TRI>(r0.h, o, d, MX_TMIN);
                 const double tb = two ? x_prim_t<TRI>(r1.h, o, d, MX_TMIN) : INFINITY;
                 nprim += two ? 2 : 1;
-                if (phase != PH_CLOSEST && phase != PH_SUB) {
+                if (phase != PH_CLOSEST) {
                     if (ta < tmax || tb < tmax) {   // any hit occludes
                         best = ta < tmax ? r0.h.prim : r1.h.prim;
                         raying = false;
@@ -1310,7 +1397,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     // end of the step that sets up the level (descend, climb or ray start), so the pop itself waits
     // for no load: one dependent round trip per step (the child's node or leaf records) instead of
     // two.  (lvl mask, node) do not change between that fetch and the pop.
-    constexpr bool PF = PAIR ? GI_X_PREFETCH_LDS != 0 : GI_X_PREFETCH != 0;
+    constexpr bool PF = !PAIR && GI_X_PREFETCH != 0;   // (LDS-resident scenes: a ds_read away; +3% with PF)
     int pf_ch = 0, pf_cnt = 0;
     auto prefetch = [&]() {
         const uint32_t m = lvl_get<SH>(mlo, mhi, level);
@@ -1336,35 +1423,22 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 dmask = (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
                 level = 0;
                 mlo = mhi = 0;
-                if (SUB && (ow & 0x100)) {   // a closest-hit subtree: child (ow >> 12) of node snode
-                    hslot = (ow >> 9) & 7;
-                    tmax = INFINITY;
-                    tbest = r[1536];
-                    tbest_f = tbest < INFINITY ? up32(tbest) : INFINITY;
-                    best = hp_.sbest[tid];
-                    phase = PH_SUB;
-                    root0 = hp_.snode[tid];
-                    node = root0;
-                    lvl_set<SH>(mlo, mhi, 0, 1u << ((ow >> 12) & 7));
-                    raying = true;
-                } else {                     // a shadow ray
-                    tmax = r[1536];
-                    tbest = tmax;
-                    tbest_f = up32(tmax);
-                    phase = PH_HELP;
-                    best = -1;
-                    const uint32_t rm = children_mask<PAIR>(W, of, ivf, tbest_f, dmask);
-                    root0 = 0;
-                    node = 0;
-                    lvl_set<SH>(mlo, mhi, 0, rm);
-                    raying = rm != 0;
-                }
+                // a shadow ray
+                tmax = r[1536];
+                tbest = tmax;
+                tbest_f = up32(tmax);
+                phase = PH_HELP;
+                best = -1;
+                const uint32_t rm = children_mask<PAIR>(W, of, ivf, tbest_f, dmask);
+                node = 0;
+                lvl_set<SH>(mlo, mhi, 0, rm);
+                raying = rm != 0;
                 if (PF && raying) prefetch();
             }
         }
         const unsigned long long m_live = __ballot(phase != PH_DEAD);
         if (m_live == 0) break;
-        unsigned long long m_idle = HELP ? ~m_live : 0ull;   // lanes free to take a shadow ray
+        const unsigned long long m_idle = HELP ? ~m_live : 0ull;   // lanes free to take a shadow ray
         bool gave = false;
         const bool trav = raying;
         const unsigned long long m_trav = __ballot(trav);
@@ -1387,33 +1461,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
         }
         const uint64_t t0 = STATS ? clock64() : 0;
         if (STATS) ++cnt.path_it;
-        // LQ (leaf postponement): a lane whose step reaches a leaf keeps it pending; the wave then
-        // runs node steps for the other lanes until leaf8 eighths (xflags bits 12-15, GI_X_LEAF8
-        // when 0) of its traversing lanes hold a pending leaf, and tests them in one leaf phase:
-        // node tests and fp64 primitive tests no longer share one divergent step.  Each lane's own
-        // sequence of node and leaf operations is unchanged (it pops nothing while a leaf is
-        // pending), so results and work counters are the same.
-        bool leaf_phase = false;
-        if constexpr (LQ) {
-            const unsigned long long m_pl = __ballot(trav && pcnt > 0);
-            leaf_phase = m_pl != 0 && (m_pl == m_trav || 8 * __popcll(m_pl) >= leaf8 * __popcll(m_trav));
-        }
         if (trav) {
-            // up to GI_X_TRAV_UNROLL steps per loop iteration: the scheduling ballots and the handler
-            // decision are paid once per iteration (a lane whose ray ends stops stepping)
-#pragma unroll 1
-            for (int u = 0; u < GI_X_TRAV_UNROLL; ++u) {
-            if (u > 0 && !raying) break;
-            if (LQ && leaf_phase) {
-                if (pcnt > 0) {   // the pending leaf's fp64 primitive tests
-                    leaf_test(H + poff, pcnt);
-                    pcnt = 0;
-                    if (pdone) {   // the step that popped this leaf exhausted the ray's last level
-                        pdone = false;
-                        raying = false;
-                    }
-                }
-            } else if (!LQ || pcnt == 0) {
             if (STATS) {
                 ++nsteps;
                 ++cnt.path_st;
@@ -1421,11 +1469,6 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             // ---- one traversal step (stackless: 8-bit "children left" mask per level).  Invariant:
             // the current level has a child left; the step pops it, then climbs past exhausted
             // levels, so a ray ends in the step that exhausts the root level (no empty iteration).
-            const double tb0 = tbest;
-            if (SUB && (phase == PH_SUB || nsub > 0)) {   // the best t of the ray's lanes culls too
-                const double gb = hp_.sg[phase == PH_SUB ? wbase + howner : tid];
-                if (gb < tbest) tbest_f = up32(gb);
-            }
             const auto* nd = W + node;
             const uint32_t msk = lvl_get<SH>(mlo, mhi, level);
             const int kc = __builtin_ctz(msk);         // next child in front-to-back order
@@ -1435,14 +1478,13 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             xch = ch;
             desc = false;
             // a closer hit may have arrived since the mask was computed: re-cull this child -- in
-            // the LDS kernel only (GI_X_RECULL_*_HBM 0): in HBM-resident scenes an interior child's
-            // own node test culls its children against the same t, and skipping the re-cull drops a
-            // node-record fetch and ~60 instructions from the step (C5 214 -> 199 ms, C4 1.96 ->
-            // 1.82; the LDS kernel, whose re-cull is cheaper than a node test, keeps it: C3 +0.9%
-            // without)
+            // the LDS kernel only: in HBM-resident scenes an interior child's own node test culls its
+            // children against the same t, and skipping the re-cull drops a node-record fetch and ~60
+            // instructions from the step (round 3: C5 214 -> 199 ms, C4 1.96 -> 1.82; leaves: their
+            // fp64 tests run against the best t as it stands; the LDS kernel, whose re-cull is cheaper
+            // than a node test, keeps it: C3 +0.9% without)
             bool keep = true;
-            if ((phase == PH_CLOSEST || phase == PH_SUB) && best >= 0 && (PAIR || GI_X_RECULL_INT_HBM || (ch < 0 && GI_X_RECULL_LEAF_HBM)))
-                keep = child_hit(nd, c, of, ivf, tbest_f);
+            if (PAIR && phase == PH_CLOSEST && best >= 0) keep = child_hit(nd, c, of, ivf, tbest_f);
             if (STATS) {
                 const unsigned long long mn = __ballot(keep && ch >= 0), ml = __ballot(keep && ch < 0);
                 if (lane == 0) {
@@ -1452,7 +1494,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     cnt.ln_leaf += __popcll(ml);
                 }
             }
-            if (UL && keep) {   // (keep is false only under the GI_X_RECULL_*_HBM A/B knobs)
+            if (UL) {   // (keep is always true in HBM-resident scenes: no re-cull)
                 // one memory round trip for the wave's node-test AND leaf-test lanes: each lane's
                 // load (the child's 64 slab bytes, or its leaf's first record) is issued before
                 // either test waits, instead of a node-test block and a leaf-test block each
@@ -1480,10 +1522,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     }
                 }
             } else if (keep) {
-                if (LQ && ch < 0) {       // leaf: pending until the wave's next leaf phase
-                    poff = ~ch;
-                    pcnt = PF ? pf_cnt : (int)nd->cnt[c];
-                } else if (ch < 0) {      // leaf: fp64 primitive tests (these decide the result)
+                if (ch < 0) {             // leaf: fp64 primitive tests (these decide the result)
                     leaf_test(H + ~ch, PF ? pf_cnt : (int)nd->cnt[c]);
                 } else if (MERGE) {       // the node test runs below, shared with the restarts
                     desc = true;
@@ -1498,9 +1537,6 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     }
                 }
             }
-            if (SUB && tbest < tb0 && (phase == PH_SUB || nsub > 0))   // (t > 0: its bits order as t)
-                atomicMin(reinterpret_cast<unsigned long long*>(hp_.sg + (phase == PH_SUB ? wbase + howner : tid)),
-                          (unsigned long long)__double_as_longlong(tbest));
             if (raying && !desc) {        // climb to the nearest level with children left
                 uint32_t rest = lvl_get<SH>(mlo, mhi, level);
                 if constexpr (NST) {
@@ -1517,7 +1553,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                             rest = lvl_get<SH>(mlo, mhi, level);
                         } while (rest == 0 && level > 0);
 #endif
-                        node = level == 0 ? root0 : nst[level * 256];
+                        node = level == 0 ? 0 : nst[level * 256];
                     }
                 } else {
                     while (rest == 0 && level > 0) {
@@ -1526,13 +1562,9 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                         rest = lvl_get<SH>(mlo, mhi, level);
                     }
                 }
-                if (rest == 0) {          // ray finished (after its pending leaf, if any)
-                    if (LQ && pcnt > 0) pdone = true;
-                    else raying = false;
-                }
+                if (rest == 0) raying = false;   // ray finished
             }
-            if (PF && raying && !pdone && !desc) prefetch();   // (MERGE: descending lanes below)
-            }
+            if (PF && raying && !desc) prefetch();   // (MERGE: descending lanes below)
             // a finished shadow ray whose path continues: resolve it and start the next bounce
             // right here (the bounce direction was drawn when the hit was shaded), so the lane
             // keeps traversing instead of waiting for the shading handler (short-traversal scenes;
@@ -1598,51 +1630,6 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 rs = false;
                 desc = false;
             }
-            }
-        }
-        if (SUB && phase == PH_SUB && !raying) {   // a finished subtree: its answer, at once; idle again
-            const int si = hslot * 256 + wbase + howner;
-            hp_.st[si] = tbest;
-            hp_.sp[si] = best;
-            __builtin_amdgcn_wave_barrier();
-            hp_.sf[si] = 1;
-            phase = PH_DEAD;
-            root0 = 0;
-        }
-        // SUB: closest-hit lanes give a pending child of their shallowest unfinished level (above the
-        // current one) to an idle lane -- the k-th giver the k-th idle lane
-        if (SUB && handoff && m_idle) {
-            int gl = -1;
-            if (phase == PH_CLOSEST && raying && nsub < GI_X_SUBS && level > 0) {
-                const uint64_t lm = level >= 8 ? mlo : mlo & ((1ull << (8 * level)) - 1);
-                const uint64_t hm = (SH || level <= 8) ? 0ull : mhi & ((1ull << (8 * (level - 8))) - 1);
-                gl = lm ? __builtin_ctzll(lm) / 8 : hm ? 8 + __builtin_ctzll(hm) / 8 : -1;
-            }
-            const unsigned long long m_want = __ballot(gl >= 0);
-            if (m_want) {
-                const unsigned n_idle = (unsigned)__popcll(m_idle);
-                if (gl >= 0) {
-                    const unsigned r = (unsigned)__popcll(m_want & ((1ull << lane) - 1));
-                    if (r < n_idle) {
-                        const int ht = wbase + nth_set_bit(m_idle, r);
-                        const uint32_t gm = lvl_get<SH>(mlo, mhi, gl);
-                        const int kc = __builtin_ctz(gm);
-                        lvl_set<SH>(mlo, mhi, gl, gm & (gm - 1));
-                        double* hr = hp_.ray + ht;
-                        hr[0] = o.x; hr[256] = o.y; hr[512] = o.z;
-                        hr[768] = d.x; hr[1024] = d.y; hr[1280] = d.z;
-                        hr[1536] = tbest;
-                        hp_.snode[ht] = gl == 0 ? root0 : nst[gl * 256];
-                        hp_.sbest[ht] = best;
-                        hp_.sf[nsub * 256 + tid] = 0;
-                        if (nsub == 0) hp_.sg[tid] = tbest;
-                        hp_.own[ht] = lane | 0x100 | (nsub << 9) | (kc << 12);
-                        ++nsub;
-                        gave = true;
-                    }
-                }
-                for (unsigned i = min(n_idle, (unsigned)__popcll(m_want)); i > 0; --i) m_idle &= m_idle - 1;
-            }
         }
         const uint64_t t1 = STATS ? clock64() : 0;
         uint64_t t2 = t1;
@@ -1654,21 +1641,6 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
         bool hold = false;   // an owner whose helper has not answered yet: no handling this time
         if (HELP) {
             __builtin_amdgcn_wave_barrier();
-            if (SUB && handle && phase == PH_CLOSEST && nsub > 0) {
-                // the ray's subtrees: once all have answered, the (t, primitive) minimum
-                bool all = true;
-                for (int s2 = 0; s2 < nsub; ++s2) all = all && hp_.sf[s2 * 256 + tid] != 0;
-                if (!all) {
-                    hold = true;
-                } else {
-                    for (int s2 = 0; s2 < nsub; ++s2) {
-                        const double t = hp_.st[s2 * 256 + tid];
-                        const int pi = hp_.sp[s2 * 256 + tid];
-                        if (t < tbest || (t == tbest && pi < best)) { tbest = t; best = pi; }
-                    }
-                    nsub = 0;
-                }
-            }
             if (handle && pend) {
                 const int r = hp_.res[tid];
                 if (r == 0) {
@@ -2020,32 +1992,24 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
         // (occluded sum, next direction, throughput T, RNG key) live in a per-lane LDS slot after
         // the scene instead of in VGPRs / scratch
         double* pslot = reinterpret_cast<double*>(lds_scene + nw + nh + np + ne) + 10 * threadIdx.x;
-        mode_x_wave<STATS, GI_X_PAIR != 0, W4 && GI_X_PSL, false, false, SH, GI_X_LEAFQ_LDS != 0, W4 && GI_X_TRI>(sc, W, H, XP, EN, pslot, nullptr, XHelp{},
+        mode_x_wave<STATS, GI_X_PAIR != 0, W4 && GI_X_PSL, false, false, SH, W4 && GI_X_TRI>(sc, W, H, XP, EN, pslot, nullptr, XHelp{},
                                                                         cam, light, m, spp, depth, seed, rgb, rgb8, blk,
                                                                         wk, handle8, xflags, c);
     } else {
         // dynamic LDS: GI_X_NSTK's 16 levels x 256 lanes of node indices, then GI_X_HELP's handoff
-        // slots (7 x 256 doubles, 2 x 256 ints) and GI_X_SUBS's (2 x 256 ints, 256 doubles per slot,
-        // 256 doubles of shared best t, 2 x 256 ints per slot)
+        // slots (7 x 256 doubles, 2 x 256 ints)
         extern __shared__ int lds_nst[];
         XHelp hp;
         hp.ray = reinterpret_cast<double*>(lds_nst + (GI_X_NSTK ? 16 * 256 : 0));
         hp.own = reinterpret_cast<int*>(hp.ray + 7 * 256);
         hp.res = hp.own + 256;
-        hp.snode = hp.res + 256;   // GI_X_SUBS: the subtree hand-over and the owners' slots
-        hp.sbest = hp.snode + 256;
-        hp.st = reinterpret_cast<double*>(hp.sbest + 256);
-        hp.sg = hp.st + GI_X_SUBS * 256;
-        hp.sp = reinterpret_cast<int*>(hp.sg + 256);
-        hp.sf = hp.sp + GI_X_SUBS * 256;
-        if constexpr (CN)   // quantised nodes (the default for large HBM-resident scenes); LQ in
-                            // long launches (the handoff build's short launches are latency-bound)
-            mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0, SH, GI_X_LEAFQ != 0 && !W4, TR && GI_X_TRI>(sc, sc.xcnodes, sc.xhot, sc.xprims,
+        if constexpr (CN)   // quantised nodes (the default for large HBM-resident scenes)
+            mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0, SH, TR && GI_X_TRI>(sc, sc.xcnodes, sc.xhot, sc.xprims,
                                                                             sc.ents, nullptr, lds_nst + threadIdx.x, hp,
                                                                             cam, light, m, spp, depth, seed, rgb, rgb8,
                                                                             blk, wk, handle8, xflags, c);
         else
-            mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0, SH, false, TR && GI_X_TRI>(sc, sc.xwnodes, sc.xhot, sc.xprims,
+            mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0, SH, TR && GI_X_TRI>(sc, sc.xwnodes, sc.xhot, sc.xprims,
                                                                             sc.ents, nullptr, lds_nst + threadIdx.x, hp,
                                                                             cam, light, m, spp, depth, seed, rgb, rgb8,
                                                                             blk, wk, handle8, xflags, c);
@@ -2220,7 +2184,7 @@ long long shard_tiles(int w, int h, int shard_count) { return make_map(w, h, sha
 // overrides the shading-handler threshold, GI_X_FLAGS the schedule flags, GI_X_MAX_RUN the largest
 // work-unit run length (scenes of cheap background samples such as the main.cpp scene prefer 8).
 struct XEnv {
-    int lds = 1, h8 = 0, xf = -1, run_log2 = 0, help = 1, spread = -1, leaf8 = 0, wf = -1;
+    int lds = 1, h8 = 0, xf = -1, run_log2 = 0, help = 1, spread = -1, wf = -1;
     int r_flat = -1;                  // Mode R kernels (GI_R_FLAT): 1 the flat phases for every scene, 0 k_mode_r
                                       // for every scene, 2 k_mode_r_batch for the whole frame (tests); -1 by size
     long long wf_chunk = 8ll << 20;   // wavefront Mode X: units (pixel samples) per chunk = queue capacity
@@ -2237,7 +2201,6 @@ const XEnv& x_env() {
         if (const char* v = std::getenv("GI_X_SPREAD")) env.spread = std::atoi(v);
         if (const char* v = std::getenv("GI_R_FLAT")) env.r_flat = std::atoi(v);
         if (const char* v = std::getenv("GI_RF_PER_SLOT")) env.rf_per_slot = std::max(0, std::min(1024, std::atoi(v)));
-        if (const char* v = std::getenv("GI_X_LEAF8")) env.leaf8 = std::max(0, std::min(8, std::atoi(v)));
         if (const char* v = std::getenv("GI_X_WF")) env.wf = std::atoi(v);
         if (const char* v = std::getenv("GI_X_WF_CHUNK")) env.wf_chunk = std::max(1ll << 16, std::min(1ll << 30, std::atoll(v)));
         const char* v = std::getenv("GI_X_MAX_RUN");
@@ -2283,6 +2246,7 @@ int x_env_rf_per_slot() { return x_env().rf_per_slot; }
 unsigned rf_own_pairs() { return GI_RF_S0; }
 unsigned rf_page_pairs() { return GI_RF_PAGE; }
 unsigned rf_max_pages() { return GI_RF_KMAX; }
+unsigned rf_seg_pairs() { return GI_RF_SEG; }
 // Mode R kernel of a launch: 0 k_mode_r (one lane per pixel; small scenes, the reverse-DFS flag, an
 // octree that never split), 1 the flat phases (scenes of more than 4096 entities; their overflowed
 // tiles through k_mode_r_batch), 2 k_mode_r_batch for the whole frame (GI_R_FLAT=2, tests; and
@@ -2299,8 +2263,7 @@ hipError_t x_launch_config(const DevScene& sc, int device, XLaunchCfg& cfg) {
     const bool lds = x_env().lds != 0 && sc.x_lds_bytes > 0;
     cfg.lds_bytes = lds ? (size_t)sc.x_lds_bytes + ((sc.x_waves4 && GI_X_PSL) ? 256 * 10 * sizeof(double) : 0)
                         : (GI_X_NSTK ? 16 * 256 * sizeof(int) : 0) +
-                              (GI_X_HELP ? 256 * (7 * sizeof(double) + 2 * sizeof(int)) : 0) +
-                              (GI_X_HELP && GI_X_SUBS ? 256 * (2 * sizeof(int) + sizeof(double) + GI_X_SUBS * (sizeof(double) + 2 * sizeof(int))) : 0);
+                              (GI_X_HELP ? 256 * (7 * sizeof(double) + 2 * sizeof(int)) : 0);
     cfg.kv = 2 * (int)lds + ((lds && sc.x_waves4) ? 1 : 0);   // 0 / 1 (per launch, HELP): HBM-resident
     int cus = 0, per_cu = 0;
     hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
@@ -2352,19 +2315,21 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
         mark(ev_begin);
         if (rk == 1 && xs.rf_pairs && xs.rf_slots >= m.n_local * (kTile * kTile)) {   // flat phases
             const RFlat f{xs.rf_pairs, xs.rf_pairs + (size_t)(xs.rf_slots / 64) * GI_RF_S0, xs.rf_pt, xs.rf_best, xs.rf_cnt,
-                          xs.rf_ovf, xs.rf_rcnt, xs.rf_hcnt, xs.rf_coff, xs.rf_dir, xs.rf_pages};
+                          xs.rf_ovf, xs.rf_rcnt, xs.rf_soff, xs.rf_shc, xs.rf_sreg, xs.rf_hoff, xs.rf_dir, xs.rf_pages};
             const dim3 pgrid((unsigned)((m.n_local * (kTile * kTile) + 255) / 256)), fgrid(4096);
             hipError_t e1 = hipMemsetAsync(xs.rf_cnt, 0, 2 * sizeof(unsigned), stream);
             if (e1 != hipSuccess) return e1;
             // the overflowed tiles' fallback: half a tile per workgroup item, a grid that returns at once
             // when the list is empty
             const dim3 bgrid((unsigned)std::min<long long>(2 * m.n_local, 2048));
+            const dim3 hgrid(16384);   // k_rf_hit: persistent waves (one per workgroup) over the segments
             if (stats) hipLaunchKernelGGL(k_rf_walk<true>, pgrid, block, 0, stream, sc, cam, m, tau, f, st);
             else hipLaunchKernelGGL(k_rf_walk<false>, pgrid, block, 0, stream, sc, cam, m, tau, f, st);
 #define GI_LAUNCH_RF(S, T)                                                                                                \
     do {                                                                                                                  \
-        hipLaunchKernelGGL((k_rf_hit<S, T>), fgrid, block, 0, stream, sc, cam, m, f, st);                                 \
-        hipLaunchKernelGGL(k_rf_scan, dim3(1), dim3(1024), 0, stream, m, f);                                              \
+        hipLaunchKernelGGL(k_rf_scan, dim3(1), dim3(1024), 0, stream, f.rcnt, f.soff, nullptr, m.n_local, GI_RF_SEG);    \
+        hipLaunchKernelGGL((k_rf_hit<S, T>), hgrid, dim3(64), 0, stream, sc, cam, m, f, st);                              \
+        hipLaunchKernelGGL(k_rf_scan, dim3(1), dim3(1024), 0, stream, f.shc, f.hoff, f.soff + m.n_local, 0ll, 1u);       \
         hipLaunchKernelGGL(k_rf_reach<S>, dim3(4 * fgrid.x), dim3(64), 0, stream, sc, cam, m, f, st);                     \
         hipLaunchKernelGGL((k_rf_shade<S, T>), pgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, f, st);             \
         hipLaunchKernelGGL((k_mode_r_batch<S, T>), bgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau,        \
@@ -2424,7 +2389,7 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
         // length (log2, bits 8-10)
         const int xf = (env.xf >= 0 ? env.xf : sc.x_flags) | (env.run_log2 << 8) |
                        ((o.flags & GI_FLAG_X_NO_SHADOW) ? 4 : 0) | (env.help ? 8 : 0) |
-                       ((env.spread > 0 || (env.spread < 0 && help)) ? 16 : 0) | (env.leaf8 << 12);
+                       ((env.spread > 0 || (env.spread < 0 && help)) ? 16 : 0);
         if (form) {   // gi_wf.hip's forms, timed as one pass
             if (!xs.wcnt || (form == 1 && (!xs.wq[0] || !xs.wq[1] || !xs.h_nlist || xs.wcap <= 0))) return hipErrorInvalidValue;
             e = launch_wf(sc, xc.kv, xc.wf_lds_bytes, form == 2 ? xc.seg_resident : xc.wf_resident, form, cam, light, w, h, y0,

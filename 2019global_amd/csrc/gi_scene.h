@@ -238,7 +238,7 @@ struct XScratch {
     // of GI_RF_S0, then the pool of rf_pages pages of GI_RF_PAGE (rf_pairs holds both); per tile its
     // pool page ids (GI_RF_KMAX), its pairs / hits and its first chunk of hits; per pixel slot the best
     // rank + 1 and the primary direction; the counters (pool pages taken, overflowed tiles) and the
-    // overflowed tiles' list.  Sized for rf_slots pixel slots.
+    // overflowed tiles' list; the segment offsets and hit counts.  Sized for rf_slots pixel slots.
     unsigned* rf_pairs = nullptr;
     unsigned* rf_pt = nullptr;
     unsigned long long* rf_best = nullptr;
@@ -246,8 +246,10 @@ struct XScratch {
     unsigned* rf_cnt = nullptr;
     unsigned* rf_ovf = nullptr;
     unsigned* rf_rcnt = nullptr;
-    unsigned* rf_hcnt = nullptr;
-    unsigned* rf_coff = nullptr;
+    unsigned* rf_soff = nullptr;    // per tile + 1: its first segment of pairs (k_rf_hit's unit)
+    unsigned* rf_shc = nullptr;     // per segment: its hits
+    unsigned* rf_sreg = nullptr;    // per segment: its tile
+    unsigned* rf_hoff = nullptr;    // per segment + 1: the hits before it (k_rf_reach's chunks of 64)
     unsigned rf_pages = 0;
     long long rf_slots = 0;
     size_t rf_bytes = 0;

@@ -39,11 +39,6 @@ namespace {
 #ifndef GI_WF_PAIR
 #define GI_WF_PAIR 1   // LDS-resident scenes: leaf records tested two at a time (two interleaved fp64 chains)
 #endif
-#ifndef GI_WF_SKIP
-// closest-hit traversal, LDS scenes: re-culled siblings skipped within one step -- measured slower
-// (k_seg C3 5.31 -> 5.39 ms, C2 0.161 -> 0.170, X-zoo 4.39 -> 4.48: a longer divergent step)
-#define GI_WF_SKIP 0
-#endif
 #ifndef GI_WF_TAKE
 #define GI_WF_TAKE 16   // most 64-entry batches a wave takes per atomic on the queue's counter
 #endif
@@ -101,19 +96,10 @@ __device__ __forceinline__ int wf_trace(NodeP W, HotP H, V3 o, V3 d, double tmax
         const uint32_t msk = lvl_get<SH>(mlo, mhi, level);
         const int kc = __builtin_ctz(msk);   // next child in front-to-back order
         lvl_set<SH>(mlo, mhi, level, msk & (msk - 1));
-        int c = kc ^ dmask;
+        const int c = kc ^ dmask;
         bool keep = true;
         if (!ANY && !NST && best >= 0) {   // (LDS scenes) re-cull against the current best t
             keep = child_hit(nd, c, of, ivf, tbf);
-            if (GI_WF_SKIP) {   // culled siblings are passed over inside this step, not one per step
-                uint32_t rest = lvl_get<SH>(mlo, mhi, level);
-                while (!keep && rest) {
-                    c = __builtin_ctz(rest) ^ dmask;
-                    rest &= rest - 1;
-                    lvl_set<SH>(mlo, mhi, level, rest);
-                    keep = child_hit(nd, c, of, ivf, tbf);
-                }
-            }
         }
         const int ch = nd->child[c];
         if (keep) {
@@ -516,9 +502,6 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
 #ifndef GI_SEG_BURST
 #define GI_SEG_BURST 16
 #endif
-#ifndef GI_SEG_PREFETCH
-#define GI_SEG_PREFETCH 0   // k_seg: a run's work-list entries fetched when it is taken (lane shuffles)
-#endif
 #ifndef GI_SEG_TAKE
 #define GI_SEG_TAKE 4   // k_seg: most batches of 64 units per run (one atomic per run)
 #endif
@@ -540,11 +523,6 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
     const unsigned long long run = 64ull * (unsigned long long)max(1ll, min((long long)GI_SEG_TAKE, (long long)(total / (64ull * 8ull * n_waves))));
     uint32_t nnode = 0, nprim = 0, nrays = 0, nres = 0, npx = 0;
     unsigned long long cur = 0, cur_end = 0;   // the wave's unhanded units [cur, cur_end) (uniform)
-    // the work-list entries of the current run's pixels, lane k holding pixel p0 + k (fetched when the
-    // run is taken, so a refill reads its pixel with a lane shuffle instead of a dependent load);
-    // np > 64 (runs of more than 64 pixels): read from the list instead
-    unsigned lst = 0;
-    unsigned long long p0 = 0, np = 0;
     bool exhausted = false;                    // the frame's units are all handed out (uniform)
     bool live = false;                         // this lane carries a path
     unsigned li = 0, smp = 0;
@@ -565,9 +543,6 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
             const unsigned n_need = (unsigned)__popcll(m_need);
             unsigned long long u = ~0ull;
             const unsigned long long avail = cur_end - cur;
-            bool from_new = false;
-            unsigned lst_new = 0;
-            unsigned long long p0_new = 0, np_new = 0;
             if (n_need > avail && !exhausted) {   // a new run of units for the lanes beyond it
                 unsigned long long nb = 0;
                 if (lane == 0) nb = atomicAdd(reinterpret_cast<unsigned long long*>(a.take), run);
@@ -578,12 +553,9 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
                     cur = cur_end;
                 } else {
                     const unsigned long long ne = min(total, nb + run);
-                    p0_new = nb / (unsigned long long)spp;
-                    np_new = (ne - 1) / (unsigned long long)spp - p0_new + 1;
-                    if (GI_SEG_PREFETCH && np_new <= 64 && (unsigned long long)lane < np_new) lst_new = a.list[p0_new + lane];
                     if (!live) {
                         if (rank < avail) u = cur + rank;
-                        else if (nb + (rank - avail) < ne) { u = nb + (rank - avail); from_new = true; }
+                        else if (nb + (rank - avail) < ne) u = nb + (rank - avail);
                     }
                     cur = min(ne, nb + (n_need - avail));
                     cur_end = ne;
@@ -603,19 +575,10 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
                     smp_u = (unsigned)(u - (unsigned long long)li_u * (unsigned long long)spp);
                 }
             }
-            // the new unit's pixel from the prefetched entries (shuffles run in every lane)
-            const unsigned ps_cur = __shfl(lst, (int)((li_u - p0) & 63));
-            const unsigned ps_new = __shfl(lst_new, (int)((li_u - p0_new) & 63));
-            const bool pre = GI_SEG_PREFETCH && (from_new ? np_new <= 64 : np <= 64);   // (np: the unit's run)
-            if (np_new) {   // a run was taken: it is the current one from now on
-                lst = lst_new;
-                p0 = p0_new;
-                np = np_new;
-            }
             if (!live && u != ~0ull) {
                 li = li_u;
                 smp = smp_u;
-                const unsigned ps = pre ? (from_new ? ps_new : ps_cur) : a.list[li];
+                const unsigned ps = a.list[li];   // (prefetching a run's entries into lanes: +3%, round 4)
                 const V3 d0 = wf_primary(cam, m, ps, spp, seed, li, smp, idx, key);
                 if (smp == 0) ++npx;
                 if (wf_primary_misses(sc, cam, d0)) {

@@ -9,6 +9,10 @@
 #   profiles/r05.sh rab <spec> ...             Mode R: parity subset, then R-C4 / R-C3 bench lines
 #   profiles/r05.sh benchq <wls,> [steps]      quick bench lines (kernel ms, schedule block)
 #   profiles/r05.sh tk <pytest -k expr> [wls,]  GPU tests selected by -k, then quick bench lines
+#   profiles/r05.sh ktrace <wls,> <spec> ...    rocprofv3 --kernel-trace --stats of the bench (5 frames):
+#                                              every kernel's calls and average us
+#   profiles/r05.sh ab <wls,> <spec> ...        bench lines (kernel ms, ms/frame) per workload and spec,
+#                                              interleaved twice (spec order ABAB) against drift
 #   profiles/r05.sh evidence 1|2|forms         1: GPU suite + rocprofv3 stats/PMC of the default kernels
 #                                              (C3 C2 C4 R-C4 C5, or $WLS); 2: shard probes, bench lines
 #                                              of every workload, the C3 bench with its CPU baseline, the
@@ -64,11 +68,44 @@ benchq)
     timeout -k 10 200 python3 bench.py --workload $W --steps ${2:-5} --warmup 1 --no-cpu-baseline --no-host-path > $O/bench_$W.json 2> $O/bench_$W.err || { echo "bench $W failed"; tail -5 $O/bench_$W.err; exit 1; }
     python3 -c "import json; d=json.loads(open('$O/bench_$W.json').read().strip().splitlines()[-1]); print('$W', d['roofline']['kernel'], d['roofline']['kernel_ms'], d['ms_per_step'], d['value'], json.dumps(d.get('schedule')))"
   done ;;
+ab)
+  O=gpurun_out/r05ab; mkdir -p $O
+  WL=${1//,/ }; shift
+  for REP in 1 2; do
+  for SPEC in "$@"; do
+    V=${SPEC%%:*}; E=""; [[ "$SPEC" == *:* ]] && E=${SPEC#*:}; E=${E//,/ }
+    T=${V}_$(echo "$E" | tr ' =' '_-')
+    for W in $WL; do
+      env GI_LIB=$(lib $V) $E timeout -k 10 200 python3 bench.py --workload $W --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline --no-host-path > $O/${W}_$T.json 2> $O/${W}_$T.err || { echo "bench fail $SPEC $W"; tail -5 $O/${W}_$T.err; exit 1; }
+      python3 -c "import json; d=json.loads(open('$O/${W}_$T.json').read().strip().splitlines()[-1]); print('%-34s %-6s kernel %.4f ms  frame %.4f ms' % ('$SPEC', '$W', d['roofline']['kernel_ms'], d['ms_per_step']))"
+    done
+  done
+  done ;;
+ktrace)
+  O=$GRAFT_REPO_ROOT/gpurun_out/r05kt; mkdir -p $O
+  WL=${1//,/ }; shift
+  export TMPDIR=/tmp
+  for SPEC in "$@"; do
+    V=${SPEC%%:*}; E=""; [[ "$SPEC" == *:* ]] && E=${SPEC#*:}; E=${E//,/ }
+    T=${V}_$(echo "$E" | tr ' =' '_-')
+    for W in $WL; do
+      D=$O/${W}_$T
+      ( cd /tmp && env GI_LIB=$(lib $V) $E timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o run -- python3 $GRAFT_REPO_ROOT/bench.py --workload $W --steps 5 --warmup 1 --no-cpu-baseline --no-host-path > $D.log 2>&1 ) || { echo "ktrace fail $SPEC $W"; tail -5 $D.log; exit 1; }
+      python3 - "$D" "$SPEC" "$W" <<'PY'
+import csv, glob, sys
+f = glob.glob(sys.argv[1] + "/**/run_kernel_stats.csv", recursive=True)[0]
+for r in csv.DictReader(open(f)):
+    n = r["Name"].replace("void gi::(anonymous namespace)::", "").replace("gi::(anonymous namespace)::", "").split("(gi::")[0]
+    if float(r["TotalDurationNs"]) > 20000:
+        print("%-26s %-6s %-60s calls %4d  avg %9.1f us" % (sys.argv[2], sys.argv[3], n[:60], int(r["Calls"]), float(r["AverageNs"]) / 1e3))
+PY
+    done
+  done ;;
 tk)
   O=gpurun_out/r05tk; mkdir -p $O
   timeout -k 10 500 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$1" > $O/tests.log 2>&1 || { grep -E "FAILED|Error|error" $O/tests.log | head -20; tail -30 $O/tests.log; exit 1; }
   tail -1 $O/tests.log
-  [ -n "$2" ] && bash $0 benchq $2
+  if [ -n "$2" ]; then bash $0 benchq $2; fi
   ;;
 evidence)
   O=gpurun_out/r05ev; mkdir -p $O
