@@ -89,7 +89,7 @@ class Opts(ctypes.Structure):
     _fields_ = [("mode", ctypes.c_int32), ("spp", ctypes.c_int32), ("depth", ctypes.c_int32),
                 ("shard_count", ctypes.c_int32), ("shard_index", ctypes.c_int32), ("band_rows", ctypes.c_int32),
                 ("flags", ctypes.c_uint32), ("reserved", ctypes.c_int32), ("seed", ctypes.c_uint64),
-                ("stats", ctypes.c_void_p)]
+                ("stats", ctypes.c_void_p), ("sample_begin", ctypes.c_int32), ("sample_end", ctypes.c_int32)]
 
 
 class SceneInfo(ctypes.Structure):
@@ -450,19 +450,22 @@ class DeviceScene:
 
     @staticmethod
     def opts(mode=MODE_R, spp=1, depth=1, seed=0, shard_count=1, shard_index=0, band_rows=0, stats_ptr=0,
-             flags=0) -> Opts:
+             flags=0, samples=None) -> Opts:
+        """samples=(begin, end): a progressive pass of Mode X samples [begin, end) (gi.h gi_opts)."""
         o = Opts()
         o.mode, o.spp, o.depth, o.seed = mode, spp, depth, seed
         o.shard_count, o.shard_index, o.band_rows = shard_count, shard_index, band_rows
         o.flags = (FLAG_STATS if stats_ptr else 0) | flags
         o.stats = stats_ptr or None
+        if samples is not None:
+            o.sample_begin, o.sample_end = samples
         return o
 
     def render(self, cam: Camera, light, w: int, h: int, mode=MODE_R, spp=1, depth=1, seed=0, band_rows=0,
-               cancel: Optional[ctypes.c_int] = None, callback=None, out=None, flags=0):
+               cancel: Optional[ctypes.c_int] = None, callback=None, out=None, flags=0, samples=None):
         """Host-buffer render (gi_render).  Returns (rgb float64 [h,w,3], rgb8 uint8 [h,w,3]).
         out=(rgb, rgb8): caller-owned C-contiguous arrays to fill instead (either may be None:
-        that output is not copied back)."""
+        that output is not copied back).  samples=(begin, end): one progressive Mode X pass."""
         if out is None:
             rgb, rgb8 = np.zeros((h, w, 3), np.float64), np.zeros((h, w, 3), np.uint8)
         else:
@@ -471,7 +474,7 @@ class DeviceScene:
             if a is not None and (a.dtype != dt or a.size != w * h * 3 or not a.flags.c_contiguous):
                 raise ValueError("render: out arrays must be C-contiguous [h, w, 3] float64 / uint8")
         cb = TILE_CB(callback) if callback is not None else TILE_CB()
-        o = self.opts(mode, spp, depth, seed, band_rows=band_rows, flags=flags)
+        o = self.opts(mode, spp, depth, seed, band_rows=band_rows, flags=flags, samples=samples)
         _check(lib().gi_render(self._h, ctypes.byref(cam._c), _d3(light), w, h, ctypes.byref(o),
                                rgb.ctypes.data_as(ctypes.POINTER(ctypes.c_double)) if rgb is not None else None,
                                rgb8.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)) if rgb8 is not None else None,
@@ -480,9 +483,10 @@ class DeviceScene:
 
     def render_device(self, cam: Camera, light, w: int, h: int, d_rgb: int, d_rgb8: int = 0, stream: int = 0,
                       mode=MODE_R, spp=1, depth=1, seed=0, shard_count=1, shard_index=0, stats_ptr=0,
-                      flags=0) -> None:
+                      flags=0, samples=None) -> None:
         """Asynchronous render into device buffers (gi_render_device); pointers are ints."""
-        o = self.opts(mode, spp, depth, seed, shard_count, shard_index, stats_ptr=stats_ptr, flags=flags)
+        o = self.opts(mode, spp, depth, seed, shard_count, shard_index, stats_ptr=stats_ptr, flags=flags,
+                      samples=samples)
         _check(lib().gi_render_device(self._h, ctypes.byref(cam._c), _d3(light), w, h, ctypes.byref(o),
                                       d_rgb or None, d_rgb8 or None, stream or None), "gi_render_device")
 

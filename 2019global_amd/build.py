@@ -88,9 +88,16 @@ def build(verbose: bool = False, force: bool = False, variant: str = "", hip_def
                 print(" ".join(cmd), flush=True)
             jobs.append((cmd, subprocess.Popen(cmd)))
         objs.append(obj)
-    for cmd, p in jobs:
-        if p.wait() != 0:
-            raise subprocess.CalledProcessError(p.returncode, cmd)
+    # wait for every job before reporting (a failed one must not leave the others writing objects that
+    # a later build would take as up to date); a failed job's object is removed
+    failed = [(cmd, p.returncode) for cmd, p in [(c, p) for c, p in jobs if p.wait() != 0]]
+    for cmd, _ in failed:
+        if os.path.exists(cmd[-1]):
+            os.remove(cmd[-1])
+    if failed:
+        for cmd, rc in failed:
+            print(f"build failed ({rc}): {' '.join(cmd)}", file=sys.stderr)
+        raise subprocess.CalledProcessError(failed[0][1], failed[0][0])
     if force or _stale(out, objs):
         _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-o", out, *objs, f"-L{ROCM}/lib", "-lamdhip64", "-ldl"], verbose)
     # hipcc's unbundling temporaries (libgi.so.<n>.hipv4-..., .host-...): removed on every build

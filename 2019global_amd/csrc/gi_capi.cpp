@@ -69,6 +69,8 @@ struct gi_scene {
     // and the work counters), whatever stream each is issued on
     hipEvent_t last = nullptr;
     bool launched = false;
+    uint64_t prog_key = 0;   // progressive passes: the frame's key and the next pass's sample_begin
+    int prog_next = -1;
     std::mutex mu;     // host-side calls on one scene are serialised
     int device = -1;
     int64_t bytes = 0;
@@ -410,7 +412,44 @@ int check_opts(int w, int h, const gi_opts* o) {
     if (o->mode == GI_MODE_X && (o->spp < 1 || o->depth < 1 || o->depth > 0xFFFF))
         return fail(GI_ERR_ARG, "mode X needs spp >= 1, 1 <= depth <= 65535");
     if ((o->flags & GI_FLAG_STATS) && !o->stats) return fail(GI_ERR_ARG, "GI_FLAG_STATS without stats buffer");
+    if ((o->sample_begin != 0 || o->sample_end != 0) &&
+        (o->mode != GI_MODE_X || o->spp < 2 || o->sample_begin < 0 || o->sample_begin >= o->sample_end || o->sample_end > o->spp))
+        return fail(GI_ERR_ARG, "progressive pass: mode X, spp > 1, 0 <= sample_begin < sample_end <= spp");
     return GI_OK;
+}
+
+// Progressive passes (gi_opts sample_begin / sample_end) continue one frame on one scene: the first
+// pass (sample_begin 0) records the frame's key, a later one must match it and start where the
+// previous pass ended.  Any other render of the scene ends the frame.
+uint64_t prog_key(const gi_camera& c, const double light[3], int w, int h, const gi_opts& o) {
+    uint64_t k = 1469598103934665603ull;
+    auto mix = [&](const void* p, size_t n) {
+        for (size_t i = 0; i < n; ++i) k = (k ^ static_cast<const unsigned char*>(p)[i]) * 1099511628211ull;
+    };
+    mix(&c, sizeof c);
+    mix(light, 3 * sizeof(double));
+    const int64_t v[8] = {w, h, o.spp, o.depth, (int64_t)o.seed, o.shard_count, o.shard_index,
+                          (int64_t)(o.flags & ~(GI_FLAG_STATS | GI_FLAG_TIME))};
+    mix(v, sizeof v);
+    return k;
+}
+int prog_check(gi_scene* s, const gi_camera& c, const double light[3], int w, int h, const gi_opts& o) {
+    if (o.sample_end == 0) {
+        s->prog_next = -1;
+        return GI_OK;
+    }
+    const uint64_t key = prog_key(c, light, w, h, o);
+    if (o.sample_begin > 0 && (s->prog_next != o.sample_begin || s->prog_key != key)) {
+        s->prog_next = -1;
+        return fail(GI_ERR_ARG, "progressive pass out of order: a pass continues the previous pass's frame "
+                                "(same camera, light, size, spp, depth, seed, shard) from its sample_end");
+    }
+    s->prog_key = key;
+    s->prog_next = -1;   // set once this pass has been issued
+    return GI_OK;
+}
+void prog_done(gi_scene* s, const gi_opts& o) {
+    s->prog_next = (o.sample_end > 0 && o.sample_end < o.spp) ? o.sample_end : -1;
 }
 
 int band_rows_of(const gi_opts* o, int h) {
@@ -604,8 +643,11 @@ int gi_render_device(gi_scene* s, const gi_camera* cam, const double light[3], i
         if (rc) return rc;
         if (!cam || !light) return fail(GI_ERR_ARG, "null camera or light");
         std::lock_guard<std::mutex> lk(s->mu);
-        return scene_render_band(s, make_cam(*cam, w), light, w, h, 0, *o, d_rgb, d_rgb8, static_cast<hipStream_t>(stream),
-                                 true);
+        if ((rc = prog_check(s, *cam, light, w, h, *o))) return rc;
+        rc = scene_render_band(s, make_cam(*cam, w), light, w, h, 0, *o, d_rgb, d_rgb8, static_cast<hipStream_t>(stream),
+                               true);
+        if (rc == GI_OK) prog_done(s, *o);
+        return rc;
     });
 }
 
@@ -625,6 +667,9 @@ int gi_render(gi_scene* s, const gi_camera* cam, const double light[3], int w, i
         const int band = band_rows_of(o, h);
         const size_t band_px = (size_t)w * (size_t)band;
         const int n_bands = (h + band - 1) / band;
+        if (o->sample_end > 0 && n_bands > 1)   // (a pass's rows are the whole frame's work list)
+            return fail(GI_ERR_ARG, "progressive passes render whole frames: band_rows 0 or >= h");
+        if ((rc = prog_check(s, *cam, light, w, h, *o))) return rc;
         if ((rc = ensure_hostpath(s, band_px, std::min(n_bands, HostPath::kSlots)))) return rc;
         HostPath& hp = s->hp;
         const CamDev cd = make_cam(*cam, w);
@@ -672,6 +717,7 @@ int gi_render(gi_scene* s, const gi_camera* cam, const double light[3], int w, i
         // nothing of this call stays in flight (a cancelled or failed call drains its bands)
         const hipError_t e1 = hipStreamSynchronize(hp.render), e2 = hipStreamSynchronize(hp.copy);
         if (rc == GI_OK && (e1 != hipSuccess || e2 != hipSuccess)) rc = hip_fail(e1 != hipSuccess ? e1 : e2, "render");
+        if (rc == GI_OK) prog_done(s, *o);
         return rc;
     });
 }

@@ -1228,6 +1228,7 @@ struct XWork {
     const unsigned* n_list;  // device count written by k_x_classify
     double* part;            // per-sample radiance [list index][sample][3] (spp > 1)
     unsigned* blocks;        // device counter of blocks taken
+    int s0, s1;              // the launch's samples [s0, s1) of the spp (0, spp; or a progressive pass)
 };
 
 #ifndef GI_X_UNITS_PER_LANE
@@ -1279,11 +1280,11 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     int k = 1;
     {
         const double lanes = (double)gridDim.x * (double)blockDim.x;
-        const double samples = (double)n_list * (double)spp;
+        const double samples = (double)n_list * (double)(wk.s1 - wk.s0);
         const int max_run = 1 << ((xflags >> 8) & 7);
-        while (2 * k <= max_run && 2 * k <= spp && samples / (2.0 * k) >= GI_X_UNITS_PER_LANE * lanes) k *= 2;
+        while (2 * k <= max_run && 2 * k <= wk.s1 - wk.s0 && samples / (2.0 * k) >= GI_X_UNITS_PER_LANE * lanes) k *= 2;
     }
-    const unsigned runs = (unsigned)((spp + k - 1) / k);              // units per pixel
+    const unsigned runs = (unsigned)((wk.s1 - wk.s0 + k - 1) / k);    // units per pixel (run c: samples s0 + c k ...)
     const unsigned n_groups = (n_list + 63u) >> 6;
     const unsigned n_blocks = n_groups * runs;
     // xflags bit 4 (spread): group g holds list entries g, g + G, g + 2G, ... (G groups) instead of
@@ -1776,7 +1777,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     q[0] = Lv.x; q[1] = Lv.y; q[2] = Lv.z;
                 }
                 ++smp;
-                phase = (smp < spp && (smp & (k - 1)) != 0) ? PH_START : PH_DONEPX;
+                phase = (smp < wk.s1 && ((smp - wk.s0) & (k - 1)) != 0) ? PH_START : PH_DONEPX;
             }
             if (STATS) t2 = clock64();
             // ---- the lane's next ray.  A primary ray that misses every child box of the root
@@ -1849,7 +1850,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                             if (spp > 1) idx = (long long)i;        // per-sample radiance row
                             key = mx_key(seed, (uint64_t)y * (uint64_t)m.w + (uint64_t)x);
                             if (PSL) reinterpret_cast<uint64_t*>(pslot)[9] = key;
-                            smp = (int)c * k;
+                            smp = wk.s0 + (int)c * k;
                             phase = PH_START;
                             if (c == 0) ++npx;
                         }
@@ -1882,7 +1883,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                             }
                             ++burst;
                             ++smp;
-                            phase = (smp < spp && (smp & (k - 1)) != 0) ? PH_START : PH_DONEPX;
+                            phase = (smp < wk.s1 && ((smp - wk.s0) & (k - 1)) != 0) ? PH_START : PH_DONEPX;
                             continue;
                         }
                     }
@@ -2081,8 +2082,8 @@ __global__ __launch_bounds__(kClassifyBlock) void k_x_classify(DevScene sc, CamD
         if (rgb) { rgb[3 * idx] = 0; rgb[3 * idx + 1] = 0; rgb[3 * idx + 2] = 0; }
         if (rgb8) { rgb8[3 * idx] = 0; rgb8[3 * idx + 1] = 0; rgb8[3 * idx + 2] = 0; }
     }
-    const unsigned long long ms = __ballot(scene);
-    __shared__ unsigned s_cnt[kClassifyBlock / 64 + 1];
+    const unsigned long long ms = __ballot(scene && list != nullptr);   // (a progressive pass after the
+    __shared__ unsigned s_cnt[kClassifyBlock / 64 + 1];                  //  first keeps the frame's list)
     const int wv = threadIdx.x >> 6;
     if (lane == 0) s_cnt[wv] = (unsigned)__popcll(ms);
     __syncthreads();
@@ -2093,10 +2094,10 @@ __global__ __launch_bounds__(kClassifyBlock) void k_x_classify(DevScene sc, CamD
             s_cnt[k] = acc;
             acc += c;
         }
-        s_cnt[kClassifyBlock / 64] = acc ? atomicAdd(n_list, acc) : 0u;
+        s_cnt[kClassifyBlock / 64] = acc ? atomicAdd(n_list, acc) : 0u;   // (acc > 0 only with a list)
     }
     __syncthreads();
-    if (scene) list[s_cnt[kClassifyBlock / 64] + s_cnt[wv] + (unsigned)__popcll(ms & ((1ull << lane) - 1))] = (unsigned)s;
+    if (scene && list) list[s_cnt[kClassifyBlock / 64] + s_cnt[wv] + (unsigned)__popcll(ms & ((1ull << lane) - 1))] = (unsigned)s;
     if (STATS && (s & ~63ll) < m.n_local * 64) {
         wave_add_stats(stats, bg ? (uint64_t)spp : 0, 0, 0, bg ? 1 : 0);
         uint64_t r = bg ? (uint64_t)spp : 0;   // samples resolved here, without traversal
@@ -2106,7 +2107,8 @@ __global__ __launch_bounds__(kClassifyBlock) void k_x_classify(DevScene sc, CamD
 }
 
 // Mode X pass 3 (spp > 1): a listed pixel's per-sample radiance added in sample order from +0, then
-// min(sum / spp, 1) and the 8-bit store -- the oracle's operations (pixel_mode_x).
+// min(sum / spp, 1) and the 8-bit store -- the oracle's operations (pixel_mode_x).  A progressive
+// pass sums its frame's samples [0, s1): the frame of spp = s1, the one-shot frame for s1 = spp.
 __global__ __launch_bounds__(256) void k_x_reduce(TileMap m, XWork wk, int spp, double* rgb, uint8_t* rgb8) {
     const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= *wk.n_list) return;
@@ -2116,12 +2118,13 @@ __global__ __launch_bounds__(256) void k_x_reduce(TileMap m, XWork wk, int spp, 
     slot_pixel(m, (long long)(ps >> 6), (int)(ps & 63), idx, x, y);
     double a = 0, b = 0, c = 0;
     const double* p = wk.part + 3 * (size_t)i * (size_t)spp;
-    for (int s = 0; s < spp; ++s) {
+    for (int s = 0; s < wk.s1; ++s) {
         a = a + p[3 * s];
         b = b + p[3 * s + 1];
         c = c + p[3 * s + 2];
     }
-    const double c0 = smin(a / (double)spp, 1.0), c1 = smin(b / (double)spp, 1.0), c2 = smin(c / (double)spp, 1.0);
+    const double n = (double)wk.s1;
+    const double c0 = smin(a / n, 1.0), c1 = smin(b / n, 1.0), c2 = smin(c / n, 1.0);
     if (rgb) { rgb[3 * idx] = c0; rgb[3 * idx + 1] = c1; rgb[3 * idx + 2] = c2; }
     if (rgb8) quantize(c0, c1, c2, rgb8 + 3 * idx);
 }
@@ -2368,19 +2371,28 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
         const dim3 pgrid((unsigned)std::max<long long>(1, std::min<long long>(want, xc.resident)));
         if (!xs.list || (unsigned long long)xs.cap < (unsigned long long)n_slots || (o.spp > 1 && (!xs.part || xs.spp < o.spp)))
             return hipErrorInvalidValue;
-        hipError_t e = hipMemsetAsync(sc.work, 0, 16 * sizeof(unsigned), stream);
+        // the launch's samples: the whole spp, or a progressive pass [sample_begin, sample_end) -- a pass
+        // after the first continues the frame: its work list (and count, work[1]) and the earlier
+        // passes' per-sample rows stay; classify only rewrites the background pixels
+        const int s0 = o.sample_end > 0 ? o.sample_begin : 0, s1 = o.sample_end > 0 ? o.sample_end : o.spp;
+        const bool cont = s0 > 0;
+        hipError_t e = hipMemsetAsync(sc.work, 0, (cont ? 1 : 16) * sizeof(unsigned), stream);
+        if (e == hipSuccess && cont) e = hipMemsetAsync(sc.work + 2, 0, 14 * sizeof(unsigned), stream);
         if (e != hipSuccess) return e;
         XWork wk;
         wk.list = xs.list;
         wk.n_list = sc.work + 1;
         wk.part = xs.part;
         wk.blocks = sc.work;
+        wk.s0 = s0;
+        wk.s1 = s1;
         const dim3 sgrid((unsigned)((n_slots + 255) / 256));
         const dim3 cgrid((unsigned)((n_slots + kClassifyBlock - 1) / kClassifyBlock));
         const int form = x_form_choice(sc, xc, o);
         unsigned* zero2 = form == 2 ? xs.wcnt : nullptr;   // k_seg's unit counter, zeroed by the classify pass
-        if (stats) hipLaunchKernelGGL(k_x_classify<true>, cgrid, dim3(kClassifyBlock), 0, stream, sc, cam, m, o.spp, rgb, rgb8, xs.list, sc.work + 1, st, zero2);
-        else hipLaunchKernelGGL(k_x_classify<false>, cgrid, dim3(kClassifyBlock), 0, stream, sc, cam, m, o.spp, rgb, rgb8, xs.list, sc.work + 1, st, zero2);
+        unsigned* cl = cont ? nullptr : xs.list;
+        if (stats) hipLaunchKernelGGL(k_x_classify<true>, cgrid, dim3(kClassifyBlock), 0, stream, sc, cam, m, s1 - s0, rgb, rgb8, cl, sc.work + 1, st, zero2);
+        else hipLaunchKernelGGL(k_x_classify<false>, cgrid, dim3(kClassifyBlock), 0, stream, sc, cam, m, s1 - s0, rgb, rgb8, cl, sc.work + 1, st, zero2);
         // shading-handler threshold (eighths of the live lanes that must wait): the builder's
         // estimate for the scene (DevScene::x_handle8) unless GI_X_HANDLE8 overrides it
         const int h8 = env.h8 > 0 ? env.h8 : sc.x_handle8;

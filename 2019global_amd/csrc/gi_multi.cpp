@@ -363,6 +363,7 @@ int gi_multi_render(gi_multi* m, const gi_camera* cam, const double light[3], in
         if (o->shard_count != 1 || o->shard_index != 0)
             return error(GI_ERR_ARG, "gi_multi_render shards by itself: opts shard_count must be 1");
         if (o->flags & GI_FLAG_STATS) return error(GI_ERR_ARG, "GI_FLAG_STATS is per device: use gi_render_device");
+        if (o->sample_end != 0) return error(GI_ERR_ARG, "progressive passes: gi_render / gi_render_device of one scene");
         DeviceRestore keep;   // the caller's current device, restored on return
         std::lock_guard<std::mutex> lk(m->mu);
         const int band = band_rows_of(o, h);

@@ -181,7 +181,8 @@ struct WFArgs {
     unsigned* take;            // this bounce's input entries handed out (device counter)
     const unsigned* n_in;      // this bounce's input length (bounce > 0: the previous bounce's n_out)
     unsigned* n_out;           // entries appended to qout
-    unsigned long long u0, u1; // bounce 0: the chunk's units [u0, u1) of n_list * spp
+    unsigned long long u0, u1; // bounce 0: the chunk's units [u0, u1) of n_list * ns
+    unsigned s0, ns;           // the launch's samples [s0, s0 + ns) of the spp (0, spp; or a progressive pass)
 };
 
 // The scene views of a bounce / segment kernel.  LDS: wide nodes, leaf records, primitives and
@@ -395,7 +396,7 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
     // the bounce's input length: bounce 0, the chunk's units of the work list; else the queue
     unsigned n_in;
     if (b == 0) {
-        const unsigned long long tot = (unsigned long long)*a.n_list * (unsigned long long)spp;
+        const unsigned long long tot = (unsigned long long)*a.n_list * (unsigned long long)a.ns;
         n_in = (unsigned)(min(tot, a.u1) > a.u0 ? min(tot, a.u1) - a.u0 : 0ull);
     } else {
         n_in = *a.n_in;
@@ -430,11 +431,11 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
             if (b == 0) {
                 const unsigned long long u = a.u0 + j;
                 if (u < (1ull << 32)) {   // 32-bit division where it suffices
-                    li = (unsigned)u / (unsigned)spp;
-                    smp = (unsigned)u - li * (unsigned)spp;
+                    li = (unsigned)u / a.ns;
+                    smp = a.s0 + ((unsigned)u - li * a.ns);
                 } else {
-                    li = (unsigned)(u / (unsigned long long)spp);
-                    smp = (unsigned)(u - (unsigned long long)li * (unsigned long long)spp);
+                    li = (unsigned)(u / (unsigned long long)a.ns);
+                    smp = a.s0 + (unsigned)(u - (unsigned long long)li * (unsigned long long)a.ns);
                 }
             } else {
                 const uint2 id = qin.id[j];
@@ -513,7 +514,7 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
     const WFView v = wf_stage<LDS>(sc, lds_dyn);
     const bool no_shadow = (xflags & 4) != 0;
     const int lane = threadIdx.x & 63;
-    const unsigned long long total = (unsigned long long)*a.n_list * (unsigned long long)spp;
+    const unsigned long long total = (unsigned long long)*a.n_list * (unsigned long long)a.ns;
     // run length: up to GI_SEG_TAKE batches of 64 units per atomic (background-heavy frames burn units
     // fast: longer runs, fewer atomics on the one counter), fewer when the launch has less than about
     // 8 runs per resident wave (small launches: every wave gets work).  Guided self-scheduling --
@@ -568,11 +569,11 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
             unsigned li_u = 0, smp_u = 0;
             if (u != ~0ull) {
                 if (u < (1ull << 32)) {
-                    li_u = (unsigned)u / (unsigned)spp;
-                    smp_u = (unsigned)u - li_u * (unsigned)spp;
+                    li_u = (unsigned)u / a.ns;
+                    smp_u = a.s0 + ((unsigned)u - li_u * a.ns);
                 } else {
-                    li_u = (unsigned)(u / (unsigned long long)spp);
-                    smp_u = (unsigned)(u - (unsigned long long)li_u * (unsigned long long)spp);
+                    li_u = (unsigned)(u / (unsigned long long)a.ns);
+                    smp_u = a.s0 + (unsigned)(u - (unsigned long long)li_u * (unsigned long long)a.ns);
                 }
             }
             if (!live && u != ~0ull) {
@@ -700,6 +701,7 @@ hipError_t launch_wf(const DevScene& sc, int kv, size_t lds_bytes, int resident,
                      hipEvent_t ev_begin, hipEvent_t ev_end) {
     const TileMap m = make_map(w, h, o.shard_count, o.shard_index, y0);
     const int depth = o.depth;
+    const int s0 = o.sample_end > 0 ? o.sample_begin : 0, s1 = o.sample_end > 0 ? o.sample_end : o.spp;
     const dim3 grid((unsigned)std::max(1, resident)), block(256);
     hipError_t e = hipSuccess;
     if (form == 2) {   // (the unit counter xs.wcnt[0..1] was zeroed by k_x_classify)
@@ -708,6 +710,8 @@ hipError_t launch_wf(const DevScene& sc, int kv, size_t lds_bytes, int resident,
         a.n_list = n_list_dev;
         a.part = xs.part;
         a.take = xs.wcnt;
+        a.s0 = (unsigned)s0;
+        a.ns = (unsigned)(s1 - s0);
         if (ev_begin) (void)hipEventRecord(ev_begin, stream);
         wf_dispatch(sc, kv, [&](auto L, auto W, auto SHt, auto T, auto C) {
             constexpr bool l = decltype(L)::value, wv = decltype(W)::value, sh = decltype(SHt)::value,
@@ -721,7 +725,7 @@ hipError_t launch_wf(const DevScene& sc, int kv, size_t lds_bytes, int resident,
     e = hipMemcpyAsync(xs.h_nlist, n_list_dev, sizeof(unsigned), hipMemcpyDeviceToHost, stream);
     if (e == hipSuccess) e = hipStreamSynchronize(stream);
     if (e != hipSuccess) return e;
-    const unsigned long long units = (unsigned long long)*xs.h_nlist * (unsigned long long)o.spp;
+    const unsigned long long units = (unsigned long long)*xs.h_nlist * (unsigned long long)(s1 - s0);
     if (ev_begin) (void)hipEventRecord(ev_begin, stream);
     for (unsigned long long u0 = 0; u0 < units; u0 += (unsigned long long)xs.wcap) {
         e = hipMemsetAsync(xs.wcnt, 0, 2 * (size_t)depth * sizeof(unsigned), stream);
@@ -736,6 +740,8 @@ hipError_t launch_wf(const DevScene& sc, int kv, size_t lds_bytes, int resident,
             a.n_out = xs.wcnt + 2 * b + 1;
             a.u0 = u0;
             a.u1 = std::min(units, u0 + (unsigned long long)xs.wcap);
+            a.s0 = (unsigned)s0;
+            a.ns = (unsigned)(s1 - s0);
             WFQ qin, qout;
             qin.cap = qout.cap = xs.wcap;
             qin.r = xs.wq[(b + 1) & 1];

@@ -129,6 +129,17 @@ typedef struct gi_opts {
     int32_t reserved;
     uint64_t seed;         /* Mode X RNG seed */
     uint64_t* stats;       /* device pointer to GI_STATS_N uint64 counters (GI_FLAG_STATS) */
+    /* Mode X progressive passes (ABI 10; both 0: the whole frame at once).  A pass renders samples
+     * [sample_begin, sample_end) of the spp-sample frame (spp > 1) and delivers the running estimate
+     * min(sum over samples s < sample_end / sample_end, 1) -- exactly the frame of spp = sample_end,
+     * since the samples' jitter and paths do not depend on spp; the pass with sample_end == spp is
+     * the one-shot frame bit for bit.  Passes continue one frame: they are issued on one scene in
+     * order (sample_begin = the previous pass's sample_end, the first at 0) with the same camera,
+     * light, size, spp, depth, seed and shard, and no other render of the scene in between; the
+     * scene keeps the frame's per-sample radiance rows and work list between them (GI_ERR_ARG
+     * otherwise).  gi_render: whole-frame bands only (band_rows 0 or >= h). */
+    int32_t sample_begin;
+    int32_t sample_end;
 } gi_opts;
 
 /* stats[] slots */

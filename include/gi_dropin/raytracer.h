@@ -17,6 +17,13 @@
 //     construction -- GI_MODE=X (or 1), GI_SPP, GI_DEPTH, GI_SEED -- selects the build-defined
 //     depth / spp path tracer (DESIGN.md "Mode X": recursive secondary-ray spawn, jittered samples)
 //     behind the same run(w, h); default GI_MODE_R, 1 spp, depth 1 (raytracer.h:41-84).
+//   * progressive samples (Mode X): setIntegrator(GI_MODE_X, spp, depth, seed, pass) or GI_PASS=n
+//     renders the frame's spp in passes of n samples; after each pass the whole frame's running
+//     estimate -- exactly the frame of that many samples -- goes through Image::setPixel, so a 64-spp
+//     frame shows a first image after the first pass instead of nothing until it is done (the
+//     viewer restarts on every resize, viewer.h:41-52), and stop() is honoured between passes (the
+//     image keeps the last delivered pass).  The last pass's frame is the one-shot frame bit for
+//     bit (gi.h gi_opts sample_begin / sample_end).  One device (not with GI_DEVICES).
 //   * several GPUs: GI_DEVICES="0,1,..." or "all" (every gfx950 of the node) renders each frame's
 //     8x8 tiles across them (gi_multi, RCCL gather).  Unset: one device, the one current on the
 //     thread that uploads the scene (hipSetDevice by the host app is honoured); if the multi-device
@@ -27,6 +34,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <vector>
 
@@ -48,10 +56,10 @@ class RayTracer {
     /// Extension (not in the reference): the integrator run() uses.  GI_MODE_R (default) is the
     /// reference's per-pixel body; GI_MODE_X is the depth / spp path tracer.  Returns false (and
     /// keeps the current choice) on an invalid combination.
-    bool setIntegrator(int mode, int spp, int depth, uint64_t seed = 0) {
+    bool setIntegrator(int mode, int spp, int depth, uint64_t seed = 0, int pass = 0) {
         if (mode != GI_MODE_R && mode != GI_MODE_X) return false;
-        if (mode == GI_MODE_X && (spp < 1 || depth < 1 || depth > 0xFFFF)) return false;
-        _integ = Integrator{mode, mode == GI_MODE_X ? spp : 1, mode == GI_MODE_X ? depth : 1, seed};
+        if (mode == GI_MODE_X && (spp < 1 || depth < 1 || depth > 0xFFFF || pass < 0)) return false;
+        _integ = Integrator{mode, mode == GI_MODE_X ? spp : 1, mode == GI_MODE_X ? depth : 1, seed, mode == GI_MODE_X ? pass : 0};
         return true;
     }
     int integratorMode() const { return _integ.mode; }
@@ -94,6 +102,23 @@ class RayTracer {
         o.band_rows = _integ.mode == GI_MODE_X ? std::max(32, (h + 63) / 64 * 8) : 32;
         Band band{_image.get(), w, _keep_radiance ? &_radiance : nullptr};
         if (_keep_radiance) _radiance.assign((size_t)w * h * 3, 0.0);
+        _passes = 0;
+        if (_integ.mode == GI_MODE_X && _integ.pass > 0 && _integ.pass < _integ.spp && !_gpu->multi) {
+            // progressive samples: whole-frame passes, each delivered as the running estimate
+            o.band_rows = 0;
+            int rc = GI_OK;
+            for (int s0 = 0; s0 < _integ.spp && rc == GI_OK; s0 += _integ.pass) {
+                o.sample_begin = s0;
+                o.sample_end = std::min(_integ.spp, s0 + _integ.pass);
+                rc = gi_render(_gpu->scene, &cam, light, w, h, &o, nullptr, nullptr, &_cancel, &RayTracer::on_band, &band);
+                if (rc == GI_OK) {
+                    ++_passes;
+                    if (_on_pass) _on_pass(_passes, o.sample_end);   // (may stop() the frame)
+                }
+            }
+            if (rc != GI_OK && rc != GI_ERR_CANCELLED) std::fprintf(stderr, "gi_render: %s\n", gi_last_error());
+            return;
+        }
         const int rc = _gpu->multi ? gi_multi_render(_gpu->multi, &cam, light, w, h, &o, nullptr, nullptr, &_cancel,
                                                      &RayTracer::on_band, &band)
                                    : gi_render(_gpu->scene, &cam, light, w, h, &o, nullptr, nullptr, &_cancel,
@@ -111,11 +136,17 @@ class RayTracer {
     /// Image, whose RGB888 is its (int)(255*c) quantisation (image.h:14-16).
     void keepRadiance(bool on) { _keep_radiance = on; }
     const std::vector<double>& radiance() const { return _radiance; }
+    /// Extension (tests): progressive passes the last run() delivered (0 without passes).
+    int passesDelivered() const { return _passes; }
+    /// Extension (tools, tests): called on the render thread after each delivered progressive pass
+    /// with the passes so far and the samples the image now holds; it may call stop().
+    void setPassCallback(std::function<void(int passes, int samples)> f) { _on_pass = std::move(f); }
 
   private:
     struct Integrator {
         int mode, spp, depth;
         uint64_t seed;
+        int pass;   // Mode X progressive passes of this many samples (0: the whole spp at once)
     };
     struct Band {
         Image* image;
@@ -126,15 +157,18 @@ class RayTracer {
     // GI_MODE / GI_SPP / GI_DEPTH / GI_SEED, read once per process; invalid values keep Mode R
     static Integrator env_integrator() {
         static const Integrator v = [] {
-            Integrator r{GI_MODE_R, 1, 1, 0};
+            Integrator r{GI_MODE_R, 1, 1, 0, 0};
             const char* m = std::getenv("GI_MODE");
             if (!m || !(std::strcmp(m, "X") == 0 || std::strcmp(m, "x") == 0 || std::strcmp(m, "1") == 0)) return r;
             const char* sp = std::getenv("GI_SPP");
             const char* dp = std::getenv("GI_DEPTH");
             const char* sd = std::getenv("GI_SEED");
+            const char* ps = std::getenv("GI_PASS");
             const long spp = sp ? std::strtol(sp, nullptr, 10) : 1, depth = dp ? std::strtol(dp, nullptr, 10) : 1;
-            if (spp < 1 || depth < 1 || depth > 0xFFFF || spp > (1L << 30)) return r;
-            return Integrator{GI_MODE_X, (int)spp, (int)depth, sd ? (uint64_t)std::strtoull(sd, nullptr, 10) : 0};
+            const long pass = ps ? std::strtol(ps, nullptr, 10) : 0;
+            if (spp < 1 || depth < 1 || depth > 0xFFFF || spp > (1L << 30) || pass < 0) return r;
+            return Integrator{GI_MODE_X, (int)spp, (int)depth, sd ? (uint64_t)std::strtoull(sd, nullptr, 10) : 0,
+                              (int)std::min(pass, spp)};
         }();
         return v;
     }
@@ -220,4 +254,6 @@ class RayTracer {
     Integrator _integ;
     bool _keep_radiance = false;
     std::vector<double> _radiance;
+    int _passes = 0;
+    std::function<void(int, int)> _on_pass;
 };

@@ -15,7 +15,9 @@
 // (raytracer.h:26-30, 41-43), as int32 -- compared with the compiled reference's lists; with "rad"
 // it writes the frame's fp64 radiance (RayTracer::keepRadiance) instead of its RGB888.
 // The integrator is the drop-in's default (the reference's, Mode R) unless the environment opts in
-// (GI_MODE=X GI_SPP=.. GI_DEPTH=.. GI_SEED=.., read by the drop-in RayTracer's constructor).
+// (GI_MODE=X GI_SPP=.. GI_DEPTH=.. GI_SEED=.. [GI_PASS=..], read by the drop-in RayTracer's
+// constructor).  DEMO_STOP_AFTER=k stops the frame after k progressive passes (RayTracer::stop from
+// the pass callback, as a Viewer resize would); the demo prints the passes delivered to stderr.
 //   dropin_demo <w> <h> <out> [zoo|main|obj:<path>|scn:<path>] [cands|rad]
 #include <cmath>
 #include <cstdio>
@@ -124,8 +126,15 @@ int main(int argc, char** argv) {
     const bool rad = argc > 5 && std::string(argv[5]) == "rad";
     RayTracer viewer_copy = raytracer;
     viewer_copy.keepRadiance(rad);
+    if (const char* sa = std::getenv("DEMO_STOP_AFTER")) {
+        const int k = std::atoi(sa);
+        viewer_copy.setPassCallback([&viewer_copy, k](int passes, int) {
+            if (passes >= k) viewer_copy.stop();
+        });
+    }
     viewer_copy.start();
     viewer_copy.run(w, h);
+    std::fprintf(stderr, "passes %d\n", viewer_copy.passesDelivered());
     std::shared_ptr<Image> img = viewer_copy.getImage();
     if (img->width() != w || img->height() != h) return 1;
     FILE* f = std::fopen(argv[3], "wb");

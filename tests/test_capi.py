@@ -38,7 +38,7 @@ def test_library_loads_and_abi_version():
     L = gi.lib()
     assert L.gi_abi_version() == gi.ABI_VERSION
     assert ctypes.sizeof(gi.EntityDesc) == 160
-    assert ctypes.sizeof(gi.Opts) == 48
+    assert ctypes.sizeof(gi.Opts) == 56   # ABI 10: + sample_begin, sample_end
     assert ctypes.sizeof(gi.CameraDesc) == 80
 
 

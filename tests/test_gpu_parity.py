@@ -597,6 +597,63 @@ def test_cpp_dropin_raytracer_mode_x_opt_in(torch_cuda, tmp_path, band_env):
     assert float(err.max()) <= 1e-5
 
 
+def test_cpp_dropin_progressive_passes(torch_cuda, tmp_path):
+    """SURVEY §5 (checkpoint/resume: progressive spp): the drop-in RayTracer::run renders a Mode X
+    frame's spp in passes (GI_PASS=2 of 8 samples) and delivers each pass's running estimate through
+    Image::setPixel.  Stopped after the first pass (stop() from the pass callback, as a Viewer resize
+    does), the image holds that pass -- exactly the 2-sample frame of the oracle; run to the end, the
+    frame is the 8-sample oracle frame bit for bit, after 4 passes."""
+    import subprocess
+    exe = os.path.join(U.ROOT, "integration", "_build", "dropin_demo")
+    if not os.path.exists(exe):
+        pytest.skip("integration/_build/dropin_demo not built (needs the reference tree)")
+    sc = S.cornell_scene()
+    scn = tmp_path / "c.scn"
+    scn.write_text(sc.to_scn())
+    w, h, spp, depth, seed = 72, 56, 8, 5, 11
+    env = dict(os.environ, QT_QPA_PLATFORM="offscreen", GI_MODE="X", GI_SPP=str(spp), GI_DEPTH=str(depth),
+               GI_SEED=str(seed), GI_PASS="2")
+    out = tmp_path / "f.f64"
+    for stop_after, samples, passes in ((1, 2, 1), (0, 8, 4)):
+        e = dict(env, DEMO_STOP_AFTER=str(stop_after)) if stop_after else env
+        r = subprocess.run([exe, str(w), str(h), str(out), f"scn:{scn}", "rad"], check=True, env=e, timeout=120,
+                           capture_output=True, text=True)
+        assert f"passes {passes}" in r.stderr, r.stderr
+        got = np.frombuffer(out.read_bytes(), np.float64).reshape(-1, 3)
+        o = U.oracle_render(sc.to_scn(), w, h, mode=1, spp=samples, depth=depth, seed=seed)
+        assert U.bits_equal(got, o["rgb"]).all(), (stop_after, samples)
+
+
+@pytest.mark.parametrize("name,w,h,spp,depth,passes", [("cornell", 64, 48, 8, 5, (0, 2, 3, 8)),
+                                                       ("soup1000", 48, 40, 6, 8, (0, 4, 6)),
+                                                       ("zoo", 40, 32, 4, 4, (0, 1, 4))])
+def test_mode_x_progressive_passes(torch_cuda, name, w, h, spp, depth, passes):
+    """Progressive Mode X passes (gi_opts sample_begin / sample_end, ABI 10): after the pass ending at
+    sample e the frame is the e-sample frame bit for bit (jitter and paths do not depend on spp; e > 1),
+    and the last pass's frame equals the one-shot spp frame and the oracle's; the three Mode X forms
+    alike.  A pass out of order, or after another render of the scene, is refused."""
+    sc = _scene(name)
+    d = dev_scene(name)
+    kw = dict(mode=gi.MODE_X, spp=spp, depth=depth, seed=5)
+    for fl in (0, gi.FLAG_X_MEGA, gi.FLAG_X_WF, gi.FLAG_X_SEG):
+        for b, e in zip(passes[:-1], passes[1:]):
+            rgb, rgb8 = d.render(cam_of(sc), sc.light, w, h, flags=fl, samples=(b, e), **kw)
+            if e > 1:
+                ref, ref8 = d.render(cam_of(sc), sc.light, w, h, mode=gi.MODE_X, spp=e, depth=depth, seed=5, flags=fl)
+                assert U.bits_equal(rgb, ref).all() and (rgb8 == ref8).all(), (name, fl, b, e)
+            if e == spp:
+                o = U.oracle_render(sc.to_scn(), w, h, mode=1, spp=spp, depth=depth, seed=5)
+                assert U.bits_equal(rgb.reshape(-1, 3), o["rgb"]).all(), (name, fl)
+            if e > 1 and e < spp:   # (the reference render above ended the progressive frame: resume it)
+                d.render(cam_of(sc), sc.light, w, h, flags=fl, samples=(0, e), **kw)
+    with pytest.raises(gi.GIError):   # out of order: a frame starts at sample 0
+        d.render(cam_of(sc), sc.light, w, h, samples=(passes[1], passes[2]), **kw)
+    d.render(cam_of(sc), sc.light, w, h, samples=(0, passes[1]), **kw)
+    d.render(cam_of(sc), sc.light, w, h, **kw)   # another render ends the progressive frame
+    with pytest.raises(gi.GIError):
+        d.render(cam_of(sc), sc.light, w, h, samples=(passes[1], passes[2]), **kw)
+
+
 @pytest.mark.parametrize("scene,w,h,spp,depth", [("cornell", 37, 29, 3, 5), ("zoo", 45, 19, 2, 4),
                                                   ("main", 13, 61, 1, 3)])
 def test_mode_x_ragged_frames_bit_exact(torch_cuda, scene, w, h, spp, depth):
