@@ -714,20 +714,21 @@ __device__ __forceinline__ unsigned rf_pages_of(const RFlat& f, long long r, uns
 // fp64, the box widened by 2 tau) holds no pixel's candidate.  The wave pops up to 8 nodes per round
 // from its LDS stack and tests their 64 children together, one per lane; hit interior children are
 // pushed, hit leaf slots are then tested by every lane against its own line with the per-line slab
-// test of the per-pixel walk (child_hit_line, the same arithmetic), and a passing lane queues the
+// test of the per-pixel walk (box_hit_line: children_mask_line's arithmetic), and a passing lane queues the
 // slot's entities.  Since a node's box contains its children's, the pairs are exactly those of a
 // per-pixel walk; a tile's loads are the same for all its lanes (broadcasts) instead of 64
 // divergent walks.  A stack that would exceed GI_RF_STK marks the tile overflowed (k_mode_r_batch).
 #define GI_RF_STK 512u   // traversal stack entries per wave (tile)
-__device__ __forceinline__ bool child_hit_line(const XWNode* nd, int c, F3 of, F3 ivf, float tau) {
+// one existing child's box (lo xyz, hi xyz) against the line: children_mask_line's arithmetic
+__device__ __forceinline__ bool box_hit_line(const float* b, F3 of, F3 ivf, float tau) {
     const int sm = iv_signs(ivf);
-    const float nx = (sm & 1) ? nd->hi[0][c] : nd->lo[0][c], fx = (sm & 1) ? nd->lo[0][c] : nd->hi[0][c];
-    const float ny = (sm & 2) ? nd->hi[1][c] : nd->lo[1][c], fy = (sm & 2) ? nd->lo[1][c] : nd->hi[1][c];
-    const float nz = (sm & 4) ? nd->hi[2][c] : nd->lo[2][c], fz = (sm & 4) ? nd->lo[2][c] : nd->hi[2][c];
+    const float nx = (sm & 1) ? b[3] : b[0], fx = (sm & 1) ? b[0] : b[3];
+    const float ny = (sm & 2) ? b[4] : b[1], fy = (sm & 2) ? b[1] : b[4];
+    const float nz = (sm & 4) ? b[5] : b[2], fz = (sm & 4) ? b[2] : b[5];
     const float sx = (sm & 1) ? tau : -tau, sy = (sm & 2) ? tau : -tau, sz = (sm & 4) ? tau : -tau;
     const float tn = fmaxf(fmaxf(((nx + sx) - of.x) * ivf.x, ((ny + sy) - of.y) * ivf.y), ((nz + sz) - of.z) * ivf.z);
     const float tf = fminf(fminf(((fx - sx) - of.x) * ivf.x, ((fy - sy) - of.y) * ivf.y), ((fz - sz) - of.z) * ivf.z);
-    return (tn <= tf) & ((nd->exists >> c) & 1);
+    return tn <= tf;
 }
 // may some line of the tile's double cone (side-plane normals n[4], through the camera c) meet the
 // box [lo - wd, hi + wd]?  Forward nappe: every side plane has part of the box on its inner side;
@@ -761,6 +762,8 @@ __global__ __launch_bounds__(256) void k_rf_walk(DevScene sc, CamDev cam, TileMa
     __shared__ unsigned s_pt[4][GI_RF_KMAX];   // the wave's pool pages
     __shared__ int s_stk[4][GI_RF_STK];        // the tile's traversal stack (line-BVH nodes)
     __shared__ int s_leaf[4][64];              // a round's hit leaf slots: (node << 3) | slot
+    __shared__ float s_lb[4][64][6];           //   their boxes (lo xyz, hi xyz)
+    __shared__ int s_le[4][64][6];             //   their first entity, count and first 4 entity ids
     const long long slot = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     const long long region = slot >> 6;
     const int lane = threadIdx.x & 63;
@@ -768,6 +771,8 @@ __global__ __launch_bounds__(256) void k_rf_walk(DevScene sc, CamDev cam, TileMa
     unsigned* pt = s_pt[threadIdx.x >> 6];
     int* stk = s_stk[threadIdx.x >> 6];
     int* leaves = s_leaf[threadIdx.x >> 6];
+    float (*lb)[6] = s_lb[threadIdx.x >> 6];
+    int (*le)[6] = s_le[threadIdx.x >> 6];
     long long idx = -1;
     int x = 0, y = 0;
     const bool in = slot < m.n_local * 64;
@@ -886,18 +891,36 @@ __global__ __launch_bounds__(256) void k_rf_walk(DevScene sc, CamDev cam, TileMa
         if (hit && ch < 0) leaves[__popcll(m_lf & ((1ull << lane) - 1))] = ~ch;
         sp += n_in;
         __builtin_amdgcn_wave_barrier();
-        // ---- the round's leaf slots against every lane's own line
-        for (int i = 0; i < n_lf; ++i) {
-            const int it = leaves[i];
+        // ---- the round's leaf slots against every lane's own line.  Their records are fetched first,
+        // lane j those of slot j, into LDS (one memory round trip for the round instead of one per
+        // slot); then every slot is tested by every lane from LDS
+        if (lane < n_lf) {
+            const int it = leaves[lane];
             const XWNode* nd = W + (it >> 3);
             const int sl = it & 7;
-            const bool pass = ok && child_hit_line(nd, sl, of, ivf, tau);
-            const int e0 = ~nd->child[sl], cnt = nd->cnt[sl];   // (uniform: one leaf for the wave)
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                lb[lane][a] = nd->lo[a][sl];
+                lb[lane][3 + a] = nd->hi[a][sl];
+            }
+            const int e0 = ~nd->child[sl], cnt = nd->cnt[sl];
+            le[lane][0] = e0;
+            le[lane][1] = cnt;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) le[lane][2 + k] = k < cnt ? sc.rc_ent[e0 + k] : 0;
+        }
+        __builtin_amdgcn_wave_barrier();
+        for (int i = 0; i < n_lf; ++i) {
+            const bool pass = ok && box_hit_line(lb[i], of, ivf, tau);
+            const int e0 = le[i][0], cnt = le[i][1];   // (uniform: one leaf for the wave)
             for (int k0 = 0; k0 < cnt; k0 += (int)GI_RF_BUF / 2) {
                 const int kk = min(cnt - k0, (int)GI_RF_BUF / 2);
                 if (__ballot(nb + kk > (int)GI_RF_BUF) != 0) flush();
                 if (pass)
-                    for (int k = 0; k < kk; ++k) buf[nb++] = (int)(tag | (unsigned)sc.rc_ent[e0 + k0 + k]);
+                    for (int k = 0; k < kk; ++k) {
+                        const int q = k0 + k;
+                        buf[nb++] = (int)(tag | (unsigned)(q < 4 ? le[i][2 + q] : sc.rc_ent[e0 + q]));
+                    }
             }
         }
         __builtin_amdgcn_wave_barrier();

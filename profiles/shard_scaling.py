@@ -60,9 +60,11 @@ def main():
             if n == 1:
                 t1 = ms
             res[f"N{n}_rank{r}_ms"] = round(ms, 3)
-            res[f"N{n}_rank{r}_speedup"] = round(t1 / ms, 3)
+            if t1:
+                res[f"N{n}_rank{r}_speedup"] = round(t1 / ms, 3)
             print(json.dumps({"n": n, "rank": r, "ms": round(ms, 3), "kernel_ms": round(kms, 3),
-                              "ideal_ms": round(t1 / n, 3), "speedup": round(t1 / ms, 3), **sched}), flush=True)
+                              "ideal_ms": round(t1 / n, 3) if t1 else None,
+                              "speedup": round(t1 / ms, 3) if t1 else None, **sched}), flush=True)
     print(json.dumps(res))
 
 
