@@ -1071,6 +1071,7 @@ __global__ __launch_bounds__(64) void k_rf_reach(DevScene sc, CamDev cam, TileMa
         for (int k = 0; k < GI_R_MEMO; ++k) s_memo[lane * GI_R_MEMO + k] = -1;   // (matches no key)
     __builtin_amdgcn_wave_barrier();
     uint32_t nnode = 0;
+    // (chunks from a device counter instead, as waves free up: R-C4 0.80 -> 0.88 ms)
     for (long long c = gw; 64 * c < n_hits; c += n_w) {
         const long long i = 64 * c + lane;
         long long sg = rf_find(f.hoff, n_seg, 64 * c);   // the chunk's first segment (uniform)
