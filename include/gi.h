@@ -112,7 +112,10 @@ typedef enum gi_mode {
                                     shading (raytracer.h:41-84, material.h:48-62), so its stages can
                                     be checked against the reference's frames (tests) */
 #define GI_FLAG_X_WF 16u         /* Mode X: the wavefront form (one launch per bounce over a compacted queue of
-                                    live paths, gi_wf.hip) whatever the scene; same frame bit for bit */
+                                    live paths, gi_wf.hip) whatever the scene; same frame bit for bit.  An A/B
+                                    form (slower everywhere): it reads the work list's length back to size its
+                                    chunks, so a render with it synchronises the render's stream on the host and
+                                    cannot be captured in a graph */
 #define GI_FLAG_X_MEGA 32u       /* Mode X: the persistent path-state kernel (k_mode_x) whatever the scene */
 #define GI_FLAG_X_SEG 64u        /* Mode X: the segment-synchronous persistent form (k_seg: every loop
                                     iteration one whole path segment per lane).  None of the three form
