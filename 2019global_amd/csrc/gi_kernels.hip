@@ -1192,6 +1192,15 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 #ifndef GI_X_TRI
 #define GI_X_TRI 1   // 4-wave LDS kernel: triangle-only primitive tests and texture mapping (TRI)
 #endif
+#ifndef GI_X_TAILPROBE
+#define GI_X_TAILPROBE 0   // (measurement variant) k_mode_x's STATS launch records drain / wave life
+#endif
+#ifndef GI_X_TAILPROBE_T1
+#define GI_X_TAILPROBE_T1 8
+#endif
+#ifndef GI_X_TAILPROBE_T2
+#define GI_X_TAILPROBE_T2 16
+#endif
 #ifndef GI_X_PREFETCH
 // HBM-resident scenes: fetch the next pop's child reference a step ahead (PF): C4 1.94 -> 1.75-1.78 ms,
 // C5 199.7 -> 198.5 ms
@@ -1231,6 +1240,11 @@ struct XCounters {
     // divergence profile (wave-level, lane 0): loop iterations in which some lane ran a node test /
     // a leaf test / an inline bounce restart / a handler start-loop pass, and the lanes that did
     uint64_t it_node = 0, ln_node = 0, it_leaf = 0, ln_leaf = 0, it_rs = 0, ln_rs = 0, it_st = 0, ln_st = 0;
+#if GI_X_TAILPROBE
+    uint64_t w_start = 0, w_exh = 0;   // (probe) wave start, first sight of the exhausted block counter
+    uint64_t w_t1 = 0, w_t2 = 0;       // (probe) first iteration after it with <= T1 / T2 live lanes
+    uint64_t p_it = 0, p_lo = 0;       // (probe) iterations after it; of those with <= T1 paths
+#endif
 };
 
 // Mode X work list (k_x_classify -> k_mode_x -> k_x_reduce).  A pixel whose every jittered primary
@@ -1434,6 +1448,9 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     };
 
     const uint64_t t_begin = STATS ? clock64() : 0;
+#if GI_X_TAILPROBE
+    if (STATS) cnt.w_start = (uint64_t)wall_clock64();
+#endif
     for (;;) {
         if (HELP && any_gave && phase == PH_DEAD) {   // an idle lane given a shadow ray starts it
             const int ow = hp_.own[tid];
@@ -1463,6 +1480,15 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
         }
         const unsigned long long m_live = __ballot(phase != PH_DEAD);
         if (m_live == 0) break;
+#if GI_X_TAILPROBE
+        if (STATS) {
+            const bool ex = __ballot(cnt.w_exh != 0) != 0;
+            const int own = __popcll(__ballot(phase != PH_DEAD && phase != PH_HELP));   // paths, not helpers
+            if (ex && cnt.w_t1 == 0 && own <= GI_X_TAILPROBE_T1) cnt.w_t1 = (uint64_t)wall_clock64();
+            if (ex && cnt.w_t2 == 0 && own <= GI_X_TAILPROBE_T2) cnt.w_t2 = (uint64_t)wall_clock64();
+            if (ex) { ++cnt.p_it; if (own <= GI_X_TAILPROBE_T1) ++cnt.p_lo; }
+        }
+#endif
         const unsigned long long m_idle = HELP ? ~m_live : 0ull;   // lanes free to take a shadow ray
         bool gave = false;
         const bool trav = raying;
@@ -1863,6 +1889,9 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                         } else if (!have && phase == PH_NEED) {
                             phase = PH_DEAD;                        // no work left
                         }
+#if GI_X_TAILPROBE
+                        if (STATS && nb >= n_blocks && cnt.w_exh == 0) cnt.w_exh = (uint64_t)wall_clock64();
+#endif
                     }
                     if (lane == leader) blk_meta[0] = used_new;
                     __builtin_amdgcn_wave_barrier();
@@ -2051,6 +2080,7 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
             atomicAdd(stats + GI_STAT_X_CYC_HIT, (unsigned long long)c.cyc_hit);
             atomicAdd(stats + GI_STAT_X_CYC_NEXT, (unsigned long long)c.cyc_next);
             atomicAdd(stats + GI_STAT_X_CYC_ALL, (unsigned long long)c.cyc_all);
+#if !GI_X_TAILPROBE
             atomicAdd(stats + GI_STAT_X_IT_NODE, (unsigned long long)c.it_node);
             atomicAdd(stats + GI_STAT_X_LN_NODE, (unsigned long long)c.ln_node);
             atomicAdd(stats + GI_STAT_X_IT_LEAF, (unsigned long long)c.it_leaf);
@@ -2059,6 +2089,7 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
             atomicAdd(stats + GI_STAT_X_LN_RS, (unsigned long long)c.ln_rs);
             atomicAdd(stats + GI_STAT_X_IT_ST, (unsigned long long)c.it_st);
             atomicAdd(stats + GI_STAT_X_LN_ST, (unsigned long long)c.ln_st);
+#endif
         }
         wave_add_stats(stats, c.rays, c.nodes, c.prims, c.px);
         uint64_t cr = c.res, pm = c.path_max;
@@ -2070,6 +2101,25 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
             atomicAdd(stats + GI_STAT_X_RESOLVED, (unsigned long long)cr);
             atomicMax(stats + GI_STAT_X_PATH_MAX, (unsigned long long)pm);
         }
+#if GI_X_TAILPROBE   // (probe, Mode R's slots): the longest drain and the longest wave life, wall ticks
+        uint64_t ex = c.w_exh ? c.w_exh : ~0ull;
+        for (int off = 32; off > 0; off >>= 1) ex = min(ex, (uint64_t)__shfl_xor(ex, off));
+        if ((threadIdx.x & 63) == 0) {   // (slots 16-25 reused) times from the wave's start, wall ticks
+            const uint64_t we = (uint64_t)wall_clock64();
+            const uint64_t te = (ex != ~0ull ? ex : we) - c.w_start, t1 = (c.w_t1 ? c.w_t1 : we) - c.w_start,
+                           t2 = (c.w_t2 ? c.w_t2 : we) - c.w_start, tl = we - c.w_start;
+            atomicMax(stats + 16, (unsigned long long)te);
+            atomicAdd(stats + 17, (unsigned long long)te);
+            atomicMax(stats + 18, (unsigned long long)t1);
+            atomicAdd(stats + 19, (unsigned long long)t1);
+            atomicMax(stats + 20, (unsigned long long)t2);
+            atomicAdd(stats + 21, (unsigned long long)t2);
+            atomicAdd(stats + 22, (unsigned long long)tl);
+            atomicAdd(stats + 23, 1ull);
+            atomicAdd(stats + 24, (unsigned long long)c.p_it);   // wave iterations after exhaustion
+            atomicAdd(stats + 25, (unsigned long long)c.p_lo);   // of those, with <= T1 paths live
+        }
+#endif
     }
 }
 
