@@ -13,6 +13,8 @@
 #                                              every kernel's calls and average us
 #   profiles/r05.sh ab <wls,> <spec> ...        bench lines (kernel ms, ms/frame) per workload and spec,
 #                                              interleaved twice (spec order ABAB) against drift
+#   profiles/r05.sh mem <wls,> <spec> ...       memory-pipeline PMC passes (L2 latency at the L1, TA/TCP
+#                                              stalls, instruction cache) of the dominant kernel
 #   profiles/r05.sh evidence 1|2|forms         1: GPU suite + rocprofv3 stats/PMC of the default kernels
 #                                              (C3 C2 C4 R-C4 C5, or $WLS); 2: shard probes, bench lines
 #                                              of every workload, the C3 bench with its CPU baseline, the
@@ -107,6 +109,21 @@ tk)
   tail -1 $O/tests.log
   if [ -n "$2" ]; then bash $0 benchq $2; fi
   ;;
+mem)
+  # memory-pipeline counters (L2 read latency seen by the L1, TA / TCP stalls, instruction cache)
+  # of a workload's dominant kernel per spec: gpurun_out/r05mem/<w>_mem_<variant>.json
+  O=gpurun_out/r05mem; mkdir -p $O
+  WL=${1//,/ }; shift
+  for SPEC in "$@"; do
+    V=${SPEC%%:*}; E=""; [[ "$SPEC" == *:* ]] && E=${SPEC#*:}; E=${E//,/ }
+    for W in $WL; do
+      w=$(echo $W | tr A-Z a-z); T=${w}_mem_${V}
+      env GI_LIB=$(lib $V) $E PMC_PASSES="TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TCP_TCP_LATENCY_sum TCP_PENDING_STALL_CYCLES_sum;TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_sum;SQC_ICACHE_MISSES SQC_ICACHE_HITS GRBM_GUI_ACTIVE;TCP_READ_TAGCONFLICT_STALL_CYCLES_sum TCP_TCR_TCP_STALL_CYCLES_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum TCP_LFIFO_STALL_CYCLES_sum;SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS" \
+        timeout -k 10 900 bash profiles/run_profile.sh $T --workload $W --steps 3 --warmup 1 > $O/$T.log 2>&1 || { echo "mem $SPEC $W failed"; tail -5 $O/$T.log; exit 1; }
+      python3 profiles/summarize.py gpurun_out/prof_$T $W auto $O/$T.json 4 > /dev/null || exit 1
+      python3 -c "import json,sys; d=json.load(open(sys.argv[1])); c=d['counters_per_launch']; print(sys.argv[2], sys.argv[3], round(d['avg_launch_ns']/1e6,4), {k: round(v) for k, v in sorted(c.items())})" $O/$T.json $SPEC $W
+    done
+  done ;;
 evidence)
   O=gpurun_out/r05ev; mkdir -p $O
   case $1 in
