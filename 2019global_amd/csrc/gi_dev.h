@@ -364,81 +364,6 @@ __device__ __forceinline__ bool child_hit(const XCNode* nd, int c, F3 of, F3 ivf
     return tn <= tf;
 }
 
-// Lane groups (G consecutive lanes tracing one ray together, k_mode_x's group form): a value from the
-// lane q ^ OFF of the group.  Quads by DPP quad permutations (no LDS crossbar), wider by ds_swizzle.
-template <int OFF>
-__device__ __forceinline__ int grp_xor(int v) {
-    if constexpr (OFF == 1) return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);   // [1,0,3,2]
-    else if constexpr (OFF == 2) return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);   // [2,3,0,1]
-    else return __shfl_xor(v, OFF);
-}
-template <int OFF>
-__device__ __forceinline__ double grp_xor(double v) {
-    const long long b = __double_as_longlong(v);
-    const int lo = grp_xor<OFF>((int)(b & 0xFFFFFFFF)), hi = grp_xor<OFF>((int)(b >> 32));
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-// OR of a group's values (every lane of the group gets it)
-template <int G>
-__device__ __forceinline__ uint32_t grp_or(uint32_t m) {
-    if constexpr (G >= 2) m |= (uint32_t)grp_xor<1>((int)m);
-    if constexpr (G >= 4) m |= (uint32_t)grp_xor<2>((int)m);
-    if constexpr (G >= 8) m |= (uint32_t)grp_xor<4>((int)m);
-    return m;
-}
-// the group's (t, primitive) minimum, lexicographic (ties to the lower primitive index, as the serial
-// leaf scan's update rule): every lane of the group ends with it
-template <int G>
-__device__ __forceinline__ void grp_min(double& t, int& p) {
-    auto step = [&](double to, int po) {
-        if (to < t || (to == t && po < p)) { t = to; p = po; }
-    };
-    if constexpr (G >= 2) step(grp_xor<1>(t), grp_xor<1>(p));
-    if constexpr (G >= 4) step(grp_xor<2>(t), grp_xor<2>(p));
-    if constexpr (G >= 8) step(grp_xor<4>(t), grp_xor<4>(p));
-}
-// A quantised node's slab tests split over a G-lane group: lane q tests children q*8/G .. (q+1)*8/G - 1
-// (children_mask_q's arithmetic per child) and the group ORs the bits: the same mask, bit k for child
-// k ^ dmask, on every lane of the group
-template <int G>
-__device__ __forceinline__ uint32_t group_mask_q(int4 h, int4 q1, int4 q2, int4 q3, F3 of, F3 ivf, float tmax,
-                                                 int dmask, int q) {
-    constexpr int PER = 8 / G;
-    const F3 no = neg_oiv(of, ivf);
-    const int sm = iv_signs(ivf);
-    const float iv3[3] = {ivf.x, ivf.y, ivf.z}, no3[3] = {no.x, no.y, no.z};
-    const float o3[3] = {__int_as_float(h.x), __int_as_float(h.y), __int_as_float(h.z)};
-    const int lw[3][2] = {{q1.x, q1.y}, {q1.z, q1.w}, {q2.x, q2.y}};   // qlo x, y, z
-    const int hw[3][2] = {{q2.z, q2.w}, {q3.x, q3.y}, {q3.z, q3.w}};   // qhi x, y, z
-    const int c0 = q * PER;
-    const bool upper = c0 >= 4;   // this lane's children's bytes are all in the second word of each pair
-    float siv[3], base[3];
-    int nw[3], fw[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        siv[a] = xc_scale(h.w, a) * iv3[a];
-        base[a] = __builtin_fmaf(o3[a], iv3[a], no3[a]);
-        const bool neg = (sm >> a) & 1;
-        const int l = upper ? lw[a][1] : lw[a][0], u = upper ? hw[a][1] : hw[a][0];
-        nw[a] = neg ? u : l;
-        fw[a] = neg ? l : u;
-    }
-    uint32_t m = 0;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const int sh = 8 * ((c0 + i) & 3);
-        float tn = 0.0f, tf = tmax;
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            tn = fmaxf(tn, __builtin_fmaf((float)((nw[a] >> sh) & 0xFF), siv[a], base[a]));
-            tf = fminf(tf, __builtin_fmaf((float)((fw[a] >> sh) & 0xFF), siv[a], base[a]));
-        }
-        m |= tn <= tf ? 1u << (c0 + i) : 0u;
-    }
-    m = grp_or<G>(m);
-    return xor_permute8(m & (uint32_t)((h.w >> 24) & 0xFF), dmask);
-}
-
 __device__ __forceinline__ bool root_hit(const DevScene& sc, F3 of, F3 ivf) {
     const float tx0 = (sc.root_lo[0] - of.x) * ivf.x, tx1 = (sc.root_hi[0] - of.x) * ivf.x;
     const float ty0 = (sc.root_lo[1] - of.y) * ivf.y, ty1 = (sc.root_hi[1] - of.y) * ivf.y;

@@ -1192,29 +1192,8 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 #ifndef GI_X_TRI
 #define GI_X_TRI 1   // 4-wave LDS kernel: triangle-only primitive tests and texture mapping (TRI)
 #endif
-#ifndef GI_X_ROOT_LDS
-#define GI_X_ROOT_LDS 1   // k_mode_x, quantised-node scenes: the root's slab bytes in the wave's LDS row
-#endif
-#ifndef GI_X_EXH_SKIP
-#define GI_X_EXH_SKIP 1   // k_mode_x: no refill atomic once the wave has seen the work run out
-#endif
-#ifndef GI_X_GROUP
-#define GI_X_GROUP 1   // quantised-node scenes: lanes per path (mode_x_wave's group form)
-#endif
-#ifndef GI_X_PRIO
-#define GI_X_PRIO 0   // (experiment) wave priority from its remaining paths (1) / its oldest path's age (2)
-#endif
 #ifndef GI_X_TAILPROBE
 #define GI_X_TAILPROBE 0   // (measurement variant) k_mode_x's STATS launch records drain / wave life
-#endif
-#ifndef GI_X_PRIO_A
-#define GI_X_PRIO_A 16
-#endif
-#ifndef GI_X_PRIO_B
-#define GI_X_PRIO_B 8
-#endif
-#ifndef GI_X_PRIO_C
-#define GI_X_PRIO_C 3
 #endif
 #ifndef GI_X_TAILPROBE_T1
 #define GI_X_TAILPROBE_T1 8
@@ -1323,12 +1302,7 @@ __device__ __forceinline__ int nth_set_bit(unsigned long long m, unsigned n) {
 // NST: the wide-node index of every level of the current traversal path lives in LDS (nst[level *
 // 256], one column per lane), so climbing out of exhausted levels is one ds_read instead of a chain
 // of dependent parent-pointer loads from HBM / L2 (one per level climbed).
-// G > 1 (quantised-node scenes): the group form -- G consecutive lanes carry one path, every path
-// value replicated on each of them (all take the same branches), and cooperate only inside a
-// traversal step: a node's 8 slab tests split 8 / G per lane, a leaf's records one per lane, the
-// group's (t, primitive) minimum by DPP.  A wave then runs 64 / G paths with a step of ~1/3 the
-// instructions of the per-lane step.
-template <bool STATS, bool PAIR, bool PSL, bool NST, bool HELP, bool SH, bool TRI, int G, typename NodeP,
+template <bool STATS, bool PAIR, bool PSL, bool NST, bool HELP, bool SH, bool TRI, typename NodeP,
           typename HotP, typename PrimP, typename EntP>
 __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H, PrimP XP, EntP EN, double* pslot,
                                             int* nst, XHelp hp_,
@@ -1343,7 +1317,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     // GI_X_UNITS_PER_LANE units per lane of the grid (every wave computes the same k)
     int k = 1;
     {
-        const double lanes = (double)gridDim.x * (double)blockDim.x / G;   // (paths in flight)
+        const double lanes = (double)gridDim.x * (double)blockDim.x;
         const double samples = (double)n_list * (double)(wk.s1 - wk.s0);
         const int max_run = 1 << ((xflags >> 8) & 7);
         while (2 * k <= max_run && 2 * k <= wk.s1 - wk.s0 && samples / (2.0 * k) >= GI_X_UNITS_PER_LANE * lanes) k *= 2;
@@ -1367,11 +1341,6 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     const bool no_shadow = (xflags & 4) != 0;   // GI_FLAG_X_NO_SHADOW (tests): every light visible
     const bool handoff = HELP && (xflags & 8) != 0 && !no_shadow;
     const int tid = threadIdx.x, wbase = tid & ~63;
-    static_assert(G == 1 || (!HELP && !PAIR && !PSL), "the group form: HBM-resident quantised-node scenes, no handoff");
-    const int gq = lane & (G - 1);   // the lane's place in its group
-    const bool wr = gq == 0;         // the group's writer (output, counters)
-    constexpr unsigned long long kLead = G == 1 ? ~0ull : G == 2 ? 0x5555555555555555ull
-                                       : G == 4 ? 0x1111111111111111ull : 0x0101010101010101ull;
     if (HELP) {
         hp_.own[tid] = -1;
         hp_.res[tid] = 0;
@@ -1463,49 +1432,6 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
         }
     };
 
-    // the group form's leaf: record j = q, q + G, ... on lane q (the first already in cur), then the
-    // group's (t, primitive) minimum -- the serial scan's result (its update rule is that minimum)
-    auto leaf_test_grp = [&](XHotR cur, const auto* hp, int cntl) {
-        double tm = INFINITY;
-        int pm = 0x7FFFFFFF;
-        for (int j0 = 0; j0 < cntl; j0 += G) {
-            const int j = j0 + gq;
-            if (j0 > 0) cur = load_hot(hp + min(j, cntl - 1));
-            if (j < cntl) {
-                ++nprim;
-                const double t = x_prim_t<TRI>(cur.h, o, d, MX_TMIN);
-                if (t < tm || (t == tm && cur.h.prim < pm)) { tm = t; pm = cur.h.prim; }
-            }
-        }
-        grp_min<G>(tm, pm);
-        if (phase != PH_CLOSEST) {
-            if (tm < tmax) { best = pm; raying = false; }   // any hit occludes
-        } else if (tm < tbest || (tm == tbest && pm < best)) {
-            tbest = tm;
-            best = pm;
-            tbest_f = up32(tm);
-        }
-    };
-    // the root's child mask at a ray start: per lane, or split over the group.  Quantised-node
-    // scenes read the root's 64 slab bytes from the wave's LDS row (copied at the start: every ray
-    // start tests the root, and an L2 round trip there sits on every path's critical path)
-    constexpr bool ROOTL = GI_X_ROOT_LDS != 0 &&
-                           std::is_same<std::remove_cv_t<std::remove_pointer_t<NodeP>>, XCNode>::value;
-    int4* root_q = reinterpret_cast<int4*>(blk_list + 68);
-    if constexpr (ROOTL) {
-        if (lane < 4) root_q[lane] = reinterpret_cast<const int4*>(W)[lane];
-        __builtin_amdgcn_wave_barrier();
-    }
-    auto root_mask = [&]() -> uint32_t {
-        if constexpr (G > 1) {
-            const int4* qb = ROOTL ? root_q : reinterpret_cast<const int4*>(W);
-            return group_mask_q<G>(qb[0], qb[1], qb[2], qb[3], of, ivf, tbest_f, dmask, gq);
-        } else if constexpr (ROOTL) {
-            return children_mask_q(root_q[0], root_q[1], root_q[2], root_q[3], of, ivf, tbest_f, dmask);
-        } else {
-            return children_mask<PAIR>(W, of, ivf, tbest_f, dmask);
-        }
-    };
 
     // PF (HBM-resident scenes): the next pop's child reference and leaf count are fetched at the
     // end of the step that sets up the level (descend, climb or ray start), so the pop itself waits
@@ -1523,10 +1449,6 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     };
 
     const uint64_t t_begin = STATS ? clock64() : 0;
-#if GI_X_PRIO
-    int prio = 0;
-    uint32_t prio_it = 0, age = 0;   // age: traversal steps of the lane's current path
-#endif
 #if GI_X_TAILPROBE
     if (STATS) cnt.w_start = (uint64_t)wall_clock64();
 #endif
@@ -1550,7 +1472,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 tbest_f = up32(tmax);
                 phase = PH_HELP;
                 best = -1;
-                const uint32_t rm = root_mask();
+                const uint32_t rm = children_mask<PAIR>(W, of, ivf, tbest_f, dmask);
                 node = 0;
                 lvl_set<SH>(mlo, mhi, 0, rm);
                 raying = rm != 0;
@@ -1559,29 +1481,6 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
         }
         const unsigned long long m_live = __ballot(phase != PH_DEAD);
         if (m_live == 0) break;
-#if GI_X_PRIO
-        if ((++prio_it & 7) == 0) {
-            int p = 0;
-            if (GI_X_PRIO == 1) {
-                if (blk_meta[3]) {
-                    const int own = __popcll(__ballot(phase != PH_DEAD && phase != PH_HELP));
-                    p = own >= GI_X_PRIO_A ? 3 : own >= GI_X_PRIO_B ? 2 : own >= GI_X_PRIO_C ? 1 : 0;
-                }
-            } else {
-                uint32_t mx = (phase != PH_DEAD && phase != PH_HELP) ? age : 0u;
-                for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, off));
-                p = mx >= GI_X_PRIO_A ? 3 : mx >= GI_X_PRIO_B ? 2 : mx >= GI_X_PRIO_C ? 1 : 0;
-            }
-            p = __builtin_amdgcn_readfirstlane(p);
-            if (p != prio) {
-                prio = p;
-                if (p == 3) __builtin_amdgcn_s_setprio(3);
-                else if (p == 2) __builtin_amdgcn_s_setprio(2);
-                else if (p == 1) __builtin_amdgcn_s_setprio(1);
-                else __builtin_amdgcn_s_setprio(0);
-            }
-        }
-#endif
 #if GI_X_TAILPROBE
         if (STATS) {
             const bool ex = __ballot(cnt.w_exh != 0) != 0;
@@ -1615,9 +1514,6 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
         const uint64_t t0 = STATS ? clock64() : 0;
         if (STATS) ++cnt.path_it;
         if (trav) {
-#if GI_X_PRIO
-            ++age;
-#endif
             if (STATS) {
                 ++nsteps;
                 ++cnt.path_st;
@@ -1658,7 +1554,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 XHotR ur;
                 const int cntl = ch < 0 ? (PF ? pf_cnt : (int)nd->cnt[c]) : 0;
                 if (ch < 0) {
-                    ur = load_hot(H + ~ch + (G > 1 ? min(gq, cntl - 1) : 0));
+                    ur = load_hot(H + ~ch);
                 } else {
                     const int4* qb = reinterpret_cast<const int4*>(W + ch);
                     ur.q[0] = qb[0];
@@ -1667,12 +1563,10 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     ur.q[3] = qb[3];
                 }
                 if (ch < 0) {
-                    if constexpr (G > 1) leaf_test_grp(ur, H + ~ch, cntl);
-                    else leaf_test_from(ur, H + ~ch, cntl);
+                    leaf_test_from(ur, H + ~ch, cntl);
                 } else {
                     ++nnode;
-                    const uint32_t cm = G > 1 ? group_mask_q<G>(ur.q[0], ur.q[1], ur.q[2], ur.q[3], of, ivf, tbest_f, dmask, gq)
-                                              : children_mask_q(ur.q[0], ur.q[1], ur.q[2], ur.q[3], of, ivf, tbest_f, dmask);
+                    const uint32_t cm = children_mask_q(ur.q[0], ur.q[1], ur.q[2], ur.q[3], of, ivf, tbest_f, dmask);
                     if (cm) {
                         node = ch;
                         ++level;
@@ -1925,9 +1819,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     cnt.path_max = max(cnt.path_max, (((uint64_t)wall_clock64() - cnt.path_t0) << 32) |
                                                          ((uint64_t)min(cnt.path_it, 65535u) << 16) |
                                                          (uint64_t)min(cnt.path_st, 65535u));
-                if (!wr) {
-                    // (group form: the group's first lane writes)
-                } else if (spp == 1) {   // the pixel: min((0 + L) / 1, 1), the reduce pass's operations
+                if (spp == 1) {   // the pixel: min((0 + L) / 1, 1), the reduce pass's operations
                     const double c0 = smin((0.0 + Lv.x) / 1.0, 1.0), c1 = smin((0.0 + Lv.y) / 1.0, 1.0),
                                  c2 = smin((0.0 + Lv.z) / 1.0, 1.0);
                     if (rgb) { rgb[3 * idx] = c0; rgb[3 * idx + 1] = c1; rgb[3 * idx + 2] = c2; }
@@ -1961,10 +1853,8 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     // for at most 64 units = one block).  The block's 64 list entries live in this
                     // wave's LDS row (the lanes that run the handler load them; the others may be
                     // traversing), so handing out a unit costs one ds_read.
-                    // (group form: one unit per group, ranked among the groups' first lanes)
-                    const unsigned long long m_nl = m_need & kLead;
-                    const unsigned rank = (unsigned)__popcll(m_nl & ((1ull << (lane & ~(G - 1))) - 1));
-                    const unsigned n_need = (unsigned)__popcll(m_nl);
+                    const unsigned rank = (unsigned)__popcll(m_need & ((1ull << lane) - 1));
+                    const unsigned n_need = (unsigned)__popcll(m_need);
                     const int leader = __ffsll((long long)m_need) - 1;
                     const unsigned used = blk_meta[0];
                     unsigned g = blk_meta[1], c = blk_meta[2];
@@ -1978,7 +1868,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                         // each would be an L2 round trip for nothing (C4 spends ~90% of its loop
                         // iterations after that point, ending ~100 paths per wave)
                         unsigned nb = n_blocks;
-                        if (!GI_X_EXH_SKIP || blk_meta[3] == 0u) {
+                        if (blk_meta[3] == 0u) {
                             if (lane == leader) nb = atomicAdd(wk.blocks, 1u);
                             nb = __shfl(nb, leader);
                         }
@@ -2045,8 +1935,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                         if (!root_hit(sc, f3((float)cam.pos.x, (float)cam.pos.y, (float)cam.pos.z), iv0)) {
                             ++nrays;   // background sample: L = 0
                             ++nres;
-                            if (!wr) {
-                            } else if (spp > 1) {
+                            if (spp > 1) {
                                 double* q = wk.part + 3 * ((size_t)idx * (size_t)spp + (size_t)smp);
                                 q[0] = 0.0; q[1] = 0.0; q[2] = 0.0;
                             } else {   // spp == 1: the pixel is 0
@@ -2059,9 +1948,6 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                             continue;
                         }
                     }
-#if GI_X_PRIO
-                    age = 0;
-#endif
                     if (STATS) {
                         cnt.path_t0 = (uint64_t)wall_clock64();
                         cnt.path_it = 0;
@@ -2087,7 +1973,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 of = f3((float)o.x, (float)o.y, (float)o.z);
                 ivf = inv_dir(d);
                 dmask = (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
-                const uint32_t rm = root_mask();
+                const uint32_t rm = children_mask<PAIR>(W, of, ivf, tbest_f, dmask);
                 if (phase == PH_START) phase = PH_CLOSEST;
                 best = -1;
                 node = 0;   // root wide node
@@ -2108,9 +1994,6 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
         }
     }
     if (STATS) cnt.cyc_all += clock64() - t_begin;
-    if (!wr) {   // (group form: a group's rays, nodes, pixels and steps counted once; leaf records per lane)
-        nrays = nres = npx = nnode = nsteps = 0;
-    }
     if (STATS) {   // lane traversal steps, summed over the wave into lane 0
         uint64_t ns = nsteps;
         for (int off = 32; off > 0; off >>= 1) ns += __shfl_xor(ns, off);
@@ -2144,8 +2027,7 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
                                                  uint64_t seed, double* rgb, uint8_t* rgb8,
                                                  unsigned long long* stats, XWork wk, int handle8, int xflags) {
     XCounters c;
-    // per wave: current block's list entries + state, then the root node's 64 slab bytes (ROOTL)
-    __shared__ __align__(16) unsigned s_blk[kWavesPerBlock][84];
+    __shared__ unsigned s_blk[kWavesPerBlock][68];   // per wave: current block's list entries + state
     unsigned* blk = s_blk[threadIdx.x >> 6];
     if (LDS) {
         extern __shared__ int4 lds_scene[];
@@ -2172,7 +2054,7 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
         // (occluded sum, next direction, throughput T, RNG key) live in a per-lane LDS slot after
         // the scene instead of in VGPRs / scratch
         double* pslot = reinterpret_cast<double*>(lds_scene + nw + nh + np + ne) + 10 * threadIdx.x;
-        mode_x_wave<STATS, GI_X_PAIR != 0, W4 && GI_X_PSL, false, false, SH, W4 && GI_X_TRI, 1>(sc, W, H, XP, EN, pslot, nullptr, XHelp{},
+        mode_x_wave<STATS, GI_X_PAIR != 0, W4 && GI_X_PSL, false, false, SH, W4 && GI_X_TRI>(sc, W, H, XP, EN, pslot, nullptr, XHelp{},
                                                                         cam, light, m, spp, depth, seed, rgb, rgb8, blk,
                                                                         wk, handle8, xflags, c);
     } else {
@@ -2184,12 +2066,12 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
         hp.own = reinterpret_cast<int*>(hp.ray + 7 * 256);
         hp.res = hp.own + 256;
         if constexpr (CN)   // quantised nodes (the default for large HBM-resident scenes)
-            mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0 && GI_X_GROUP == 1, SH, TR && GI_X_TRI, GI_X_GROUP>(sc, sc.xcnodes, sc.xhot, sc.xprims,
+            mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0, SH, TR && GI_X_TRI>(sc, sc.xcnodes, sc.xhot, sc.xprims,
                                                                             sc.ents, nullptr, lds_nst + threadIdx.x, hp,
                                                                             cam, light, m, spp, depth, seed, rgb, rgb8,
                                                                             blk, wk, handle8, xflags, c);
         else
-            mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0, SH, TR && GI_X_TRI, 1>(sc, sc.xwnodes, sc.xhot, sc.xprims,
+            mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0, SH, TR && GI_X_TRI>(sc, sc.xwnodes, sc.xhot, sc.xprims,
                                                                             sc.ents, nullptr, lds_nst + threadIdx.x, hp,
                                                                             cam, light, m, spp, depth, seed, rgb, rgb8,
                                                                             blk, wk, handle8, xflags, c);
