@@ -701,6 +701,19 @@ void build_rcand(HostScene& hs) {
         }
         hs.app_off[e + 1] = (int32_t)hs.app_rank.size();
     }
+    // the device's records: every path entry's node box, every appearance's rank and path range
+    hs.rpath_rec.resize(hs.rpath.size());
+    for (size_t i = 0; i < hs.rpath.size(); ++i) {
+        const RNode& r = hs.rnodes[(size_t)hs.rpath[i]];
+        RPathRec& q = hs.rpath_rec[i];
+        for (int k = 0; k < 3; ++k) { q.mn[k] = r.mn[k]; q.mx[k] = r.mx[k]; }
+        q.node = hs.rpath[i];
+        q.ent_cnt = r.ent_cnt;
+        q.pad[0] = q.pad[1] = 0;
+    }
+    hs.app_rec.resize(hs.app_rank.size());
+    for (size_t a = 0; a < hs.app_rank.size(); ++a)
+        hs.app_rec[a] = RApp{hs.app_rank[a], hs.rpath_off[(size_t)hs.app_leaf[a]], hs.rpath_off[(size_t)hs.app_leaf[a] + 1]};
     // line BVH over the entities that appear somewhere
     std::vector<XPrim> atoms;
     std::vector<double> bounds;

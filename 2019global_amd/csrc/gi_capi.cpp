@@ -478,9 +478,8 @@ int scene_create_on(const gi_scene_desc* desc, int device, gi_scene** out) {
         (e = upload(sp, h.xbox, &d.xbox)) != hipSuccess ||
         (e = upload(sp, h.xprims, &d.xprims)) != hipSuccess ||
         (e = upload(sp, std::vector<unsigned>(16, 0u), const_cast<const unsigned**>(&d.work))) != hipSuccess ||
-        (e = upload(sp, h.app_off, &d.app_off)) != hipSuccess || (e = upload(sp, h.app_leaf, &d.app_leaf)) != hipSuccess ||
-        (e = upload(sp, h.app_rank, &d.app_rank)) != hipSuccess || (e = upload(sp, h.rpath_off, &d.rpath_off)) != hipSuccess ||
-        (e = upload(sp, h.rpath, &d.rpath)) != hipSuccess || (e = upload(sp, h.rc_nodes, &d.rc_nodes)) != hipSuccess ||
+        (e = upload(sp, h.app_off, &d.app_off)) != hipSuccess || (e = upload(sp, h.app_rec, &d.app_rec)) != hipSuccess ||
+        (e = upload(sp, h.rpath_rec, &d.rpath_rec)) != hipSuccess || (e = upload(sp, h.rc_nodes, &d.rc_nodes)) != hipSuccess ||
         (e = upload(sp, h.rc_ent, &d.rc_ent)) != hipSuccess || (e = upload(sp, h.rc_maxkey, &d.rc_maxkey)) != hipSuccess ||
         (e = upload(sp, h.r_always, &d.r_always)) != hipSuccess ||
         (e = upload(sp, h.r_leaf_of_rank, &d.r_leaf_of_rank)) != hipSuccess)

@@ -319,14 +319,32 @@ struct RMemo {
 };
 __device__ __forceinline__ int r_memo_slot(int node) { return (int)(((unsigned)node * 2654435761u) >> 26) & (GI_R_MEMO - 1); }
 
-// is leaf `leaf` in the ray's candidate list?  (octree.h:139-150 on its root path, top-down)
-__device__ __forceinline__ bool r_leaf_reachable(const DevScene& sc, int leaf, V3 o, V3 d, uint32_t& nnode,
+// is the leaf whose root path is rpath_rec[p0 .. p1) in the ray's candidate list?  (octree.h:139-150
+// on that path, top-down: every node non-empty and hit by the exact ExpBox test.)  The path's node
+// records are consecutive, so the next one is loaded before the current one's test -- the walk waits
+// on one load round trip per path, not two per node (rpath[i], then rnodes[rpath[i]]).
+struct RPathR {
+    union {
+        int4 q[4];
+        RPathRec r;
+    };
+};
+__device__ __forceinline__ RPathR load_rpath(const RPathRec* p) {
+    const int4* s = reinterpret_cast<const int4*>(p);
+    RPathR r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r.q[i] = s[i];
+    return r;
+}
+__device__ __forceinline__ bool r_path_reachable(const DevScene& sc, int p0, int p1, V3 o, V3 d, uint32_t& nnode,
                                                  RMemo memo = RMemo{nullptr}) {
-    const int p1 = sc.rpath_off[leaf + 1];
-    for (int i = sc.rpath_off[leaf]; i < p1; ++i) {
-        const int ni = sc.rpath[i];
-        const RNode& nd = sc.rnodes[ni];
-        if (nd.ent_cnt == 0) return false;   // octree.h:140
+    if (p0 >= p1) return true;
+    RPathR cur = load_rpath(sc.rpath_rec + p0);
+    for (int i = p0; i < p1; ++i) {
+        const RPathR nd = cur;
+        if (i + 1 < p1) cur = load_rpath(sc.rpath_rec + i + 1);
+        if (nd.r.ent_cnt == 0) return false;   // octree.h:140
+        const int ni = nd.r.node;
         if (GI_R_MEMO > 0 && memo.e) {
             int* slot = memo.e + r_memo_slot(ni);
             const int m = *slot;
@@ -336,13 +354,13 @@ __device__ __forceinline__ bool r_leaf_reachable(const DevScene& sc, int leaf, V
                 continue;
             }
             ++nnode;
-            const bool ok = box_hit(ld3(nd.mn), ld3(nd.mx), o, d);
+            const bool ok = box_hit(ld3(nd.r.mn), ld3(nd.r.mx), o, d);
             *slot = key | (ok ? 1 : 0);
             if (!ok) return false;
             continue;
         }
         ++nnode;
-        if (!box_hit(ld3(nd.mn), ld3(nd.mx), o, d)) return false;
+        if (!box_hit(ld3(nd.r.mn), ld3(nd.r.mx), o, d)) return false;
     }
     return true;
 }
@@ -352,13 +370,14 @@ template <bool TRI = false>
 __device__ __forceinline__ void r_consider(const DevScene& sc, int e, V3 o, V3 d, long long& best, RResult& r,
                                            uint32_t& nnode, uint32_t& nprim, RMemo memo = RMemo{nullptr}) {
     const int a0 = sc.app_off[e], a1 = sc.app_off[e + 1];
-    if (a0 == a1 || sc.app_rank[a0] <= best) return;
+    if (a0 == a1 || sc.app_rec[a0].rank <= best) return;
     V3 P, N;
     if (!ent_hit<TRI>(sc, sc.ents[e], o, d, P, N, nprim) || !(sq3(P - o) < DBL_MAX)) return;   // raytracer.h:58-65
     for (int i = a0; i < a1; ++i) {
-        const long long rk = sc.app_rank[i];
+        const RApp ap = sc.app_rec[i];
+        const long long rk = ap.rank;
         if (rk <= best) return;
-        if (r_leaf_reachable(sc, sc.app_leaf[i], o, d, nnode, memo)) {
+        if (r_path_reachable(sc, ap.p0, ap.p1, o, d, nnode, memo)) {
             best = rk;
             r.ent = e;
             r.P = P;
@@ -565,7 +584,7 @@ __global__ __launch_bounds__(256) void k_mode_r_batch(DevScene sc, CamDev cam, V
                     if (pcur < pend) {   // the current leaf's entities: those that can still win
                         const int e = sc.rc_ent[pcur++];
                         const int a0 = sc.app_off[e];
-                        if (a0 != sc.app_off[e + 1] && sc.app_rank[a0] > best) seg[nq++] = e;
+                        if (a0 != sc.app_off[e + 1] && sc.app_rec[a0].rank > best) seg[nq++] = e;
                         continue;
                     }
                     if (steps >= GI_R_BATCH_STEPS || done) break;
@@ -674,6 +693,12 @@ __global__ __launch_bounds__(256) void k_mode_r_batch(DevScene sc, CamDev cam, V
 #define GI_RF_S0 512u     // pairs of a tile's own region (8 per pixel slot)
 #define GI_RF_PAGE 512u   // pairs per pool page
 #define GI_RF_KMAX 64u    // pool pages a tile may take (so at most 33,280 pairs per tile)
+#ifndef GI_RF_CHUNK
+#define GI_RF_CHUNK 64   // k_rf_reach: hits per wave chunk
+#endif
+#ifndef GI_RF_PROBE
+#define GI_RF_PROBE 0   // (measurement variant) k_rf_reach's STATS launch records its chunks' work and time
+#endif
 constexpr unsigned kRfOvf = 0xFFFFFFFFu;
 constexpr unsigned kRfEntMask = (1u << 26) - 1u;   // scenes of more entities run k_mode_r_batch
 struct RFlat {
@@ -1071,11 +1096,19 @@ __global__ __launch_bounds__(64) void k_rf_reach(DevScene sc, CamDev cam, TileMa
         for (int k = 0; k < GI_R_MEMO; ++k) s_memo[lane * GI_R_MEMO + k] = -1;   // (matches no key)
     __builtin_amdgcn_wave_barrier();
     uint32_t nnode = 0;
+#if GI_RF_PROBE   // (measurement build; STATS launches, Mode X's slots 5-12): the chunks' work and time
+    const uint64_t pt0 = (uint64_t)wall_clock64();
+    uint32_t p_app = 0, p_nn0 = 0, p_ch = 0;
+#endif
     // (chunks from a device counter instead, as waves free up: R-C4 0.80 -> 0.88 ms)
-    for (long long c = gw; 64 * c < n_hits; c += n_w) {
-        const long long i = 64 * c + lane;
-        long long sg = rf_find(f.hoff, n_seg, 64 * c);   // the chunk's first segment (uniform)
-        if (i < n_hits) {
+    constexpr int K = GI_RF_CHUNK;   // hits per chunk (lanes >= K idle)
+    for (long long c = gw; (long long)K * c < n_hits; c += n_w) {
+#if GI_RF_PROBE
+        ++p_ch;
+#endif
+        const long long i = (long long)K * c + lane;
+        long long sg = rf_find(f.hoff, n_seg, (long long)K * c);   // the chunk's first segment (uniform)
+        if (lane < K && i < n_hits) {
             while (sg + 1 < n_seg && (long long)f.hoff[sg + 1] <= i) ++sg;   // this lane's
             const long long r = f.sreg[sg];
             const unsigned p = (unsigned)(sg - (long long)f.soff[r]) * GI_RF_SEG + (unsigned)(i - (long long)f.hoff[sg]);
@@ -1087,15 +1120,42 @@ __global__ __launch_bounds__(64) void k_rf_reach(DevScene sc, CamDev cam, TileMa
             const V3 d = rf_dir(f, slot);
             const int a1 = sc.app_off[e + 1];
             for (int a = sc.app_off[e]; a < a1; ++a) {
-                const long long rk = sc.app_rank[a];
+                const RApp ap = sc.app_rec[a];
+                const long long rk = ap.rank;
                 if (rk <= (long long)*(volatile unsigned long long*)(f.best + slot) - 1) break;
-                if (r_leaf_reachable(sc, sc.app_leaf[a], cam.pos, d, nnode, memo)) {
+#if GI_RF_PROBE
+                ++p_app;
+#endif
+                if (r_path_reachable(sc, ap.p0, ap.p1, cam.pos, d, nnode, memo)) {
                     atomicMax(f.best + slot, (unsigned long long)(rk + 1));
                     break;
                 }
             }
         }
     }
+#if GI_RF_PROBE
+    if (STATS && p_ch) {
+        const uint64_t dt = (uint64_t)wall_clock64() - pt0;
+        uint32_t mapp = p_app, mnn = nnode, sapp = p_app, snn = nnode;
+        for (int off = 32; off > 0; off >>= 1) {
+            mapp = max(mapp, (uint32_t)__shfl_xor(mapp, off));
+            mnn = max(mnn, (uint32_t)__shfl_xor(mnn, off));
+            sapp += __shfl_xor(sapp, off);
+            snn += __shfl_xor(snn, off);
+        }
+        if (lane == 0) {
+            atomicMax(stats + 5, (unsigned long long)dt);        // the slowest wave (wall ticks)
+            atomicAdd(stats + 6, (unsigned long long)dt);
+            atomicAdd(stats + 7, 1ull);                          // waves with work
+            atomicMax(stats + 8, (unsigned long long)mapp);      // most appearances one lane walked
+            atomicMax(stats + 9, (unsigned long long)mnn);       // most node tests one lane ran
+            atomicMax(stats + 10, (unsigned long long)snn);      // most node tests one wave ran
+            atomicAdd(stats + 11, (unsigned long long)sapp);     // appearances walked
+            atomicAdd(stats + 12, (unsigned long long)p_ch);     // chunks
+            atomicMax(stats + 13, ((unsigned long long)dt << 32) | min(snn, 0xFFFFFFFFu));   // the slowest wave's node tests
+        }
+    }
+#endif
     if (STATS) wave_add_stats(stats, 0, nnode, 0, 0);
 }
 // per pixel: the best rank's entity, shaded (overflowed tiles: left to k_mode_r_batch)

@@ -27,6 +27,22 @@ struct RNode {             // 64 bytes
 };
 static_assert(sizeof(RNode) == 64, "RNode layout");
 
+// Mode R reachability records (the flat reach phase and the candidate walks, round 5): a leaf's root
+// path laid out as consecutive node records, so a walk down it streams one record after another (the
+// next load issued before the current exact node test) instead of chasing rpath[i] -> rnodes[...].
+struct RPathRec {          // 64 bytes: the node's box, its id (memo key) and emptiness
+    double mn[3], mx[3];
+    int32_t node;
+    int32_t ent_cnt;
+    int32_t pad[2];
+};
+static_assert(sizeof(RPathRec) == 64, "RPathRec layout");
+struct RApp {              // 16 bytes: one appearance of an entity, by decreasing rank
+    int64_t rank;          // (leaf's rank in the reference's DFS order << 32) | position
+    int32_t p0, p1;        // its leaf's root path: rpath_rec[p0 .. p1), top-down
+};
+static_assert(sizeof(RApp) == 16, "RApp layout");
+
 struct REnt {              // 208 bytes
     int32_t kind, tri_first, tri_count, pad0;
     double pos[3];         // ImpSphere / ExpSphere / ExpCone centre, ExpQuad / ExpCube pos
@@ -137,6 +153,8 @@ struct HostScene {
     std::vector<int64_t> app_rank;   //   (leaf's rank in the reference's DFS order << 32) | position
     std::vector<int32_t> rpath_off;  // per node (n_rnodes + 1): its path below the root, top-down
     std::vector<int32_t> rpath;      //   (filled for leaves; the leaf itself is the last entry)
+    std::vector<RPathRec> rpath_rec; // rpath's node records, in the same order (the device reads these)
+    std::vector<RApp> app_rec;       // app_rank / app_leaf as (rank, path range) records (device)
     std::vector<XWNode> rc_nodes;    // line BVH over the non-sphere entities that appear in a leaf
     std::vector<int32_t> rc_ent;     //   entity of each leaf record
     std::vector<int64_t> rc_maxkey;  //   per node slot (8 per node): the highest app_rank under it;
@@ -193,10 +211,8 @@ struct DevScene {
     float root_lo[3], root_hi[3];   // Mode X: union of the root's fp32 child boxes (conservative)
     // Mode R candidate reconstruction (HostScene fields of the same names)
     const int32_t* app_off;
-    const int32_t* app_leaf;
-    const int64_t* app_rank;
-    const int32_t* rpath_off;
-    const int32_t* rpath;
+    const RApp* app_rec;
+    const RPathRec* rpath_rec;
     const XWNode* rc_nodes;
     const int32_t* rc_ent;
     const int64_t* rc_maxkey;

@@ -214,6 +214,20 @@ static int run(const std::vector<gi_entity_desc>& ents, const double box[6], int
     std::string err;
     if (!build_host_scene(sd, hs, err)) { std::printf("build failed: %s\n", err.c_str()); return 2; }
     long hits = 0, considered = 0, bad = 0;
+    // the device's records restate rpath / rnodes and app_rank / app_leaf exactly
+    if (hs.rpath_rec.size() != hs.rpath.size() || hs.app_rec.size() != hs.app_rank.size()) ++bad;
+    for (size_t i = 0; i < hs.rpath_rec.size() && i < hs.rpath.size(); ++i) {
+        const RNode& nd = hs.rnodes[(size_t)hs.rpath[i]];
+        const RPathRec& q = hs.rpath_rec[i];
+        bool ok = q.node == hs.rpath[i] && q.ent_cnt == nd.ent_cnt;
+        for (int k = 0; k < 3; ++k) ok = ok && q.mn[k] == nd.mn[k] && q.mx[k] == nd.mx[k];
+        if (!ok) { ++bad; if (bad < 5) std::printf("  path record %zu differs\n", i); }
+    }
+    for (size_t a = 0; a < hs.app_rec.size() && a < hs.app_rank.size(); ++a) {
+        const int lf = hs.app_leaf[a];
+        if (hs.app_rec[a].rank != hs.app_rank[a] || hs.app_rec[a].p0 != hs.rpath_off[(size_t)lf] ||
+            hs.app_rec[a].p1 != hs.rpath_off[(size_t)lf + 1]) { ++bad; if (bad < 5) std::printf("  appearance record %zu differs\n", a); }
+    }
     for (int r = 0; r < nrays; ++r) {
         V3 o = (r % 2 == 0) ? v3(-10, 0, 0) : v3(urand() * 24 - 12, urand() * 24 - 12, urand() * 24 - 12);
         V3 tgt = v3(urand() * 16 - 4, urand() * 14 - 7, urand() * 14 - 7);
