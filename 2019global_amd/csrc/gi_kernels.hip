@@ -693,9 +693,6 @@ __global__ __launch_bounds__(256) void k_mode_r_batch(DevScene sc, CamDev cam, V
 #define GI_RF_S0 512u     // pairs of a tile's own region (8 per pixel slot)
 #define GI_RF_PAGE 512u   // pairs per pool page
 #define GI_RF_KMAX 64u    // pool pages a tile may take (so at most 33,280 pairs per tile)
-#ifndef GI_RF_CHUNK
-#define GI_RF_CHUNK 64   // k_rf_reach: hits per wave chunk
-#endif
 #ifndef GI_RF_PROBE
 #define GI_RF_PROBE 0   // (measurement variant) k_rf_reach's STATS launch records its chunks' work and time
 #endif
@@ -1101,14 +1098,13 @@ __global__ __launch_bounds__(64) void k_rf_reach(DevScene sc, CamDev cam, TileMa
     uint32_t p_app = 0, p_nn0 = 0, p_ch = 0;
 #endif
     // (chunks from a device counter instead, as waves free up: R-C4 0.80 -> 0.88 ms)
-    constexpr int K = GI_RF_CHUNK;   // hits per chunk (lanes >= K idle)
-    for (long long c = gw; (long long)K * c < n_hits; c += n_w) {
+    for (long long c = gw; 64 * c < n_hits; c += n_w) {
 #if GI_RF_PROBE
         ++p_ch;
 #endif
-        const long long i = (long long)K * c + lane;
-        long long sg = rf_find(f.hoff, n_seg, (long long)K * c);   // the chunk's first segment (uniform)
-        if (lane < K && i < n_hits) {
+        const long long i = 64 * c + lane;
+        long long sg = rf_find(f.hoff, n_seg, 64 * c);   // the chunk's first segment (uniform)
+        if (i < n_hits) {
             while (sg + 1 < n_seg && (long long)f.hoff[sg + 1] <= i) ++sg;   // this lane's
             const long long r = f.sreg[sg];
             const unsigned p = (unsigned)(sg - (long long)f.soff[r]) * GI_RF_SEG + (unsigned)(i - (long long)f.hoff[sg]);
