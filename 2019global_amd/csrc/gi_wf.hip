@@ -504,7 +504,10 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
 #define GI_SEG_BURST 16
 #endif
 #ifndef GI_SEG_TAKE
-#define GI_SEG_TAKE 4   // k_seg: most batches of 64 units per run (one atomic per run)
+#define GI_SEG_TAKE 2       // k_seg: most batches of 64 units per run (one atomic per run)
+#endif
+#ifndef GI_SEG_TAKE_TRI
+#define GI_SEG_TAKE_TRI 1   // the same for LDS-resident triangle-only scenes (the Cornell box)
 #endif
 template <bool STATS, bool LDS, bool W4, bool SH, bool TRI, bool CN>
 __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_WAVES) void k_seg(
@@ -517,11 +520,15 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
     const unsigned long long total = (unsigned long long)*a.n_list * (unsigned long long)a.ns;
     // run length: up to GI_SEG_TAKE batches of 64 units per atomic (background-heavy frames burn units
     // fast: longer runs, fewer atomics on the one counter), fewer when the launch has less than about
-    // 8 runs per resident wave (small launches: every wave gets work).  Guided self-scheduling --
-    // run sizes from a relaxed read of the counter -- measured 1.2-2.6x slower (the read waits behind
-    // the atomics on that L2 line).
+    // 8 runs per resident wave (small launches: every wave gets work).  Round 5, after the spill fix
+    // (profiles/r05_ab.txt): 4 -> 2 batches gives C3 5.09 -> 4.95 ms and X-zoo 4.35-4.43 -> 4.17-4.19,
+    // X-main and the 1k soup unchanged; 1 batch gives C3 4.89-4.90 but X-main 0.38 -> 0.69 and X-zoo
+    // 4.67 (their frames are background-heavy or shading-heavy), so 1 only for LDS-resident
+    // triangle-only scenes.  Guided self-scheduling -- run sizes from a relaxed read of the counter --
+    // measured 1.2-2.6x slower (the read waits behind the atomics on that L2 line).
+    constexpr long long kTake = (LDS && TRI) ? GI_SEG_TAKE_TRI : GI_SEG_TAKE;
     const unsigned long long n_waves = (unsigned long long)gridDim.x * (blockDim.x >> 6);
-    const unsigned long long run = 64ull * (unsigned long long)max(1ll, min((long long)GI_SEG_TAKE, (long long)(total / (64ull * 8ull * n_waves))));
+    const unsigned long long run = 64ull * (unsigned long long)max(1ll, min(kTake, (long long)(total / (64ull * 8ull * n_waves))));
     uint32_t nnode = 0, nprim = 0, nrays = 0, nres = 0, npx = 0;
     unsigned long long cur = 0, cur_end = 0;   // the wave's unhanded units [cur, cur_end) (uniform)
     bool exhausted = false;                    // the frame's units are all handed out (uniform)
