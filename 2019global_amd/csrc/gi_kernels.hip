@@ -1248,6 +1248,9 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 #ifndef GI_X_TRI
 #define GI_X_TRI 1   // 4-wave LDS kernel: triangle-only primitive tests and texture mapping (TRI)
 #endif
+#ifndef GI_X_PM
+#define GI_X_PM 1   // k_mode_x: pixel-major work blocks for launches of >= 64 units per pixel
+#endif
 #ifndef GI_X_TAILPROBE
 #define GI_X_TAILPROBE 0   // (measurement variant) k_mode_x's STATS launch records drain / wave life
 #endif
@@ -1380,7 +1383,12 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     }
     const unsigned runs = (unsigned)((wk.s1 - wk.s0 + k - 1) / k);    // units per pixel (run c: samples s0 + c k ...)
     const unsigned n_groups = (n_list + 63u) >> 6;
-    const unsigned n_blocks = n_groups * runs;
+    // xflags bit 5 (pixel-major blocks, launches of >= 64 units per pixel): a block is ONE pixel's
+    // 64 consecutive runs instead of 64 pixels' run c, so a wave's lanes start on the same pixel's
+    // samples -- nearly the same primary ray -- and walk the same nodes together
+    const bool pm = (xflags & 32) != 0 && runs >= 64u;
+    const unsigned rpb = (runs + 63u) >> 6;   // (pm) blocks per pixel
+    const unsigned n_blocks = pm ? n_list * rpb : n_groups * runs;
     // xflags bit 4 (spread): group g holds list entries g, g + G, g + 2G, ... (G groups) instead of
     // 64 consecutive ones, so a wave's 64 pixels come from all over the frame: the expensive pixels
     // of a frame cluster in space (the soup's core), and consecutive entries would give all of them
@@ -1930,14 +1938,20 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                         }
                         used_new = 64u;
                         if (nb < n_blocks) {
-                            const unsigned ng = nb / runs, nc = nb - ng * runs;
+                            // (pm: ng = the pixel's list index, nc = its block's first run)
+                            const unsigned ng = pm ? nb / rpb : nb / runs, nc = pm ? (nb - ng * rpb) * 64u : nb - ng * runs;
                             const unsigned long long m_act = __ballot(true);
                             const unsigned ra = (unsigned)__popcll(m_act & ((1ull << lane) - 1));
                             const unsigned na = (unsigned)__popcll(m_act);
                             __builtin_amdgcn_wave_barrier();
+                            const unsigned pm_ps = pm ? wk.list[ng] : 0u;
                             for (unsigned e = ra; e < 64u; e += na) {
-                                const unsigned li = spread ? e * n_groups + ng : ng * 64u + e;
-                                blk_list[e] = li < n_list ? wk.list[li] : 0xFFFFFFFFu;
+                                if (pm) {
+                                    blk_list[e] = nc + e < runs ? pm_ps : 0xFFFFFFFFu;
+                                } else {
+                                    const unsigned li = spread ? e * n_groups + ng : ng * 64u + e;
+                                    blk_list[e] = li < n_list ? wk.list[li] : 0xFFFFFFFFu;
+                                }
                             }
                             __builtin_amdgcn_wave_barrier();
                             used_new = n_need - avail;
@@ -1960,16 +1974,17 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     if (lane == leader) blk_meta[0] = used_new;
                     __builtin_amdgcn_wave_barrier();
                     if (phase == PH_NEED && have) {
-                        const unsigned i = spread ? j * n_groups + g : g * 64u + j;   // list index
+                        const unsigned i = pm ? g : spread ? j * n_groups + g : g * 64u + j;   // list index
+                        const unsigned cu = pm ? c + j : c;        // the unit's run
                         if (ps != 0xFFFFFFFFu) {                   // else a padding unit: take another
                             slot_pixel(m, (long long)(ps >> 6), (int)(ps & 63), idx, x, y);
                             y += m.y0;
                             if (spp > 1) idx = (long long)i;        // per-sample radiance row
                             key = mx_key(seed, (uint64_t)y * (uint64_t)m.w + (uint64_t)x);
                             if (PSL) reinterpret_cast<uint64_t*>(pslot)[9] = key;
-                            smp = wk.s0 + (int)c * k;
+                            smp = wk.s0 + (int)cu * k;
                             phase = PH_START;
-                            if (c == 0) ++npx;
+                            if (cu == 0) ++npx;
                         }
                     }
                 }
@@ -2343,6 +2358,7 @@ long long shard_tiles(int w, int h, int shard_count) { return make_map(w, h, sha
 // work-unit run length (scenes of cheap background samples such as the main.cpp scene prefer 8).
 struct XEnv {
     int lds = 1, h8 = 0, xf = -1, run_log2 = 0, help = 1, spread = -1, wf = -1;
+    int pm = GI_X_PM;                 // pixel-major work blocks (GI_X_PM)
     int r_flat = -1;                  // Mode R kernels (GI_R_FLAT): 1 the flat phases for every scene, 0 k_mode_r
                                       // for every scene, 2 k_mode_r_batch for the whole frame (tests); -1 by size
     long long wf_chunk = 8ll << 20;   // wavefront Mode X: units (pixel samples) per chunk = queue capacity
@@ -2357,6 +2373,7 @@ const XEnv& x_env() {
         if (const char* v = std::getenv("GI_X_FLAGS")) env.xf = std::atoi(v);
         if (const char* v = std::getenv("GI_X_HELP")) env.help = std::atoi(v) != 0;
         if (const char* v = std::getenv("GI_X_SPREAD")) env.spread = std::atoi(v);
+        if (const char* v = std::getenv("GI_X_PM")) env.pm = std::atoi(v) != 0;
         if (const char* v = std::getenv("GI_R_FLAT")) env.r_flat = std::atoi(v);
         if (const char* v = std::getenv("GI_RF_PER_SLOT")) env.rf_per_slot = std::max(0, std::min(1024, std::atoi(v)));
         if (const char* v = std::getenv("GI_X_WF")) env.wf = std::atoi(v);
@@ -2556,7 +2573,7 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
         // length (log2, bits 8-10)
         const int xf = (env.xf >= 0 ? env.xf : sc.x_flags) | (env.run_log2 << 8) |
                        ((o.flags & GI_FLAG_X_NO_SHADOW) ? 4 : 0) | (env.help ? 8 : 0) |
-                       ((env.spread > 0 || (env.spread < 0 && help)) ? 16 : 0);
+                       ((env.spread > 0 || (env.spread < 0 && help)) ? 16 : 0) | (env.pm ? 32 : 0);
         if (form) {   // gi_wf.hip's forms, timed as one pass
             if (!xs.wcnt || (form == 1 && (!xs.wq[0] || !xs.wq[1] || !xs.h_nlist || xs.wcap <= 0))) return hipErrorInvalidValue;
             e = launch_wf(sc, xc.kv, xc.wf_lds_bytes, form == 2 ? xc.seg_resident : xc.wf_resident, form, cam, light, w, h, y0,
