@@ -89,7 +89,10 @@ def pmc_summary(workload: str, kernel: str = ""):
             continue
         if kernel and kernel + "<" not in d.get("kernel", ""):   # (the flat Mode R summary names all its kernels)
             continue
-        rnd = os.path.basename(p)[1:3]
+        base = os.path.basename(p)
+        # latest round first; within a round the plain rNN_ summary (the round's final evidence)
+        # before tagged ones (rNNa_, rNNmega_, ...: mid-round or forced-form A/B profiles)
+        rnd = (base[1:3], base[3:base.index("_")] == "")
         if best is None or rnd > best[0]:
             best = (rnd, os.path.relpath(p, ROOT), d)
     return best[1:] if best else None
