@@ -1428,7 +1428,10 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     constexpr bool MERGE = GI_X_MERGE != 0 && PAIR && PSL && !NST;
     // UL (quantised-node HBM scenes): one load round trip per step for the node-test and leaf-test
     // lanes together
-    constexpr bool UL = GI_X_UNILOAD != 0 && !PAIR &&
+    // (round 5: in the build without the shadow handoff -- long launches, C5 -- the merged round
+    // trip costs more than it saves: C5 178.3 -> 176.8 ms without it, C4 +2% without it, so it stays
+    // in the handoff build only)
+    constexpr bool UL = GI_X_UNILOAD != 0 && !PAIR && HELP &&
                         std::is_same<std::remove_cv_t<std::remove_pointer_t<NodeP>>, XCNode>::value;
     bool desc = false, rs = false;   // MERGE: this step descends into xch / restarts at the root
     int xch = 0;
