@@ -567,7 +567,9 @@ bool build_host_scene(const gi_scene_desc& desc, HostScene& hs, std::string& err
     }
     hs.xnodes.clear();
     hs.xprim_idx.clear();
-    const char* accel = std::getenv("GI_XACCEL");   // tuning knob: "octree" = the earlier SAT octree
+    // GI_XACCEL=octree (a test hook: the frame does not depend on the acceleration structure) builds
+    // the round-1 SAT octree instead of the SAH BVH; GI_XLEAF_MAX (test hook) caps leaf sizes
+    const char* accel = std::getenv("GI_XACCEL");
     if (!(accel && std::string(accel) == "octree")) {
         std::vector<double> bounds(6 * pb.size());
         for (size_t i = 0; i < pb.size(); ++i)
@@ -593,7 +595,7 @@ bool build_host_scene(const gi_scene_desc& desc, HostScene& hs, std::string& err
     xb.out = &hs.xnodes;
     xb.idx = &hs.xprim_idx;
     xb.pad = 1e-9 * ext;
-    if (const char* lm = std::getenv("GI_XLEAF_MAX")) xb.leaf_max = std::max(1, std::atoi(lm));   // tuning knob
+    if (const char* lm = std::getenv("GI_XLEAF_MAX")) xb.leaf_max = std::max(1, std::atoi(lm));
     std::vector<int32_t> all(pb.size());
     for (size_t i = 0; i < pb.size(); ++i) all[i] = (int32_t)i;
     if (pb.empty()) {

@@ -64,7 +64,6 @@ struct Builder {
     double kTraverse = 0.35;
     // > 0: every binary node at this depth is a leaf (GI_XFLAT, tuning knob for tiny scenes: depth 3
     // gives at most 8 leaves, i.e. one wide root whose children are all leaves)
-    int flat_depth = 0;
 
     int build(int first, int count, int depth) {
         const int ni = (int)nodes.size();
@@ -80,7 +79,7 @@ struct Builder {
         nodes[ni].box = box;
         nodes[ni].first = first;
         nodes[ni].count = count;
-        if (count <= 1 || depth > 60 || (flat_depth > 0 && depth >= flat_depth)) return ni;
+        if (count <= 1 || depth > 60) return ni;
         // binned SAH over the centroid bounds
         int best_axis = -1, best_split = -1;
         double best_cost = INFINITY;
@@ -411,10 +410,6 @@ void build_xbvh(const std::vector<XPrim>& prims, const std::vector<double>& boun
     Builder b;
     b.pb = &pb;
     b.leaf_max = std::max(1, leaf_max);
-    if (const char* ct = std::getenv("GI_XSAH_CT")) b.kTraverse = std::atof(ct);   // tuning knobs
-    if (const char* nb = std::getenv("GI_XSAH_BINS")) b.kBins = std::max(2, std::min(Builder::kMaxBins, std::atoi(nb)));
-    if (const char* fl = std::getenv("GI_XFLAT"))
-        if (np <= 64) b.flat_depth = std::max(0, std::min(6, std::atoi(fl)));
     b.order.resize(np);
     b.cen.resize(3 * np);
     for (size_t i = 0; i < np; ++i) {
@@ -425,9 +420,9 @@ void build_xbvh(const std::vector<XPrim>& prims, const std::vector<double>& boun
     int root;
     // The spatial-split build for scenes of more than kSpatialMin primitives (the HBM-resident
     // ones; the 100k soup: C5 -1.5%, C4 -1%, +9% leaf records, +0.9 s of build,
-    // profiles/r03_sbvh.txt); GI_XSBVH=0/1 forces it off / on (tuning knobs: the references' budget
-    // GI_XSBVH_BUDGET, default 1.5 x primitives, the overlap threshold GI_XSBVH_ALPHA, 1e-5 of the
-    // scene's area, and the deepest level tried GI_XSBVH_DEPTH, 10)
+    // profiles/r03_sbvh.txt): a references' budget of 1.5 x the primitives, splits tried where the
+    // object split's children overlap by more than 1e-5 of the scene's area, down to level 10.
+    // GI_XSBVH=0/1 forces it off / on (a test hook: the frame does not depend on it)
     constexpr size_t kSpatialMin = 8192;
     const char* sbv = std::getenv("GI_XSBVH");
     hs.x_spatial = geometric && (sbv ? std::atoi(sbv) != 0 : np > kSpatialMin);
@@ -437,14 +432,11 @@ void build_xbvh(const std::vector<XPrim>& prims, const std::vector<double>& boun
         sb.leaf_max = b.leaf_max;
         sb.kBins = b.kBins;
         sb.kTraverse = b.kTraverse;
-        const char* bud = std::getenv("GI_XSBVH_BUDGET");
-        const char* al = std::getenv("GI_XSBVH_ALPHA");
-        sb.ref_budget = (size_t)((bud ? std::atof(bud) : 1.5) * (double)np);
+        sb.ref_budget = (size_t)(1.5 * (double)np);
         std::vector<SRef> refs(np);
         for (size_t i = 0; i < np; ++i) refs[i] = SRef{(int32_t)i, pb[i]};
-        sb.alpha_area = (al ? std::atof(al) : 1e-5) * scene.area();
+        sb.alpha_area = 1e-5 * scene.area();
         sb.n_refs = np;
-        if (const char* sd = std::getenv("GI_XSBVH_DEPTH")) sb.max_split_depth = std::atoi(sd);
         root = sb.build(refs, 0);
         b.nodes = std::move(sb.nodes);
         b.order = std::move(sb.order);
@@ -484,10 +476,8 @@ void build_xbvh(const std::vector<XPrim>& prims, const std::vector<double>& boun
         gather(bn.right, out);
     };
 
-    // child-to-slot assignment of minimum total cost (C3 kernel -1%, the soups unchanged,
-    // profiles/r02_s4_sah.txt); GI_XSLOT=0 (tuning knob) restores the greedy assignment
-    const char* xs = std::getenv("GI_XSLOT");
-    const bool exact_slots = !(xs && std::atoi(xs) == 0);
+    // child-to-slot assignment of minimum total cost (C3 kernel -1% against the greedy one, the
+    // soups unchanged, profiles/r02_s4_sah.txt)
     // fill wide node `wi` (depth `wd`) from binary node `bn`'s subtree
     std::function<void(int, int, int)> fill = [&](int wi, int bn, int wd) {
         hs.x_max_depth = std::max(hs.x_max_depth, wd);
@@ -524,8 +514,7 @@ void build_xbvh(const std::vector<XPrim>& prims, const std::vector<double>& boun
                 cost[i][s] = c;
             }
         int slot_of[8];
-        bool used_kid[8] = {false}, used_slot[8] = {false};
-        if (exact_slots) {   // minimum-cost assignment: DP over the set of slots taken by kids 0..i-1
+        {   // minimum-cost assignment: DP over the set of slots taken by kids 0..i-1
             double dp[256];
             int8_t pick[9][256];
             for (int m = 0; m < 256; ++m) dp[m] = INFINITY;
@@ -550,17 +539,6 @@ void build_xbvh(const std::vector<XPrim>& prims, const std::vector<double>& boun
                 slot_of[i] = pick[i][bm];
                 bm &= ~(1 << slot_of[i]);
             }
-        }
-        for (int it = 0; it < nk && !exact_slots; ++it) {
-            int bi = -1, bs = -1;
-            double bc = INFINITY;
-            for (int i = 0; i < nk; ++i) {
-                if (used_kid[i]) continue;
-                for (int s = 0; s < 8; ++s)
-                    if (!used_slot[s] && cost[i][s] < bc) { bc = cost[i][s]; bi = i; bs = s; }
-            }
-            used_kid[bi] = used_slot[bs] = true;
-            slot_of[bi] = bs;
         }
         for (int i = 0; i < nk; ++i) {
             const int s = slot_of[i];

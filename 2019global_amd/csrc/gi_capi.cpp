@@ -142,8 +142,9 @@ int ensure_xscratch(gi_scene* s, int w, int h, const gi_opts* o) {
         // 1080p frame takes 0.28 GB (R-C4 writes 5.0 M pairs: 20 MB).  A tile whose candidates do not
         // fit is rendered by k_mode_r_batch; if the buffers cannot be had at all, the whole frame is.
         XScratch& x = s->xs;
-        if (r_kernel_choice(s->dev, *o) == 1 && x.rf_slots < need) {
+        if (r_kernel_choice(s->dev, *o) == 1 && x.rf_slots < need && !(x.rf_failed > 0 && need >= x.rf_failed)) {
             free_rflat(x);
+            const hipError_t prior = hipPeekAtLastError();   // (a caller's unchecked error is left as it was)
             const long long tiles = need / 64;
             const long long pages = (long long)x_env_rf_per_slot() * need / (long long)rf_page_pairs();
             const size_t pairs = (size_t)tiles * rf_own_pairs() + (size_t)pages * rf_page_pairs();
@@ -162,11 +163,13 @@ int ensure_xscratch(gi_scene* s, int w, int h, const gi_opts* o) {
                 hipMalloc((void**)&x.rf_shc, (size_t)segs * sizeof(unsigned)) == hipSuccess &&
                 hipMalloc((void**)&x.rf_sreg, (size_t)segs * sizeof(unsigned)) == hipSuccess &&
                 hipMalloc((void**)&x.rf_hoff, (size_t)(segs + 1) * sizeof(unsigned)) == hipSuccess;
-            if (!ok) {
-                (void)hipGetLastError();   // (clears the sticky allocation error) -- rendered by k_mode_r_batch
+            if (!ok) {   // rendered by k_mode_r_batch (gi_scene_r_kernel reports 2); not retried per frame
+                if (prior == hipSuccess) (void)hipGetLastError();   // (clears this allocation's error only)
                 free_rflat(x);
+                x.rf_failed = need;
                 return GI_OK;
             }
+            x.rf_failed = 0;
             x.rf_pages = (unsigned)pages;
             x.rf_slots = need;
             x.rf_bytes = pairs * sizeof(unsigned) + (size_t)tiles * (rf_max_pages() + 4) * sizeof(unsigned) + segs * 12 +
@@ -200,8 +203,6 @@ int ensure_xscratch(gi_scene* s, int w, int h, const gi_opts* o) {
         const long long want = std::max(64ll, std::min(x_wf_chunk(), need * (long long)o->spp));
         if (!x.wcnt) {
             if ((e = hipMalloc((void**)&x.wcnt, 2 * 64 * sizeof(unsigned))) != hipSuccess) return hip_fail(e, "hipMalloc (wavefront counters)");
-            if ((e = hipHostMalloc((void**)&x.h_nlist, sizeof(unsigned), hipHostMallocDefault)) != hipSuccess)
-                return hip_fail(e, "hipHostMalloc (wavefront)");
         }
         if (form == 1 && x.wcap < want) {
             for (int q = 0; q < 2; ++q) {
@@ -332,7 +333,6 @@ void destroy_scene(gi_scene* s) noexcept {
     }
     (void)hipFree(s->xs.wcnt);
     free_rflat(s->xs);
-    (void)hipHostFree(s->xs.h_nlist);
     for (int i = 0; i < KTimer::kRing; i++) {
         if (s->kt.ev0[i]) (void)hipEventDestroy(static_cast<hipEvent_t>(s->kt.ev0[i]));
         if (s->kt.ev1[i]) (void)hipEventDestroy(static_cast<hipEvent_t>(s->kt.ev1[i]));
@@ -439,6 +439,14 @@ int prog_check(gi_scene* s, const gi_camera& c, const double light[3], int w, in
         return GI_OK;
     }
     const uint64_t key = prog_key(c, light, w, h, o);
+    if (o.sample_begin > 0 && s->prog_next == o.sample_begin && s->launched) {
+        // the previous pass was accepted when issued: a device error since ends the frame
+        const hipError_t e = hipEventQuery(s->last);
+        if (e != hipSuccess && e != hipErrorNotReady) {
+            s->prog_next = -1;
+            return hip_fail(e, "progressive pass: the previous pass failed on the device; restart the frame at sample 0");
+        }
+    }
     if (o.sample_begin > 0 && (s->prog_next != o.sample_begin || s->prog_key != key)) {
         s->prog_next = -1;
         return fail(GI_ERR_ARG, "progressive pass out of order: a pass continues the previous pass's frame "
@@ -518,10 +526,8 @@ int scene_create_on(const gi_scene_desc* desc, int device, gi_scene** out) {
     }
     // HBM-resident scenes whose XWNode tree outgrows an XCD's L2 share (> 2 MB) traverse quantised
     // nodes (XCNode: one 128-byte line per node instead of two): C5 287 -> 270 ms; the 1k soup, whose
-    // 84 KB tree stays in L2 anyway, pays the decoding (+6%) and keeps XWNode.  GI_X_CNODE=0 / 1
-    // forces either (A/B).
-    const char* cn = std::getenv("GI_X_CNODE");
-    const bool want_cn = cn ? std::atoi(cn) != 0 : h.xwnodes.size() * sizeof(XWNode) > (size_t)2 << 20;
+    // 84 KB tree stays in L2 anyway, pays the decoding (+6%) and keeps XWNode.
+    const bool want_cn = h.xwnodes.size() * sizeof(XWNode) > (size_t)2 << 20;
     if (d.x_lds_bytes == 0 && want_cn && encode_xcnodes(h.xwnodes, s->host.xcnodes) &&
         (e = upload(sp, h.xcnodes, &d.xcnodes)) != hipSuccess)
         return hip_fail(e, "scene upload (quantised nodes)");
@@ -759,6 +765,7 @@ int gi_scene_r_kernel(gi_scene* s, const gi_opts* o, int32_t* kernel) {
         if (!s || !o || !kernel) return fail(GI_ERR_ARG, "null argument");
         std::lock_guard<std::mutex> lk(s->mu);
         *kernel = r_kernel_choice(s->dev, *o);
+        if (*kernel == 1 && s->xs.rf_failed > 0 && s->xs.rf_slots == 0) *kernel = 2;   // (its buffers failed)
         return GI_OK;
     });
 }

@@ -156,10 +156,13 @@ __device__ __forceinline__ double x_prim_t(const XHot& p, V3 o, V3 d, double tmi
         const double vn = fdot(d, qv);
         const double uvn = un + vn;
         const bool pos = det > 0.0;
-        const bool miss = det == 0.0 || (pos ? (un < 0.0 || un > det || vn < 0.0 || uvn > det)
-                                             : (un > 0.0 || un < det || vn > 0.0 || uvn < det));
+        // the comparisons combined with | and & (no short circuit: || compiled to nested exec-mask
+        // branches, ~35 scalar instructions and their VALU -> SALU latencies per test) -- the same
+        // boolean for every input, NaN included
+        const bool miss = (det == 0.0) | (pos & ((un < 0.0) | (un > det) | (vn < 0.0) | (uvn > det))) |
+                          (!pos & ((un > 0.0) | (un < det) | (vn > 0.0) | (uvn < det)));
         const double t = fdot(e2, qv) / det;   // branch-free: two tests interleave in the leaf loop
-        return (!miss && t > tmin) ? t : INFINITY;
+        return (!miss & (t > tmin)) ? t : INFINITY;
     }
     const V3 oc = o - ld3(p.a);
     const double b = fdot(oc, d);

@@ -315,7 +315,8 @@ __device__ __forceinline__ uint32_t children_mask_line_coop(const XWNode* nd, F3
 #endif
 struct RMemo {
     int* e;        // GI_R_MEMO entries of this ray, or nullptr
-    int tag = 0;   // k_rf_reach: (tile & 255) << 1 -- a row serves the same pixel slot of several tiles
+    int tag = 0;   // k_rf_reach: (the lane's run of equal tiles in its chunk) << 1 -- a row serves the same
+                   // pixel slot of the chunk's tiles, and the memo is cleared at every chunk
 };
 __device__ __forceinline__ int r_memo_slot(int node) { return (int)(((unsigned)node * 2654435761u) >> 26) & (GI_R_MEMO - 1); }
 
@@ -693,9 +694,6 @@ __global__ __launch_bounds__(256) void k_mode_r_batch(DevScene sc, CamDev cam, V
 #define GI_RF_S0 512u     // pairs of a tile's own region (8 per pixel slot)
 #define GI_RF_PAGE 512u   // pairs per pool page
 #define GI_RF_KMAX 64u    // pool pages a tile may take (so at most 33,280 pairs per tile)
-#ifndef GI_RF_PROBE
-#define GI_RF_PROBE 0   // (measurement variant) k_rf_reach's STATS launch records its chunks' work and time
-#endif
 constexpr unsigned kRfOvf = 0xFFFFFFFFu;
 constexpr unsigned kRfEntMask = (1u << 26) - 1u;   // scenes of more entities run k_mode_r_batch
 struct RFlat {
@@ -1078,50 +1076,53 @@ __global__ __launch_bounds__(1024) void k_rf_scan(const unsigned* in, unsigned* 
 // Persistent waves take chunks of 64 consecutive hits of the whole frame in turn (hoff numbers them
 // across the segments, so chunks are full; a chunk's first segment by a binary search, each lane's
 // from there), so the hits of a soup-core tile are shared by many waves.  One wave per workgroup:
-// its LDS holds a node-test memo (RMemo, GI_R_MEMO entries) per pixel slot of a tile, each entry
-// tagged with the tile (low 8 bits: a chunk spans fewer tiles), so lanes of different tiles never
-// read each other's results and the memo is never reset.
+// its LDS holds a node-test memo (RMemo, GI_R_MEMO entries) per pixel slot of a tile, cleared at
+// every chunk and each entry tagged with its lane's run of equal tiles in the chunk, so lanes of
+// different tiles never read each other's results.
 template <bool STATS>
 __global__ __launch_bounds__(64) void k_rf_reach(DevScene sc, CamDev cam, TileMap m, RFlat f, unsigned long long* stats) {
-    __shared__ int s_memo[GI_R_MEMO > 0 ? 64 * GI_R_MEMO : 1];
+    __shared__ __attribute__((aligned(16))) int s_memo[GI_R_MEMO > 0 ? 64 * GI_R_MEMO : 4];
     const int lane = threadIdx.x & 63;
     const long long n_regions = m.n_local;
     const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_w = ((long long)gridDim.x * blockDim.x) >> 6;
     const long long n_seg = f.soff[n_regions], n_hits = f.hoff[n_seg];
     const bool use_memo = GI_R_MEMO > 0 && sc.n_rnodes < (1 << 22);
-    if (use_memo)
-        for (int k = 0; k < GI_R_MEMO; ++k) s_memo[lane * GI_R_MEMO + k] = -1;   // (matches no key)
-    __builtin_amdgcn_wave_barrier();
     uint32_t nnode = 0;
-#if GI_RF_PROBE   // (measurement build; STATS launches, Mode X's slots 5-12): the chunks' work and time
-    const uint64_t pt0 = (uint64_t)wall_clock64();
-    uint32_t p_app = 0, p_nn0 = 0, p_ch = 0;
-#endif
     // (chunks from a device counter instead, as waves free up: R-C4 0.80 -> 0.88 ms)
     for (long long c = gw; 64 * c < n_hits; c += n_w) {
-#if GI_RF_PROBE
-        ++p_ch;
-#endif
         const long long i = 64 * c + lane;
         long long sg = rf_find(f.hoff, n_seg, 64 * c);   // the chunk's first segment (uniform)
+        long long r = -1;
         if (i < n_hits) {
             while (sg + 1 < n_seg && (long long)f.hoff[sg + 1] <= i) ++sg;   // this lane's
-            const long long r = f.sreg[sg];
+            r = f.sreg[sg];
+        }
+        // the memo is the chunk's: cleared here (each lane its row), its entries tagged with the
+        // lane's run of equal tiles in the chunk (<= 64 runs, so the tag fits its 8 bits).  Two lanes
+        // share a tag only if they hold the same tile, hence with the same row the same pixel: no
+        // entry is ever read for another ray (a tag of the tile's low bits alone let tiles r and
+        // r + 256 of one chunk, or of the wave's earlier chunks, read each other's results)
+        const long long r_prev = __shfl(r, lane > 0 ? lane - 1 : 0);
+        const unsigned long long runs = __ballot(r >= 0 && (lane == 0 || r != r_prev));
+        const int run_ord = __popcll(runs & ((2ull << lane) - 1)) - 1;
+        if (use_memo) {
+            int4* row = reinterpret_cast<int4*>(s_memo + lane * GI_R_MEMO);
+            for (int k = 0; k < GI_R_MEMO / 4; ++k) row[k] = make_int4(-1, -1, -1, -1);   // (matches no key)
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (r >= 0) {
             const unsigned p = (unsigned)(sg - (long long)f.soff[r]) * GI_RF_SEG + (unsigned)(i - (long long)f.hoff[sg]);
             const unsigned pg = p < GI_RF_S0 ? 0u : f.pt[(size_t)r * GI_RF_KMAX + rf_page(p)];
             const unsigned pr = *rf_pair(f, r, p, pg);
             const unsigned slot = (unsigned)r * 64u + (pr >> 26);
             const int e = (int)(pr & kRfEntMask);
-            const RMemo memo{use_memo ? s_memo + (pr >> 26) * GI_R_MEMO : nullptr, (int)((r & 255) << 1)};
+            const RMemo memo{use_memo ? s_memo + (pr >> 26) * GI_R_MEMO : nullptr, run_ord << 1};
             const V3 d = rf_dir(f, slot);
             const int a1 = sc.app_off[e + 1];
             for (int a = sc.app_off[e]; a < a1; ++a) {
                 const RApp ap = sc.app_rec[a];
                 const long long rk = ap.rank;
                 if (rk <= (long long)*(volatile unsigned long long*)(f.best + slot) - 1) break;
-#if GI_RF_PROBE
-                ++p_app;
-#endif
                 if (r_path_reachable(sc, ap.p0, ap.p1, cam.pos, d, nnode, memo)) {
                     atomicMax(f.best + slot, (unsigned long long)(rk + 1));
                     break;
@@ -1129,29 +1130,6 @@ __global__ __launch_bounds__(64) void k_rf_reach(DevScene sc, CamDev cam, TileMa
             }
         }
     }
-#if GI_RF_PROBE
-    if (STATS && p_ch) {
-        const uint64_t dt = (uint64_t)wall_clock64() - pt0;
-        uint32_t mapp = p_app, mnn = nnode, sapp = p_app, snn = nnode;
-        for (int off = 32; off > 0; off >>= 1) {
-            mapp = max(mapp, (uint32_t)__shfl_xor(mapp, off));
-            mnn = max(mnn, (uint32_t)__shfl_xor(mnn, off));
-            sapp += __shfl_xor(sapp, off);
-            snn += __shfl_xor(snn, off);
-        }
-        if (lane == 0) {
-            atomicMax(stats + 5, (unsigned long long)dt);        // the slowest wave (wall ticks)
-            atomicAdd(stats + 6, (unsigned long long)dt);
-            atomicAdd(stats + 7, 1ull);                          // waves with work
-            atomicMax(stats + 8, (unsigned long long)mapp);      // most appearances one lane walked
-            atomicMax(stats + 9, (unsigned long long)mnn);       // most node tests one lane ran
-            atomicMax(stats + 10, (unsigned long long)snn);      // most node tests one wave ran
-            atomicAdd(stats + 11, (unsigned long long)sapp);     // appearances walked
-            atomicAdd(stats + 12, (unsigned long long)p_ch);     // chunks
-            atomicMax(stats + 13, ((unsigned long long)dt << 32) | min(snn, 0xFFFFFFFFu));   // the slowest wave's node tests
-        }
-    }
-#endif
     if (STATS) wave_add_stats(stats, 0, nnode, 0, 0);
 }
 // per pixel: the best rank's entity, shaded (overflowed tiles: left to k_mode_r_batch)
@@ -1236,51 +1214,6 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 #ifndef GI_X_START_BURST
 #define GI_X_START_BURST 16   // primary rays a lane may resolve by the root test per handler run
 #endif
-#ifndef GI_X_PSL
-#define GI_X_PSL 1   // 4-wave LDS kernel: path values carried across the shadow ray kept in LDS
-#endif
-#ifndef GI_X_PAIR
-#define GI_X_PAIR 1   // LDS-resident scenes: leaf records tested two at a time (interleaved fp64 chains)
-#endif
-#ifndef GI_X_HELP
-#define GI_X_HELP 1   // HBM-resident scenes: shadow rays handed to idle lanes of the wave (XHelp)
-#endif
-#ifndef GI_X_TRI
-#define GI_X_TRI 1   // 4-wave LDS kernel: triangle-only primitive tests and texture mapping (TRI)
-#endif
-#ifndef GI_X_PM
-#define GI_X_PM 1   // k_mode_x: pixel-major work blocks for launches of >= 64 units per pixel
-#endif
-#ifndef GI_X_TAILPROBE
-#define GI_X_TAILPROBE 0   // (measurement variant) k_mode_x's STATS launch records drain / wave life
-#endif
-#ifndef GI_X_TAILPROBE_T1
-#define GI_X_TAILPROBE_T1 8
-#endif
-#ifndef GI_X_TAILPROBE_T2
-#define GI_X_TAILPROBE_T2 16
-#endif
-#ifndef GI_X_PREFETCH
-// HBM-resident scenes: fetch the next pop's child reference a step ahead (PF): C4 1.94 -> 1.75-1.78 ms,
-// C5 199.7 -> 198.5 ms
-#define GI_X_PREFETCH 1
-#endif
-#ifndef GI_X_MERGE
-// 4-wave LDS kernel: a step's interior-node test and a restarted ray's root test in one block
-// (C3 6.08 -> 5.81 ms; the 3-wave LDS kernel of the every-entity scene is 2-4% slower with it)
-#define GI_X_MERGE 1
-#endif
-#ifndef GI_X_UNILOAD
-// UL (mode_x_wave, quantised-node HBM scenes): a step's node-test and leaf-test lanes share one load
-// round trip -- C5 196.5 -> 182.5 ms (without leaf postponement), C4 ~-1% (noise band)
-#define GI_X_UNILOAD 1
-#endif
-#ifndef GI_X_CLIMB_CLZ
-#define GI_X_CLIMB_CLZ 1   // NST climb: the target level by a leading-zero count (C5 -2%), not a loop
-#endif
-#ifndef GI_X_NSTK
-#define GI_X_NSTK 1   // HBM-resident scenes: the node index of every traversal level kept in LDS
-#endif
 #ifndef GI_X_MIN_WAVES
 #define GI_X_MIN_WAVES 3       // minimum waves per SIMD, HBM-resident scenes (<= 168 VGPRs)
 #endif
@@ -1299,11 +1232,6 @@ struct XCounters {
     // divergence profile (wave-level, lane 0): loop iterations in which some lane ran a node test /
     // a leaf test / an inline bounce restart / a handler start-loop pass, and the lanes that did
     uint64_t it_node = 0, ln_node = 0, it_leaf = 0, ln_leaf = 0, it_rs = 0, ln_rs = 0, it_st = 0, ln_st = 0;
-#if GI_X_TAILPROBE
-    uint64_t w_start = 0, w_exh = 0;   // (probe) wave start, first sight of the exhausted block counter
-    uint64_t w_t1 = 0, w_t2 = 0;       // (probe) first iteration after it with <= T1 / T2 live lanes
-    uint64_t p_it = 0, p_lo = 0;       // (probe) iterations after it; of those with <= T1 paths
-#endif
 };
 
 // Mode X work list (k_x_classify -> k_mode_x -> k_x_reduce).  A pixel whose every jittered primary
@@ -1425,13 +1353,13 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     bool raying = false;
     // MERGE (LDS kernel): the step's interior-node test and a restarted ray's root test share one
     // children_mask call at the end of the step
-    constexpr bool MERGE = GI_X_MERGE != 0 && PAIR && PSL && !NST;
+    constexpr bool MERGE = PAIR && PSL && !NST;
     // UL (quantised-node HBM scenes): one load round trip per step for the node-test and leaf-test
     // lanes together
     // (round 5: in the build without the shadow handoff -- long launches, C5 -- the merged round
     // trip costs more than it saves: C5 178.3 -> 176.8 ms without it, C4 +2% without it, so it stays
     // in the handoff build only)
-    constexpr bool UL = GI_X_UNILOAD != 0 && !PAIR && HELP &&
+    constexpr bool UL = !PAIR && HELP &&
                         std::is_same<std::remove_cv_t<std::remove_pointer_t<NodeP>>, XCNode>::value;
     bool desc = false, rs = false;   // MERGE: this step descends into xch / restarts at the root
     int xch = 0;
@@ -1461,10 +1389,11 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
             const int pi = rec.h.prim;
             if (phase != PH_CLOSEST) {
                 if (t < tmax) { best = pi; raying = false; return; }   // any hit occludes
-            } else if (t < tbest || (t == tbest && pi < best)) {
-                tbest = t;
-                best = pi;
-                tbest_f = up32(t);
+            } else {   // (selects, not branches: | and & do not short-circuit)
+                const bool u = (t < tbest) | ((t == tbest) & (pi < best));
+                tbest = u ? t : tbest;
+                best = u ? pi : best;
+                tbest_f = u ? up32(t) : tbest_f;
             }
         }
     };
@@ -1479,20 +1408,18 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 const double tb = two ? x_prim_t<TRI>(r1.h, o, d, MX_TMIN) : INFINITY;
                 nprim += two ? 2 : 1;
                 if (phase != PH_CLOSEST) {
-                    if (ta < tmax || tb < tmax) {   // any hit occludes
+                    if ((ta < tmax) | (tb < tmax)) {   // any hit occludes
                         best = ta < tmax ? r0.h.prim : r1.h.prim;
                         raying = false;
                         return;
                     }
-                } else {
-                    if (ta < tbest || (ta == tbest && r0.h.prim < best)) {
-                        tbest = ta;
-                        best = r0.h.prim;
-                    }
-                    if (tb < tbest || (tb == tbest && r1.h.prim < best)) {
-                        tbest = tb;
-                        best = r1.h.prim;
-                    }
+                } else {   // (selects, not branches)
+                    const bool ua = (ta < tbest) | ((ta == tbest) & (r0.h.prim < best));
+                    tbest = ua ? ta : tbest;
+                    best = ua ? r0.h.prim : best;
+                    const bool ub = (tb < tbest) | ((tb == tbest) & (r1.h.prim < best));
+                    tbest = ub ? tb : tbest;
+                    best = ub ? r1.h.prim : best;
                     tbest_f = up32(tbest);
                 }
             }
@@ -1504,7 +1431,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     // end of the step that sets up the level (descend, climb or ray start), so the pop itself waits
     // for no load: one dependent round trip per step (the child's node or leaf records) instead of
     // two.  (lvl mask, node) do not change between that fetch and the pop.
-    constexpr bool PF = !PAIR && GI_X_PREFETCH != 0;   // (LDS-resident scenes: a ds_read away; +3% with PF)
+    constexpr bool PF = !PAIR;   // (LDS-resident scenes: a ds_read away; +3% with PF)
     int pf_ch = 0, pf_cnt = 0;
     auto prefetch = [&]() {
         const uint32_t m = lvl_get<SH>(mlo, mhi, level);
@@ -1516,9 +1443,6 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
     };
 
     const uint64_t t_begin = STATS ? clock64() : 0;
-#if GI_X_TAILPROBE
-    if (STATS) cnt.w_start = (uint64_t)wall_clock64();
-#endif
     for (;;) {
         if (HELP && any_gave && phase == PH_DEAD) {   // an idle lane given a shadow ray starts it
             const int ow = hp_.own[tid];
@@ -1548,15 +1472,6 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
         }
         const unsigned long long m_live = __ballot(phase != PH_DEAD);
         if (m_live == 0) break;
-#if GI_X_TAILPROBE
-        if (STATS) {
-            const bool ex = __ballot(cnt.w_exh != 0) != 0;
-            const int own = __popcll(__ballot(phase != PH_DEAD && phase != PH_HELP));   // paths, not helpers
-            if (ex && cnt.w_t1 == 0 && own <= GI_X_TAILPROBE_T1) cnt.w_t1 = (uint64_t)wall_clock64();
-            if (ex && cnt.w_t2 == 0 && own <= GI_X_TAILPROBE_T2) cnt.w_t2 = (uint64_t)wall_clock64();
-            if (ex) { ++cnt.p_it; if (own <= GI_X_TAILPROBE_T1) ++cnt.p_lo; }
-        }
-#endif
         const unsigned long long m_idle = HELP ? ~m_live : 0ull;   // lanes free to take a shadow ray
         bool gave = false;
         const bool trav = raying;
@@ -1661,18 +1576,11 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                 uint32_t rest = lvl_get<SH>(mlo, mhi, level);
                 if constexpr (NST) {
                     if (rest == 0 && level > 0) {
-#if GI_X_CLIMB_CLZ
                         // the deepest level below with children left, by one leading-zero count
                         const uint64_t lm = level >= 8 ? mlo : mlo & ((1ull << (8 * level)) - 1);
                         const uint64_t hm = level <= 8 ? 0ull : mhi & ((1ull << (8 * (level - 8))) - 1);
                         level = hm ? 8 + (63 - __clzll((long long)hm)) / 8 : lm ? (63 - __clzll((long long)lm)) / 8 : 0;
                         rest = lvl_get<SH>(mlo, mhi, level);
-#else
-                        do {
-                            --level;
-                            rest = lvl_get<SH>(mlo, mhi, level);
-                        } while (rest == 0 && level > 0);
-#endif
                         node = level == 0 ? 0 : nst[level * 256];
                     }
                 } else {
@@ -1970,9 +1878,6 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                             phase = PH_DEAD;                        // no work left
                         }
                         if (nb >= n_blocks && lane == leader) blk_meta[3] = 1u;   // the frame's work is all handed out
-#if GI_X_TAILPROBE
-                        if (STATS && nb >= n_blocks && cnt.w_exh == 0) cnt.w_exh = (uint64_t)wall_clock64();
-#endif
                     }
                     if (lane == leader) blk_meta[0] = used_new;
                     __builtin_amdgcn_wave_barrier();
@@ -2089,7 +1994,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
 // W4: 4 waves per SIMD (<= 128 VGPRs) for LDS-resident scenes whose shading is light (triangles
 // without acos texture mapping: +7% on the Cornell box); scenes with spheres / cones / rectangles
 // keep 3 (their heavier handler spills at 128 VGPRs: -45% on the main.cpp scene at 4).
-// For HBM-resident scenes (!LDS) W4 selects the shadow-ray handoff build (GI_X_HELP, XHelp): chosen
+// For HBM-resident scenes (!LDS) W4 selects the shadow-ray handoff build (XHelp): chosen
 // per launch for small launches, whose frame time is their longest paths' latency (C4: 3.01 ->
 // 2.64 ms, with spread work groups 2.40 ms); in long launches (C5) the handoff build's heavier code
 // costs 8%, so they run without.
@@ -2128,24 +2033,24 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
         // (occluded sum, next direction, throughput T, RNG key) live in a per-lane LDS slot after
         // the scene instead of in VGPRs / scratch
         double* pslot = reinterpret_cast<double*>(lds_scene + nw + nh + np + ne) + 10 * threadIdx.x;
-        mode_x_wave<STATS, GI_X_PAIR != 0, W4 && GI_X_PSL, false, false, SH, W4 && GI_X_TRI>(sc, W, H, XP, EN, pslot, nullptr, XHelp{},
+        mode_x_wave<STATS, true, W4, false, false, SH, W4>(sc, W, H, XP, EN, pslot, nullptr, XHelp{},
                                                                         cam, light, m, spp, depth, seed, rgb, rgb8, blk,
                                                                         wk, handle8, xflags, c);
     } else {
-        // dynamic LDS: GI_X_NSTK's 16 levels x 256 lanes of node indices, then GI_X_HELP's handoff
+        // dynamic LDS: the 16 levels x 256 lanes of node indices, then the handoff
         // slots (7 x 256 doubles, 2 x 256 ints)
         extern __shared__ int lds_nst[];
         XHelp hp;
-        hp.ray = reinterpret_cast<double*>(lds_nst + (GI_X_NSTK ? 16 * 256 : 0));
+        hp.ray = reinterpret_cast<double*>(lds_nst + 16 * 256);
         hp.own = reinterpret_cast<int*>(hp.ray + 7 * 256);
         hp.res = hp.own + 256;
         if constexpr (CN)   // quantised nodes (the default for large HBM-resident scenes)
-            mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0, SH, TR && GI_X_TRI>(sc, sc.xcnodes, sc.xhot, sc.xprims,
+            mode_x_wave<STATS, false, false, true, W4, SH, TR>(sc, sc.xcnodes, sc.xhot, sc.xprims,
                                                                             sc.ents, nullptr, lds_nst + threadIdx.x, hp,
                                                                             cam, light, m, spp, depth, seed, rgb, rgb8,
                                                                             blk, wk, handle8, xflags, c);
         else
-            mode_x_wave<STATS, false, false, GI_X_NSTK != 0, W4 && GI_X_HELP != 0, SH, TR && GI_X_TRI>(sc, sc.xwnodes, sc.xhot, sc.xprims,
+            mode_x_wave<STATS, false, false, true, W4, SH, TR>(sc, sc.xwnodes, sc.xhot, sc.xprims,
                                                                             sc.ents, nullptr, lds_nst + threadIdx.x, hp,
                                                                             cam, light, m, spp, depth, seed, rgb, rgb8,
                                                                             blk, wk, handle8, xflags, c);
@@ -2162,7 +2067,6 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
             atomicAdd(stats + GI_STAT_X_CYC_HIT, (unsigned long long)c.cyc_hit);
             atomicAdd(stats + GI_STAT_X_CYC_NEXT, (unsigned long long)c.cyc_next);
             atomicAdd(stats + GI_STAT_X_CYC_ALL, (unsigned long long)c.cyc_all);
-#if !GI_X_TAILPROBE
             atomicAdd(stats + GI_STAT_X_IT_NODE, (unsigned long long)c.it_node);
             atomicAdd(stats + GI_STAT_X_LN_NODE, (unsigned long long)c.ln_node);
             atomicAdd(stats + GI_STAT_X_IT_LEAF, (unsigned long long)c.it_leaf);
@@ -2171,7 +2075,6 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
             atomicAdd(stats + GI_STAT_X_LN_RS, (unsigned long long)c.ln_rs);
             atomicAdd(stats + GI_STAT_X_IT_ST, (unsigned long long)c.it_st);
             atomicAdd(stats + GI_STAT_X_LN_ST, (unsigned long long)c.ln_st);
-#endif
         }
         wave_add_stats(stats, c.rays, c.nodes, c.prims, c.px);
         uint64_t cr = c.res, pm = c.path_max;
@@ -2183,25 +2086,6 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
             atomicAdd(stats + GI_STAT_X_RESOLVED, (unsigned long long)cr);
             atomicMax(stats + GI_STAT_X_PATH_MAX, (unsigned long long)pm);
         }
-#if GI_X_TAILPROBE   // (probe, Mode R's slots): the longest drain and the longest wave life, wall ticks
-        uint64_t ex = c.w_exh ? c.w_exh : ~0ull;
-        for (int off = 32; off > 0; off >>= 1) ex = min(ex, (uint64_t)__shfl_xor(ex, off));
-        if ((threadIdx.x & 63) == 0) {   // (slots 16-25 reused) times from the wave's start, wall ticks
-            const uint64_t we = (uint64_t)wall_clock64();
-            const uint64_t te = (ex != ~0ull ? ex : we) - c.w_start, t1 = (c.w_t1 ? c.w_t1 : we) - c.w_start,
-                           t2 = (c.w_t2 ? c.w_t2 : we) - c.w_start, tl = we - c.w_start;
-            atomicMax(stats + 16, (unsigned long long)te);
-            atomicAdd(stats + 17, (unsigned long long)te);
-            atomicMax(stats + 18, (unsigned long long)t1);
-            atomicAdd(stats + 19, (unsigned long long)t1);
-            atomicMax(stats + 20, (unsigned long long)t2);
-            atomicAdd(stats + 21, (unsigned long long)t2);
-            atomicAdd(stats + 22, (unsigned long long)tl);
-            atomicAdd(stats + 23, 1ull);
-            atomicAdd(stats + 24, (unsigned long long)c.p_it);   // wave iterations after exhaustion
-            atomicAdd(stats + 25, (unsigned long long)c.p_lo);   // of those, with <= T1 paths live
-        }
-#endif
     }
 }
 
@@ -2355,32 +2239,27 @@ __global__ __launch_bounds__(64) void k_trace_ray(DevScene sc, V3 o, V3 d, V3 li
 
 long long shard_tiles(int w, int h, int shard_count) { return make_map(w, h, shard_count, 0).n_local; }
 
-// Tuning knobs read once per process from the environment (thread-safe; several host threads may
-// each drive their own device and scene): GI_X_LDS=0 disables LDS-resident scenes, GI_X_HANDLE8
-// overrides the shading-handler threshold, GI_X_FLAGS the schedule flags, GI_X_MAX_RUN the largest
-// work-unit run length (scenes of cheap background samples such as the main.cpp scene prefer 8).
+// Read once per process from the environment (thread-safe; several host threads may each drive their
+// own device and scene).  One user knob: GI_X_MAX_RUN, the largest Mode X work-unit run length (scenes
+// of cheap background samples such as the main.cpp scene prefer 8).  The rest are TEST hooks that pick
+// among kernels whose frames are identical bit for bit (tests/test_gpu_parity.py compares them):
+// GI_X_WF (0/1/2: force a Mode X form for a whole suite run), GI_X_HELP=0 (no shadow-ray handoff),
+// GI_R_FLAT (0/1/2: force a Mode R kernel), GI_RF_PER_SLOT (the flat Mode R pool size: 0 forces the
+// per-tile overflow path).
 struct XEnv {
-    int lds = 1, h8 = 0, xf = -1, run_log2 = 0, help = 1, spread = -1, wf = -1;
-    int pm = GI_X_PM;                 // pixel-major work blocks (GI_X_PM)
+    int run_log2 = 0, help = 1, wf = -1;
     int r_flat = -1;                  // Mode R kernels (GI_R_FLAT): 1 the flat phases for every scene, 0 k_mode_r
                                       // for every scene, 2 k_mode_r_batch for the whole frame (tests); -1 by size
-    long long wf_chunk = 8ll << 20;   // wavefront Mode X: units (pixel samples) per chunk = queue capacity
     int rf_per_slot = 16;             // flat Mode R: pool pairs per pixel slot of the frame (GI_RF_PER_SLOT)
 };
 const XEnv& x_env() {
     static XEnv env;
     static std::once_flag once;
     std::call_once(once, [] {
-        if (const char* v = std::getenv("GI_X_LDS")) env.lds = std::atoi(v);
-        if (const char* v = std::getenv("GI_X_HANDLE8")) env.h8 = std::max(1, std::min(8, std::atoi(v)));
-        if (const char* v = std::getenv("GI_X_FLAGS")) env.xf = std::atoi(v);
         if (const char* v = std::getenv("GI_X_HELP")) env.help = std::atoi(v) != 0;
-        if (const char* v = std::getenv("GI_X_SPREAD")) env.spread = std::atoi(v);
-        if (const char* v = std::getenv("GI_X_PM")) env.pm = std::atoi(v) != 0;
         if (const char* v = std::getenv("GI_R_FLAT")) env.r_flat = std::atoi(v);
         if (const char* v = std::getenv("GI_RF_PER_SLOT")) env.rf_per_slot = std::max(0, std::min(1024, std::atoi(v)));
         if (const char* v = std::getenv("GI_X_WF")) env.wf = std::atoi(v);
-        if (const char* v = std::getenv("GI_X_WF_CHUNK")) env.wf_chunk = std::max(1ll << 16, std::min(1ll << 30, std::atoll(v)));
         const char* v = std::getenv("GI_X_MAX_RUN");
         const int r = v ? std::max(1, std::min(128, std::atoi(v))) : GI_X_MAX_RUN;
         int lg = 0;
@@ -2419,7 +2298,7 @@ int x_form_choice(const DevScene& sc, const XLaunchCfg& xc, const gi_opts& o) {
     // 4.8-5.0 ms, the 1k soup even) run k_seg too
     return (xc.kv >= 2 || (size_t)sc.n_xwnodes * sizeof(XWNode) <= ((size_t)1 << 20)) ? 2 : 0;
 }
-long long x_wf_chunk() { return x_env().wf_chunk; }
+long long x_wf_chunk() { return 8ll << 20; }   // wavefront Mode X: units (pixel samples) per chunk = queue capacity
 int x_env_rf_per_slot() { return x_env().rf_per_slot; }
 unsigned rf_own_pairs() { return GI_RF_S0; }
 unsigned rf_page_pairs() { return GI_RF_PAGE; }
@@ -2438,10 +2317,9 @@ int r_kernel_choice(const DevScene& sc, const gi_opts& o) {
 }
 
 hipError_t x_launch_config(const DevScene& sc, int device, XLaunchCfg& cfg) {
-    const bool lds = x_env().lds != 0 && sc.x_lds_bytes > 0;
-    cfg.lds_bytes = lds ? (size_t)sc.x_lds_bytes + ((sc.x_waves4 && GI_X_PSL) ? 256 * 10 * sizeof(double) : 0)
-                        : (GI_X_NSTK ? 16 * 256 * sizeof(int) : 0) +
-                              (GI_X_HELP ? 256 * (7 * sizeof(double) + 2 * sizeof(int)) : 0);
+    const bool lds = sc.x_lds_bytes > 0;
+    cfg.lds_bytes = lds ? (size_t)sc.x_lds_bytes + (sc.x_waves4 ? 256 * 10 * sizeof(double) : 0)
+                        : 16 * 256 * sizeof(int) + 256 * (7 * sizeof(double) + 2 * sizeof(int));
     cfg.kv = 2 * (int)lds + ((lds && sc.x_waves4) ? 1 : 0);   // 0 / 1 (per launch, HELP): HBM-resident
     int cus = 0, per_cu = 0;
     hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
@@ -2537,7 +2415,7 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
         // at most 32 samples per resident lane -- their time is the longest paths' latency and lanes
         // run out of work early (C4: 10 per lane; X-soup1000, 169 per lane, is throughput-bound and
         // 25% slower spread)
-        const bool help = GI_X_HELP && xc.kv == 0 && env.help &&
+        const bool help = xc.kv == 0 && env.help &&
                           n_slots * (long long)o.spp <= 32ll * 256ll * (long long)xc.resident;
         const int kv = xc.kv + (help ? 1 : 0);
         const size_t lds_bytes = xc.lds_bytes;
@@ -2569,16 +2447,15 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
         if (stats) hipLaunchKernelGGL(k_x_classify<true>, cgrid, dim3(kClassifyBlock), 0, stream, sc, cam, m, s1 - s0, rgb, rgb8, cl, sc.work + 1, st, zero2);
         else hipLaunchKernelGGL(k_x_classify<false>, cgrid, dim3(kClassifyBlock), 0, stream, sc, cam, m, s1 - s0, rgb, rgb8, cl, sc.work + 1, st, zero2);
         // shading-handler threshold (eighths of the live lanes that must wait): the builder's
-        // estimate for the scene (DevScene::x_handle8) unless GI_X_HANDLE8 overrides it
-        const int h8 = env.h8 > 0 ? env.h8 : sc.x_handle8;
+        // estimate for the scene (DevScene::x_handle8)
+        const int h8 = sc.x_handle8;
         // schedule flags (bit 0: inline shadow, bit 2: no shadow rays, bit 3: shadow handoff, bit 4:
-        // spread work groups -- GI_X_SPREAD, by default with the handoff build) and the maximum run
-        // length (log2, bits 8-10)
-        const int xf = (env.xf >= 0 ? env.xf : sc.x_flags) | (env.run_log2 << 8) |
-                       ((o.flags & GI_FLAG_X_NO_SHADOW) ? 4 : 0) | (env.help ? 8 : 0) |
-                       ((env.spread > 0 || (env.spread < 0 && help)) ? 16 : 0) | (env.pm ? 32 : 0);
+        // spread work groups -- with the handoff build, bit 5: pixel-major work blocks) and the
+        // maximum run length (log2, bits 8-10)
+        const int xf = sc.x_flags | (env.run_log2 << 8) | ((o.flags & GI_FLAG_X_NO_SHADOW) ? 4 : 0) | (env.help ? 8 : 0) |
+                       (help ? 16 : 0) | 32;
         if (form) {   // gi_wf.hip's forms, timed as one pass
-            if (!xs.wcnt || (form == 1 && (!xs.wq[0] || !xs.wq[1] || !xs.h_nlist || xs.wcap <= 0))) return hipErrorInvalidValue;
+            if (!xs.wcnt || (form == 1 && (!xs.wq[0] || !xs.wq[1] || xs.wcap <= 0))) return hipErrorInvalidValue;
             e = launch_wf(sc, xc.kv, xc.wf_lds_bytes, form == 2 ? xc.seg_resident : xc.wf_resident, form, cam, light, w, h, y0,
                           o, rgb, rgb8, xs, sc.work + 1, stats ? st : nullptr, xf, stream, ev_begin, ev_end);
             if (e != hipSuccess) return e;

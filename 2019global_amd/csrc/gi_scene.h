@@ -243,12 +243,10 @@ struct XScratch {
     long long cap = 0;          // pixel slots the buffers hold
     int spp = 0;                // samples per pixel the part buffer was sized for
     // wavefront Mode X (gi_wf.hip): two path queues of wcap entries (SoA: 12 fp64 fields + a
-    // (list index, sample) pair = 104 B per entry), 2 device counters per bounce, and a pinned word
-    // for the work list's length
+    // (list index, sample) pair = 104 B per entry) and 2 device counters per bounce
     double* wq[2] = {nullptr, nullptr};
     unsigned* wid[2] = {nullptr, nullptr};
     unsigned* wcnt = nullptr;
-    unsigned* h_nlist = nullptr;
     long long wcap = 0;
     // flat Mode R (gi_kernels.hip k_rf_*): candidate pairs, one word each -- every tile's own region
     // of GI_RF_S0, then the pool of rf_pages pages of GI_RF_PAGE (rf_pairs holds both); per tile its
@@ -269,6 +267,8 @@ struct XScratch {
     unsigned rf_pages = 0;
     long long rf_slots = 0;
     size_t rf_bytes = 0;
+    long long rf_failed = 0;   // pixel slots for which the allocation failed (0: none): not retried for
+                               // that many or more; such frames render through k_mode_r_batch
 };
 
 // Mode X launch configuration, computed once per scene when it is created (gi_capi.cpp, on the

@@ -30,30 +30,24 @@
 namespace gi {
 namespace {
 
+constexpr long long kWfTile = 8;   // pixel tiles are 8 x 8 (GI_TILE)
+
 #ifndef GI_WF_MIN_WAVES_LDS
 #define GI_WF_MIN_WAVES_LDS 4   // LDS-resident scenes, light shading (<= 128 VGPRs)
 #endif
 #ifndef GI_WF_MIN_WAVES
 #define GI_WF_MIN_WAVES 3       // other scenes
 #endif
-#ifndef GI_WF_PAIR
-#define GI_WF_PAIR 1   // LDS-resident scenes: leaf records tested two at a time (two interleaved fp64 chains)
-#endif
-#ifndef GI_WF_AXIS
-#define GI_WF_AXIS 0   // LDS-resident scenes: 1 = node slab tests accumulated axis by axis (fewer live VGPRs;
-                       // round 5, spills gone: the 12 loads at once, 0, give C3 4.90 -> 4.81 ms, C2 -6%)
-#endif
 #ifndef GI_WF_TAKE
 #define GI_WF_TAKE 16   // most 64-entry batches a wave takes per atomic on the queue's counter
 #endif
-#ifndef GI_WF_PSL
 // a path's L and T wait out the two traversals in a per-lane LDS slot (column layout, 6 x 256 fp64 per
 // workgroup) instead of VGPRs: the 4-wave kernel stays within 128 VGPRs.  k_seg also keeps the path's
 // RNG key, its output index and sample, and its bounce there (fields 6, 7, 8), read where they are
-// used: carried in VGPRs across the traversals they were spilled to scratch (136 -> 56 B per lane)
-#define GI_WF_PSL 1
-#endif
-constexpr size_t kWfSlotBytes = GI_WF_PSL ? 9 * 256 * sizeof(double) : 0;
+// used: carried in VGPRs across the traversals they were spilled to scratch (136 -> 56 B per lane).
+// LDS-resident scenes test leaf records two at a time (PAIR: two interleaved fp64 chains) and their
+// node slab tests issue the 12 loads at once (round 5: C3 4.90 -> 4.81 ms against axis by axis)
+constexpr size_t kWfSlotBytes = 9 * 256 * sizeof(double);
 // a path's identity where the shading needs it: RNG key, sample, bounce
 struct PathId {
     uint64_t key;
@@ -118,13 +112,17 @@ __device__ __forceinline__ int wf_trace(NodeP W, HotP H, V3 o, V3 d, double tmax
                         const double tq = two ? x_prim_t<TRI>(r1.h, o, d, MX_TMIN) : INFINITY;
                         nprim += two ? 2 : 1;
                         if (ANY) {
-                            if (ta < tmax || tq < tmax) {
+                            if ((ta < tmax) | (tq < tmax)) {
                                 best = ta < tmax ? r0.h.prim : r1.h.prim;
                                 break;
                             }
-                        } else {
-                            if (ta < tb || (ta == tb && r0.h.prim < best)) { tb = ta; best = r0.h.prim; }
-                            if (tq < tb || (tq == tb && r1.h.prim < best)) { tb = tq; best = r1.h.prim; }
+                        } else {   // (selects, not branches: | and & do not short-circuit)
+                            const bool ua = (ta < tb) | ((ta == tb) & (r0.h.prim < best));
+                            tb = ua ? ta : tb;
+                            best = ua ? r0.h.prim : best;
+                            const bool uq = (tq < tb) | ((tq == tb) & (r1.h.prim < best));
+                            tb = uq ? tq : tb;
+                            best = uq ? r1.h.prim : best;
                             tbf = up32(tb);
                         }
                     }
@@ -137,10 +135,11 @@ __device__ __forceinline__ int wf_trace(NodeP W, HotP H, V3 o, V3 d, double tmax
                         const double t = x_prim_t<TRI>(rec.h, o, d, MX_TMIN);
                         if (ANY) {
                             if (t < tmax) { best = rec.h.prim; break; }
-                        } else if (t < tb || (t == tb && rec.h.prim < best)) {
-                            tb = t;
-                            best = rec.h.prim;
-                            tbf = up32(t);
+                        } else {
+                            const bool u = (t < tb) | ((t == tb) & (rec.h.prim < best));
+                            tb = u ? t : tb;
+                            best = u ? rec.h.prim : best;
+                            tbf = u ? up32(t) : tbf;
                         }
                     }
                 }
@@ -190,7 +189,7 @@ struct WFArgs {
 };
 
 // The scene views of a bounce / segment kernel.  LDS: wide nodes, leaf records, primitives and
-// entities staged in LDS by the workgroup (as k_mode_x does); then the per-lane path slots (GI_WF_PSL).
+// entities staged in LDS by the workgroup (as k_mode_x does); then the per-lane path slots.
 // HBM-resident scenes: the per-lane level stack (16 x 256 ints), then the path slots.
 struct WFView {
     const XWNode* LW = nullptr;
@@ -270,9 +269,9 @@ __device__ __forceinline__ void wf_store(double* part, double* rgb, uint8_t* rgb
 // One path segment, bounce b (every lane of the wave runs the same sequence): closest hit -> hit
 // point and light direction -> shadow any-hit -> texture and Blinn-Phong with the shadow answer ->
 // L += T * local -> the next direction (mirror with probability refl, else T *= texel / 2 and a
-// cosine-weighted direction).  The oracle's operations (sample_mode_x).  In: o, d and (GI_WF_PSL: in
-// the lane's path slot, else in L, T) the path's L and T.  Out: true when the path continues (o, d
-// set to its next ray; L, T in registers and, GI_WF_PSL, in the slot); false when it ends (L final).
+// cosine-weighted direction).  The oracle's operations (sample_mode_x).  In: o, d and (in the lane's
+// path slot) the path's L and T.  Out: true when the path continues (o, d set to its next ray; L, T in
+// registers and in the slot); false when it ends (L final).
 // STATS: the wave's traversal-loop iterations (closest, shadow) and the lanes' own steps, summed into
 // ws (lane 0) -- the divergence profile of a segment
 struct WFSegStats {
@@ -298,7 +297,7 @@ __device__ __forceinline__ bool x_segment(const DevScene& sc, const WFView& v, c
     // ---- closest hit
     double tbest = INFINITY;
     int best;
-    if constexpr (LDS) best = wf_trace<false, GI_WF_PAIR != 0, GI_WF_AXIS != 0, SH, TRI, false>(v.LW, v.LH, o, d, INFINITY, act, v.nst, tbest, nnode, nprim, st_steps);
+    if constexpr (LDS) best = wf_trace<false, true, false, SH, TRI, false>(v.LW, v.LH, o, d, INFINITY, act, v.nst, tbest, nnode, nprim, st_steps);
     else if constexpr (CN) best = wf_trace<false, false, false, SH, TRI, true>(sc.xcnodes, sc.xhot, o, d, INFINITY, act, v.nst, tbest, nnode, nprim, st_steps);
     else best = wf_trace<false, false, false, SH, TRI, true>(sc.xwnodes, sc.xhot, o, d, INFINITY, act, v.nst, tbest, nnode, nprim, st_steps);
     if (act) ++nrays;
@@ -321,7 +320,7 @@ __device__ __forceinline__ bool x_segment(const DevScene& sc, const WFView& v, c
     if (!no_shadow) {
         double tdummy;
         int sb;
-        if constexpr (LDS) sb = wf_trace<true, GI_WF_PAIR != 0, GI_WF_AXIS != 0, SH, TRI, false>(v.LW, v.LH, P, Ld, ldist, hit, v.nst, tdummy, nnode, nprim, st_steps);
+        if constexpr (LDS) sb = wf_trace<true, true, false, SH, TRI, false>(v.LW, v.LH, P, Ld, ldist, hit, v.nst, tdummy, nnode, nprim, st_steps);
         else if constexpr (CN) sb = wf_trace<true, false, false, SH, TRI, true>(sc.xcnodes, sc.xhot, P, Ld, ldist, hit, v.nst, tdummy, nnode, nprim, st_steps);
         else sb = wf_trace<true, false, false, SH, TRI, true>(sc.xwnodes, sc.xhot, P, Ld, ldist, hit, v.nst, tdummy, nnode, nprim, st_steps);
         occl = sb >= 0;
@@ -332,7 +331,7 @@ __device__ __forceinline__ bool x_segment(const DevScene& sc, const WFView& v, c
         ws.cyc_s += c1 - c0;
         c0 = c1;
     }
-    if (GI_WF_PSL) {   // every lane: a lane without a path never uses them, so L and T are dead during
+    {   // every lane: a lane without a path never uses them, so L and T are dead during
         L = v3(v.pl[0], v.pl[256], v.pl[512]);      // the traversals (conditioned on act, the register copies
         T = v3(v.pl[768], v.pl[1024], v.pl[1280]);  // stayed live for inactive lanes and were spilled)
     }
@@ -382,7 +381,7 @@ __device__ __forceinline__ bool x_segment(const DevScene& sc, const WFView& v, c
             }
             o = P;
         }
-        if (GI_WF_PSL && cont) {
+        if (cont) {
             v.pl[0] = L.x; v.pl[256] = L.y; v.pl[512] = L.z;
             v.pl[768] = T.x; v.pl[1024] = T.y; v.pl[1280] = T.z;
         }
@@ -463,10 +462,8 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
                     d = normalize(d0);
                 }
             }
-            if (GI_WF_PSL) {
-                v.pl[0] = L.x; v.pl[256] = L.y; v.pl[512] = L.z;
-                v.pl[768] = T.x; v.pl[1024] = T.y; v.pl[1280] = T.z;
-            }
+            v.pl[0] = L.x; v.pl[256] = L.y; v.pl[512] = L.z;
+            v.pl[768] = T.x; v.pl[1024] = T.y; v.pl[1280] = T.z;
         }
         WFSegStats ws;
         const bool cont = x_segment<false, LDS, SH, TRI, CN>(sc, v, light, depth, no_shadow, act, [&] { return PathId{key, smp, b}; }, o, d, L, T,
@@ -538,7 +535,6 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
     bool exhausted = false;                    // the frame's units are all handed out (uniform)
     bool live = false;                         // this lane carries a path
     unsigned li = 0, smp = 0;
-    int b = 0;
     long long idx = -1;
     uint64_t key = 0;
     V3 o = cam.pos, d = v3(1, 0, 0), L = v3(0, 0, 0), T = v3(1, 1, 1);
@@ -599,18 +595,15 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
                     wf_store(a.part, rgb, rgb8, spp, idx, smp, v3(0, 0, 0));
                 } else {
                     live = true;
-                    b = 0;
                     o = cam.pos;
                     d = normalize(d0);
                     L = v3(0, 0, 0);
                     T = v3(1, 1, 1);
-                    if (GI_WF_PSL) {
-                        v.pl[0] = 0.0; v.pl[256] = 0.0; v.pl[512] = 0.0;
-                        v.pl[768] = 1.0; v.pl[1024] = 1.0; v.pl[1280] = 1.0;
-                        slot_put_u64(v.pl, 6, key);
-                        slot_put_u64(v.pl, 7, (uint64_t)(uint32_t)idx | ((uint64_t)smp << 32));   // (idx < 2^32: work-list index or pixel)
-                        slot_put_u64(v.pl, 8, 0ull);
-                    }
+                    v.pl[0] = 0.0; v.pl[256] = 0.0; v.pl[512] = 0.0;
+                    v.pl[768] = 1.0; v.pl[1024] = 1.0; v.pl[1280] = 1.0;
+                    slot_put_u64(v.pl, 6, key);
+                    slot_put_u64(v.pl, 7, (uint64_t)(uint32_t)idx | ((uint64_t)smp << 32));   // (idx < 2^32: work-list index or pixel)
+                    slot_put_u64(v.pl, 8, 0ull);
                 }
             }
         }
@@ -626,19 +619,14 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
         }
         const bool cont = x_segment<STATS, LDS, SH, TRI, CN>(
             sc, v, light, depth, no_shadow, live,
-            [&] { return GI_WF_PSL ? PathId{slot_get_u64(v.pl, 6), (unsigned)(slot_get_u64(v.pl, 7) >> 32), (int)slot_get_u64(v.pl, 8)}
-                                   : PathId{key, smp, b}; },
+            [&] { return PathId{slot_get_u64(v.pl, 6), (unsigned)(slot_get_u64(v.pl, 7) >> 32), (int)slot_get_u64(v.pl, 8)}; },
             o, d, L, T, nnode, nprim, nrays, ws);
         if (live) {
             if (cont) {
-                if (GI_WF_PSL) slot_put_u64(v.pl, 8, slot_get_u64(v.pl, 8) + 1);
-                else ++b;
-            } else if (GI_WF_PSL) {
+                slot_put_u64(v.pl, 8, slot_get_u64(v.pl, 8) + 1);
+            } else {
                 const uint64_t is = slot_get_u64(v.pl, 7);
                 wf_store(a.part, rgb, rgb8, spp, (long long)(uint32_t)is, (unsigned)(is >> 32), L);
-                live = false;
-            } else {
-                wf_store(a.part, rgb, rgb8, spp, idx, smp, L);
                 live = false;
             }
         }
@@ -702,9 +690,9 @@ hipError_t wf_occupancy(const DevScene& sc, int kv, size_t lds_bytes, int form, 
 }
 
 // The Mode X pass after k_x_classify and before k_x_reduce in the wavefront forms.
-//  form 1 (wavefront): reads the work list's length back to the host (one stream synchronisation),
-//    then per chunk of units (the queue capacity) `depth` bounce launches; counters: 2 per bounce
-//    (take, n_out), zeroed per chunk.
+//  form 1 (wavefront): per chunk of units (the queue capacity; chunks for the launch's every pixel
+//    slot, those past the work list's end return at once on the device) `depth` bounce launches;
+//    counters: 2 per bounce (take, n_out), zeroed per chunk.
 //  form 2 (segment-synchronous): one persistent launch; counter: a 64-bit unit count at xs.wcnt.
 hipError_t launch_wf(const DevScene& sc, int kv, size_t lds_bytes, int resident, int form, const CamDev& cam, V3 light,
                      int w, int h, int y0, const gi_opts& o, double* rgb, uint8_t* rgb8, const XScratch& xs,
@@ -733,10 +721,11 @@ hipError_t launch_wf(const DevScene& sc, int kv, size_t lds_bytes, int resident,
         if (ev_end) (void)hipEventRecord(ev_end, stream);
         return hipGetLastError();
     }
-    e = hipMemcpyAsync(xs.h_nlist, n_list_dev, sizeof(unsigned), hipMemcpyDeviceToHost, stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(stream);
-    if (e != hipSuccess) return e;
-    const unsigned long long units = (unsigned long long)*xs.h_nlist * (unsigned long long)(s1 - s0);
+    // chunks for every pixel slot of the launch listed (the list's length stays on the device: no host
+    // synchronisation, so the form can be captured in a graph); a chunk beyond the listed units' end
+    // finds no input on the device and its bounce kernels return at once
+    const unsigned long long units = (unsigned long long)m.n_local * (unsigned long long)(kWfTile * kWfTile) *
+                                     (unsigned long long)(s1 - s0);
     if (ev_begin) (void)hipEventRecord(ev_begin, stream);
     for (unsigned long long u0 = 0; u0 < units; u0 += (unsigned long long)xs.wcap) {
         e = hipMemsetAsync(xs.wcnt, 0, 2 * (size_t)depth * sizeof(unsigned), stream);

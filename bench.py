@@ -19,15 +19,19 @@ inputs resident in HBM; `mray_s_all_rays` also counts the primar
 exactly without traversal.  The ray count per frame is exact: a counting launch (GI_FLAG_STATS) of the same
 deterministic frame runs before the timed region.
 
-roofline: the dominant kernel (k_mode_x) against HBM: achieved = algorithmic bytes per launch
-(Mode X: wide-node records x 256 B -- 128 B for the quantised nodes of large HBM-resident scenes --
-+ primitive records x 80 B + 27 B/pixel output; Mode R: 64 B nodes + 144 B triangles; DESIGN.md
-§Measurement) /
-average launch time of that kernel alone from HIP events recorded directly around it on the launch
-stream (GI_FLAG_TIME, read with gi_scene_kernel_ms); traffic = HBM bytes per launch from the
-committed rocprofv3 PMC summary when present (profiles/), else null.
-cpu_baseline: this repo's CPU port of the same integrator (oracle, test infrastructure), OpenMP,
-on a bounded window of the same frame; reference_cpu: the compiled reference itself (depth 1, the
+roofline: the resource the dominant kernel (k_seg / k_mode_x; Mode R: the flat phases) uses.  Mode X:
+the VALU pipe -- achieved = useful VALU lane-op slots per launch (PMC counters of the same workload,
+profiles/rNN_<workload>_pmc.json: pipe-weighted VALU instructions x 64 lanes x lane utilisation) /
+the kernel's average launch time from HIP events recorded directly around it on the launch stream
+(GI_FLAG_TIME, read with gi_scene_kernel_ms), against 1,024 SIMDs x 32 lanes x 2.4 GHz; `binding`
+names what holds it below (latency / valu / hbm).  Mode R: the FP64 vector peak.  The
+algorithmic record bytes (Mode X: wide-node records x 256 B -- 128 B for the quantised nodes of
+large HBM-resident scenes -- + primitive records x 80 B + 27 B/pixel output; Mode R: 64 B nodes +
+144 B triangles) per launch / that time stay beside it as hbm_alg_frac, and traffic = the HBM bytes
+the counters saw (hbm_counter_frac): the records live in LDS / L2, so the two differ 10-100x.
+cpu_baseline: this repo's CPU port of the same integrator (oracle, test infrastructure), OpenMP over
+the job's CPU share and on 1 thread, on full-width rows spread over the same frame (Mode X: those
+rows also checked against the timed GPU frame, bit for bit); reference_cpu: the compiled reference itself (depth 1, the
 only depth it has) on a strided sample of the same frame, when oracle/_ref is present.
 """
 from __future__ import annotations
@@ -71,6 +75,9 @@ def make_scene(name):
 
 
 FP64_VALU_PEAK_TFS = 78.6     # MI355X FP64 vector peak (AMD spec; half the guide's 157.3 TF FP32 vector rate)
+# VALU lane-op slots per second: 256 CUs x 4 SIMDs x 32 lanes per cycle (a wave64 instruction holds the
+# SIMD's pipe 2 cycles, an f64 one 4) x 2.4 GHz -- the Mode X roofline (f64 instructions count twice)
+VALU_LANE_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 N_SIMDS = 1024                 # 256 CUs x 4 SIMDs
 
 
@@ -108,7 +115,7 @@ def counter_ceilings(workload: str, kern_ms: float, kernel: str = ""):
       * FP64 (Mode R): f64 VALU instructions / all VALU instructions, and the f64 FLOP
         rate (SQ_INSTS_VALU_FLOPS_FP64, a per-wave-instruction count, x 64 lanes x lane utilisation)
         against the 78.6 TF/s FP64 vector peak -- Mode R's roofline.
-    `binding` names the tightest: valu_pipe when the VALU pipe is busy >= 75% of the cycles (2 cycles
+    `binding` names the tightest: valu when the VALU pipe is busy >= 75% of the cycles (2 cycles
     per wave64 instruction, 4 for f64), else hbm when counter traffic is >= 60% of peak, else latency
     (the waves wait on dependent instructions and memory)."""
     got = pmc_summary(workload, kernel)
@@ -132,6 +139,9 @@ def counter_ceilings(workload: str, kern_ms: float, kernel: str = ""):
             # every 4 cycles); valu_issue_frac above prices every instruction at 4 cycles
             n64 = sum(f64n)
             out["valu_pipe_frac"] = round(((c["SQ_INSTS_VALU"] - n64) * 2.0 + n64 * 4.0) / (N_SIMDS * cycles), 4)
+            # VALU lane-op slots per launch at pipe weight (an f64 instruction holds the pipe twice as long,
+            # so it counts twice): the useful ones are these x the lane utilisation (Mode X roofline)
+            out["valu_lane_slots"] = int(((c["SQ_INSTS_VALU"] - n64) + 2.0 * n64) * 64.0)
     if c.get("SQ_ACTIVE_INST_VALU") and c.get("SQ_THREAD_CYCLES_VALU"):
         out["valu_lane_util"] = round(c["SQ_THREAD_CYCLES_VALU"] / (64.0 * c["SQ_ACTIVE_INST_VALU"]), 4)
     if "valu_issue_frac" in out and "valu_lane_util" in out:
@@ -153,7 +163,7 @@ def counter_ceilings(workload: str, kern_ms: float, kernel: str = ""):
         out["f64_valu_frac"] = round(out["f64_tflops"] / FP64_VALU_PEAK_TFS, 5)
     pipe = out.get("valu_pipe_frac", out.get("valu_issue_frac", 0))
     if pipe >= 0.75:
-        out["binding"] = "valu_pipe"
+        out["binding"] = "valu"
     elif out.get("hbm_counter_frac", 0) >= 0.6:
         out["binding"] = "hbm"
     else:   # neither pipe is full: the waves wait on dependent instructions and memory
@@ -174,22 +184,34 @@ def cpu_info():
 
 
 def cpu_threads():
-    """Threads for the CPU port: OMP_NUM_THREADS when set (the GPU box sets it to this job's CPU share,
-    16; os.cpu_count() there reports the whole machine), else every core."""
+    """Threads for the CPU port: every CPU this job may use -- OMP_NUM_THREADS when set (the GPU box
+    sets it to the job's CPU share, 16: the pool's rules size worker pools to that share, while
+    os.cpu_count() there reports the whole machine), else the CPUs of the process's affinity mask."""
     v = os.environ.get("OMP_NUM_THREADS")
-    return max(1, int(v)) if v and v.isdigit() else (os.cpu_count() or 1)
+    if v and v.isdigit():
+        return max(1, int(v))
+    try:
+        return max(1, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
 
 
-def cpu_baseline(scn_text, w, h, mode, spp, depth, seed, target_s=20.0):
+def cpu_baseline(scn_text, w, h, mode, spp, depth, seed, target_s=16.0, target_1t_s=10.0, gpu_frame=None):
     """The oracle (this repo's CPU port, OpenMP) on a frame-representative sample of the same workload:
     full-width rows spread evenly over the frame (y = row0 + k * stride).  A probe of 8 rows sets the
-    rate, then about `target_s` seconds of rows are timed.  Mode X `value` basis: rays that reach the
+    rate, then about `target_s` seconds of rows are timed on every CPU this job may use (`value`,
+    `cores`), and about `target_1t_s` seconds on ONE thread (`value_1t`; the reference's own loop is
+    single-threaded, raytracer.h:32-33).  Mode X `value` basis: rays that reach the
     scene -- primary samples whose ray misses the scene's bounding box add exactly +0 and are counted
     apart (the GPU's classify pass and root-box pretest resolve the same kind of sample apart from its
     `value`), so `value` here is traced rays per second like the GPU line's; `value_all_rays` counts
-    them too.  Mode R: one ray per pixel over a centred window (the reference's only depth)."""
+    them too.  gpu_frame (Mode X; (rgb (h, w, 3) fp64, rgb8 (h, w, 3)) of the timed GPU frame, N = 1):
+    the sampled rows the oracle rendered are compared with it bit for bit (`gpu_rows_check`), so the
+    bench checks its own frame.  Mode R: one ray per pixel over a centred window (the reference's
+    only depth)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_util as U
+    import numpy as np
     threads = cpu_threads()
     model, host_cores = cpu_info()
     if mode == 0:
@@ -204,23 +226,52 @@ def cpu_baseline(scn_text, w, h, mode, spp, depth, seed, target_s=20.0):
                 "sample": f"Mode R window x[{win[0]},{win[2]}) y[{win[1]},{win[3]}), {rays} rays, {dt:.2f} s wall, "
                           f"OpenMP over {threads} threads"}
 
-    def run(row0, stride, n_rows):
+    def run(row0, stride, n_rows, nt, pixels=False):
         t = time.perf_counter()
-        r = U.oracle_time_rows(scn_text, w, h, spp, depth, seed, row0, stride, n_rows, threads)
+        r = U.oracle_time_rows(scn_text, w, h, spp, depth, seed, row0, stride, n_rows, nt, pixels=pixels)
         return r, time.perf_counter() - t
 
-    n, stride = min(8, h), max(1, h // min(8, h))
-    r, dt = run(stride // 2, stride, n)
-    for _ in range(3):   # rescale until the sample takes about target_s (whole frame at most)
-        if dt >= 0.5 * target_s or n >= h:
-            break
-        n = int(max(1, min(h, n * target_s / max(dt, 1e-3))))
-        stride = max(1, h // n)
-        n = min(n, (h + stride - 1) // stride)
-        r, dt = run(stride // 2, stride, n)
+    def sized(nt, target, pixels=False):
+        n, stride = min(8, h), max(1, h // min(8, h))
+        r, dt = run(stride // 2, stride, n, nt)
+        for _ in range(3):   # rescale until the sample takes about target (whole frame at most)
+            if dt >= 0.5 * target or n >= h:
+                break
+            n = int(max(1, min(h, n * target / max(dt, 1e-3))))
+            stride = max(1, h // n)
+            n = min(n, (h + stride - 1) // stride)
+            r, dt = run(stride // 2, stride, n, nt, pixels)
+        if pixels and "rgb" not in r:
+            r, dt = run(stride // 2, stride, n, nt, pixels)
+        return r, dt, stride
+
+    r, dt, stride = sized(threads, target_s, pixels=gpu_frame is not None)
     traced = r["rays"] - r["resolved"]
-    return {"value": round(traced / dt / 1e6, 4), "unit": "Mray/s", "cores": threads, "kind": "port",
+    r1, dt1, stride1 = sized(1, target_1t_s)
+    traced1 = r1["rays"] - r1["resolved"]
+    v_all, v_1t = traced / dt / 1e6, traced1 / dt1 / 1e6
+    extra = {}
+    if gpu_frame is not None:
+        g, g8 = gpu_frame
+        same = U.bits_equal(g[r["rows"]], r["rgb"]).all(2) & (g8[r["rows"]] == r["q"]).all(2)
+        extra["gpu_rows_check"] = (f"{len(r['rows'])} sampled rows ({r['pixels']} pixels) of the timed GPU frame "
+                                   + ("bit-identical to the oracle" if same.all() else
+                                      f"MISMATCH: {int((~same).sum())} pixels differ from the oracle"))
+    return {"value": round(v_all, 4), "unit": "Mray/s", "cores": threads, "kind": "port",
             "value_all_rays": round(r["rays"] / dt / 1e6, 4),
+            # VERDICT r05 item 6 / BASELINE.md: the port at 1 thread and at every CPU this job may use
+            "value_1t": round(v_1t, 4), "cores_1t": 1,
+            "value_all": round(v_all, 4), "cores_all": threads,
+            "parallel_efficiency": round(v_all / (threads * v_1t), 3) if v_1t > 0 else None,
+            # an UPPER bound for the whole host: perfect scaling of the 1-thread rate over every logical
+            # CPU (no run may use them: the pool sizes a job's worker pools to its CPU share)
+            "value_host_upper_bound": round(v_1t * host_cores, 2), "host_cores_note":
+                f"the host has {host_cores} logical CPUs; this job's share is {threads} (OMP_NUM_THREADS / "
+                f"affinity), the most any run here may use, so value_all is measured at {threads} and "
+                f"value_host_upper_bound = value_1t x {host_cores} bounds an all-core run from above",
+            "sample_1t": f"{r1['pixels'] // w} full-width rows y = {stride1 // 2} + k*{stride1}, {traced1} traced rays, "
+                         f"{dt1:.2f} s wall, 1 thread",
+            **extra,
             "cpu_model": model, "host_cores": host_cores,
             "value_basis": "rays that reach the scene (primary samples missing the scene's bounding box counted "
                            "apart, as the GPU's value does); value_all_rays includes them.  The two sides resolve "
@@ -477,11 +528,31 @@ def main():
                          "kernel_ms": round(kern_ms, 4), "render_call_ms": round(render_ms, 4),
                          "node_visits": st[gi.STAT_NODES], "prim_tests": st[gi.STAT_PRIMS],
                          "node_record_bytes": node_bytes,
-                         "alg_bytes_note": "algorithmic record bytes; for LDS-resident scenes (C2/C3) they "
-                                           "are served from LDS, see hbm_counter_frac / binding"},
+                         "alg_bytes_note": "algorithmic record bytes (north_star's HBM roofline is met on these "
+                                           "only: for LDS-resident scenes (C2/C3) they are served from LDS, for "
+                                           "C4/C5 mostly from L2/MALL -- hbm_counter_frac is what reaches HBM)"},
         }
         if ceil:
             out["roofline"].update({k: v for k, v in ceil.items() if k != "hbm_counter_bytes"})
+        if mode == 1 and ceil and ceil.get("valu_lane_slots") and "valu_lane_util" in ceil:
+            # the headline roofline is the resource the kernel actually uses.  Mode X's
+            # records live in LDS (C2/C3) or L2/MALL (C4/C5): counters show 1-9% of HBM, so HBM is not the
+            # roofline.  Its instruction stream is VALU: achieved = the USEFUL VALU lane-op slots per launch
+            # (PMC: pipe-weighted VALU instructions x 64 x lane utilisation, pmc_source) / live kernel time,
+            # against the VALU lane peak -- frac = the pipe's busy share x its lane utilisation.  `binding`
+            # says what holds it below that peak (latency: the pipe is not full, waves wait on dependent
+            # fp64 chains and LDS/L2 reads).  The algorithmic-byte figure stays as hbm_alg_*.
+            r = out["roofline"]
+            hbm_part = {"hbm_alg_achieved_gbs": r.pop("achieved"), "hbm_peak_gbs": r.pop("peak"),
+                        "hbm_alg_frac": r.pop("frac")}
+            useful = ceil["valu_lane_slots"] * ceil["valu_lane_util"]
+            ach = useful / (kern_ms * 1e-3) / 1e12
+            r.update({"bound": "valu", "achieved": round(ach, 4), "peak": round(VALU_LANE_PEAK_TOPS, 3),
+                      "unit": "Tlane-op/s", "frac": round(ach / VALU_LANE_PEAK_TOPS, 5),
+                      "achieved_note": "useful VALU lane-op slots per launch (PMC: (VALU - f64 + 2 x f64 "
+                                       "instructions) x 64 x valu_lane_util, pmc_source) / live kernel time; "
+                                       "peak = 1,024 SIMDs x 32 lanes x 2.4 GHz; frac = valu_pipe_frac x "
+                                       "valu_lane_util at the live kernel time", **hbm_part})
         if mode == 0 and ceil and "f64_tflops" in ceil:
             # Mode R is FP64-VALU bound by arithmetic intensity (the exact ExpBox node
             # test is ~20-40 fp64 ops per record byte): the roofline is the FP64 vector peak; the
@@ -545,7 +616,10 @@ def main():
             out["ms_per_frame_with_d2h"] = out["host_path"]["ms_per_frame"]["rgb8"]
         if not args.no_cpu_baseline and world == 1:
             scn = sc.to_scn()
-            out["cpu_baseline"] = cpu_baseline(scn, w, h, mode, spp, depth, args.seed)
+            gf = None
+            if mode == 1:   # the last timed frame (deterministic: every timed frame is this one)
+                gf = (buf.cpu().numpy().reshape(h, w, 3), buf8.cpu().numpy().reshape(h, w, 3))
+            out["cpu_baseline"] = cpu_baseline(scn, w, h, mode, spp, depth, args.seed, gpu_frame=gf)
             ref = reference_cpu(scn, w, h)
             if ref is not None:
                 out["reference_cpu"] = ref

@@ -112,10 +112,8 @@ typedef enum gi_mode {
                                     shading (raytracer.h:41-84, material.h:48-62), so its stages can
                                     be checked against the reference's frames (tests) */
 #define GI_FLAG_X_WF 16u         /* Mode X: the wavefront form (one launch per bounce over a compacted queue of
-                                    live paths, gi_wf.hip) whatever the scene; same frame bit for bit.  An A/B
-                                    form (slower everywhere): it reads the work list's length back to size its
-                                    chunks, so a render with it synchronises the render's stream on the host and
-                                    cannot be captured in a graph */
+                                    live paths, gi_wf.hip) whatever the scene; same frame bit for bit.  A test
+                                    reference (slower everywhere) */
 #define GI_FLAG_X_MEGA 32u       /* Mode X: the persistent path-state kernel (k_mode_x) whatever the scene */
 #define GI_FLAG_X_SEG 64u        /* Mode X: the segment-synchronous persistent form (k_seg: every loop
                                     iteration one whole path segment per lane).  None of the three form
@@ -134,9 +132,13 @@ typedef struct gi_opts {
     uint64_t* stats;       /* device pointer to GI_STATS_N uint64 counters (GI_FLAG_STATS) */
     /* Mode X progressive passes (ABI 10; both 0: the whole frame at once).  A pass renders samples
      * [sample_begin, sample_end) of the spp-sample frame (spp > 1) and delivers the running estimate
-     * min(sum over samples s < sample_end / sample_end, 1) -- exactly the frame of spp = sample_end,
-     * since the samples' jitter and paths do not depend on spp; the pass with sample_end == spp is
-     * the one-shot frame bit for bit.  Passes continue one frame: they are issued on one scene in
+     * min(sum over samples s < sample_end / sample_end, 1) -- for sample_end > 1 exactly the frame of
+     * spp = sample_end, since the samples' jitter and paths do not depend on spp (a pass ending at
+     * sample 1 holds the JITTERED sample 0 of the spp-sample frame, while a real spp = 1 frame is not
+     * jittered); the pass with sample_end == spp is the one-shot frame bit for bit.  A pass is
+     * accepted when it has been issued: a device error that surfaces later (a failed launch, a
+     * fault) ends the progressive frame -- the next continuation is refused (GI_ERR_DEVICE) and the
+     * frame restarts at sample 0.  Passes continue one frame: they are issued on one scene in
      * order (sample_begin = the previous pass's sample_end, the first at 0) with the same camera,
      * light, size, spp, depth, seed and shard, and no other render of the scene in between; the
      * scene keeps the frame's per-sample radiance rows and work list between them (GI_ERR_ARG
@@ -266,7 +268,9 @@ int gi_scene_x_form(gi_scene* scene, const gi_opts* opts, int32_t* form);
 /* Mode R kernel a render of `scene` with `opts` would run (ABI 10; bench labels, tests): 0 = k_mode_r
  * (one lane per pixel: small scenes, GI_FLAG_R_DFS), 1 = the flat phases (k_rf_walk, k_rf_hit,
  * k_rf_scan, k_rf_reach, k_rf_shade; scenes of more than 4096 entities; their overflowed tiles by
- * k_mode_r_batch), 2 = k_mode_r_batch for the whole frame.  Mode X: 0. */
+ * k_mode_r_batch), 2 = k_mode_r_batch for the whole frame -- also where the flat phases' buffers
+ * could not be allocated for the scene's last frame size (not retried for that size or larger).
+ * Mode X: 0. */
 int gi_scene_r_kernel(gi_scene* scene, const gi_opts* opts, int32_t* kernel);
 
 /* ---- host-side reference octree (no device needed) --------------------------------------------

@@ -28,6 +28,11 @@
 //     8x8 tiles across them (gi_multi, RCCL gather).  Unset: one device, the one current on the
 //     thread that uploads the scene (hipSetDevice by the host app is honoured); if the multi-device
 //     handle cannot be created (no librccl, no peer access) the frame falls back to that device.
+//
+// Failures are reported, not just printed: lastStatus() / lastError() (extensions) hold the last
+// run()'s gi_status -- GI_OK, GI_ERR_CANCELLED after stop(), or the error that left the Image black:
+// a libgi whose ABI differs from this header's (GI_ERR_ABI below), an entity the C-ABI cannot
+// describe (GI_ERR_SCENE), a failed upload or render (the gi_status libgi returned).
 #pragma once
 
 #include <algorithm>
@@ -36,6 +41,7 @@
 #include <cstring>
 #include <functional>
 #include <memory>
+#include <string>
 #include <vector>
 
 #include <glm/glm.hpp>
@@ -46,6 +52,9 @@
 #include "octree.h"   // gi_dropin/octree.h (same directory, searched first)
 #include "gi.h"
 #include "gi_describe.h"
+
+// lastStatus() of a run() refused because the loaded libgi's ABI is not this header's GI_ABI_VERSION
+#define GI_ERR_ABI (-100)
 
 class RayTracer {
   public:
@@ -71,11 +80,16 @@ class RayTracer {
 
     void run(int w, int h) {
         _image = std::make_shared<Image>(w, h);   // raytracer.h:25
+        _status = GI_OK;
+        _error.clear();
         if (!_scene || w <= 0 || h <= 0) return;
         // the reference reads the live octree on every run (raytracer.h:45): the entities are
         // described again and the scene re-uploaded when anything changed (push_back, a material)
         std::vector<gi_entity_desc> ents;
-        if (!gi_dropin::describe_all(_scene->entities(), ents)) return;
+        if (!gi_dropin::describe_all(_scene->entities(), ents)) {
+            report(GI_ERR_SCENE, "an entity of the scene has no gi_entity_desc (gi_describe.h)");
+            return;
+        }
         const double mn[3] = {_scene->min.x, _scene->min.y, _scene->min.z};
         const double mx[3] = {_scene->max.x, _scene->max.y, _scene->max.z};
         const uint64_t hash = gi_dropin::scene_hash(ents, mn, mx);
@@ -116,14 +130,14 @@ class RayTracer {
                     if (_on_pass) _on_pass(_passes, o.sample_end);   // (may stop() the frame)
                 }
             }
-            if (rc != GI_OK && rc != GI_ERR_CANCELLED) std::fprintf(stderr, "gi_render: %s\n", gi_last_error());
+            if (rc != GI_OK) report(rc, rc == GI_ERR_CANCELLED ? "cancelled" : gi_last_error());
             return;
         }
         const int rc = _gpu->multi ? gi_multi_render(_gpu->multi, &cam, light, w, h, &o, nullptr, nullptr, &_cancel,
                                                      &RayTracer::on_band, &band)
                                    : gi_render(_gpu->scene, &cam, light, w, h, &o, nullptr, nullptr, &_cancel,
                                                &RayTracer::on_band, &band);
-        if (rc != GI_OK && rc != GI_ERR_CANCELLED) std::fprintf(stderr, "gi_render: %s\n", gi_last_error());
+        if (rc != GI_OK) report(rc, rc == GI_ERR_CANCELLED ? "cancelled" : gi_last_error());
     }
 
     bool running() const { return _cancel == 0; }
@@ -136,6 +150,11 @@ class RayTracer {
     /// Image, whose RGB888 is its (int)(255*c) quantisation (image.h:14-16).
     void keepRadiance(bool on) { _keep_radiance = on; }
     const std::vector<double>& radiance() const { return _radiance; }
+    /// Extension: the last run()'s outcome -- GI_OK, GI_ERR_CANCELLED (stop()), or the error that
+    /// left the Image (partly) black: GI_ERR_ABI, GI_ERR_SCENE or the gi_status of the failed libgi
+    /// call; lastError() its message.  Errors are also printed to stderr, as before.
+    int lastStatus() const { return _status; }
+    const std::string& lastError() const { return _error; }
     /// Extension (tests): progressive passes the last run() delivered (0 without passes).
     int passesDelivered() const { return _passes; }
     /// Extension (tools, tests): called on the render thread after each delivered progressive pass
@@ -217,9 +236,18 @@ class RayTracer {
         return d;
     }
 
+    void report(int rc, const char* msg) {
+        _status = rc;
+        _error = msg ? msg : "";
+        if (rc != GI_OK && rc != GI_ERR_CANCELLED) std::fprintf(stderr, "gi: %s (status %d)\n", _error.c_str(), rc);
+    }
+
     bool upload(const std::vector<gi_entity_desc>& ents, const double mn[3], const double mx[3], uint64_t hash) {
         if (gi_abi_version() != GI_ABI_VERSION) {   // gi.h's structs must match the loaded libgi
-            std::fprintf(stderr, "gi: libgi ABI %d, built against %d\n", gi_abi_version(), GI_ABI_VERSION);
+            char m[96];
+            std::snprintf(m, sizeof m, "libgi ABI %d, this header's %d: rebuild against the loaded libgi", gi_abi_version(),
+                          GI_ABI_VERSION);
+            report(GI_ERR_ABI, m);
             return false;
         }
         gi_scene_desc sd = {};
@@ -236,8 +264,9 @@ class RayTracer {
             std::fprintf(stderr, "gi_multi_create: %s (rendering on one device)\n", gi_last_error());
             g->multi = nullptr;
         }
-        if (!g->multi && gi_scene_create(&sd, &g->scene) != GI_OK) {
-            std::fprintf(stderr, "gi_scene_create: %s\n", gi_last_error());
+        int rc = GI_OK;
+        if (!g->multi && (rc = gi_scene_create(&sd, &g->scene)) != GI_OK) {
+            report(rc, gi_last_error());
             return false;
         }
         g->hash = hash;
@@ -256,4 +285,6 @@ class RayTracer {
     std::vector<double> _radiance;
     int _passes = 0;
     std::function<void(int, int)> _on_pass;
+    int _status = GI_OK;
+    std::string _error;
 };

@@ -18,6 +18,10 @@
 // (GI_MODE=X GI_SPP=.. GI_DEPTH=.. GI_SEED=.. [GI_PASS=..], read by the drop-in RayTracer's
 // constructor).  DEMO_STOP_AFTER=k stops the frame after k progressive passes (RayTracer::stop from
 // the pass callback, as a Viewer resize would); the demo prints the passes delivered to stderr.
+// Exit status: 0 on a delivered frame (or one stopped by DEMO_STOP_AFTER), 3 when the drop-in
+// RayTracer reports an error (RayTracer::lastStatus(): a libgi of another ABI, a failed upload or
+// render -- the Image would be black), 1/2 on the demo's own input errors.  `dropin_demo --abi`
+// prints the GI_ABI_VERSION it was compiled against (tests refuse a stale build).
 //   dropin_demo <w> <h> <out> [zoo|main|obj:<path>|scn:<path>] [cands|rad]
 #include <cmath>
 #include <cstdio>
@@ -65,6 +69,7 @@ bool read_scn(const std::string& path, ScnScene& sc) {
 }
 
 int main(int argc, char** argv) {
+    if (argc == 2 && std::string(argv[1]) == "--abi") { std::printf("%d\n", GI_ABI_VERSION); return 0; }
     if (argc < 4) { std::fprintf(stderr, "usage: dropin_demo w h out.rgb\n"); return 2; }
     const int w = std::atoi(argv[1]), h = std::atoi(argv[2]);
     ScnScene scn;
@@ -135,6 +140,11 @@ int main(int argc, char** argv) {
     viewer_copy.start();
     viewer_copy.run(w, h);
     std::fprintf(stderr, "passes %d\n", viewer_copy.passesDelivered());
+    if (viewer_copy.lastStatus() != GI_OK && viewer_copy.lastStatus() != GI_ERR_CANCELLED) {
+        std::fprintf(stderr, "dropin_demo: RayTracer::run failed (status %d): %s\n", viewer_copy.lastStatus(),
+                     viewer_copy.lastError().c_str());
+        return 3;
+    }
     std::shared_ptr<Image> img = viewer_copy.getImage();
     if (img->width() != w || img->height() != h) return 1;
     FILE* f = std::fopen(argv[3], "wb");

@@ -1312,8 +1312,11 @@ int gio_render(const char* scn, int w, int h, int mode, int spp, int depth, uint
 // (out[1]) and not traced, as the GPU's classify pass / root-box pretest resolve such samples apart
 // from its `value`.  out: [0] rays (primary + bounce + shadow, resolved ones included), [1] resolved
 // primary samples, [2] pixels, [3] the sum of the pixels' radiance (keeps the work observable).
+// rgb / q (optional, 3 per pixel of the rows, row by row): the pixels as gio_render writes them
+// (fp64 radiance and RGB888) -- the whole-frame / strided-row parity tests and bench.py's check of
+// its own GPU frame.
 int gio_time_rows(const char* scn, int w, int h, int spp, int depth, uint64_t seed, int row0, int stride, int n_rows,
-                  int threads, double* out) {
+                  int threads, double* out, double* rgb, uint8_t* q) {
     Scene s;
     if (!parse(scn, s, false)) return -1;
     if (w <= 0 || h <= 0 || spp < 1 || depth < 1 || stride < 1 || n_rows < 0 || row0 < 0) { g_err = "bad arguments"; return -2; }
@@ -1359,6 +1362,12 @@ int gio_time_rows(const char* scn, int w, int h, int spp, int depth, uint64_t se
             acc[0] = acc[0] + L.x; acc[1] = acc[1] + L.y; acc[2] = acc[2] + L.z;
         }
         sum += acc[0] + acc[1] + acc[2];
+        // the pixel as pixel_mode_x forms it (a resolved sample's +0 left out of acc changes no sum:
+        // acc >= +0 throughout)
+        double col[3];
+        for (int k = 0; k < 3; ++k) col[k] = smin(acc[k] / (double)spp, 1.0);
+        if (rgb) { rgb[3 * i] = col[0]; rgb[3 * i + 1] = col[1]; rgb[3 * i + 2] = col[2]; }
+        if (q) quantize(col, q + 3 * i);
     }
     out[0] = (double)rays;
     out[1] = (double)res;

@@ -33,7 +33,7 @@ int gio_render(const char* scn, int w, int h, int mode, int spp, int depth, uint
 // samples whose ray misses the scene's bounding box are counted apart and not traced.  out[4]: rays,
 // resolved primary samples, pixels, radiance sum.
 int gio_time_rows(const char* scn, int w, int h, int spp, int depth, uint64_t seed, int row0, int stride, int n_rows,
-                  int threads, double* out);
+                  int threads, double* out, double* rgb, uint8_t* q);
 
 // Octree dump in the same text format as `ref_harness tree` (bbox lines, then DFS node lines).
 // Returns the number of bytes needed (excluding NUL); writes at most cap bytes.

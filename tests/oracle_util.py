@@ -53,7 +53,8 @@ def oracle():
         lib.gio_set_accel.argtypes = [ctypes.c_int]
         lib.gio_set_no_shadow.argtypes = [ctypes.c_int]
         lib.gio_time_rows.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                      ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, f64p]
+                                      ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, f64p,
+                                      f64p, ctypes.POINTER(ctypes.c_uint8)]
         _oracle = lib
     return _oracle
 
@@ -79,15 +80,24 @@ def oracle_render(scn: str, w: int, h: int, mode: int = 0, spp: int = 1, depth: 
 
 
 def oracle_time_rows(scn: str, w: int, h: int, spp: int, depth: int, seed: int, row0: int, stride: int, n_rows: int,
-                     threads: int = 0) -> dict:
-    """Mode X over the full-width rows row0 + k*stride (bench.py's cpu_baseline): rays traced,
-    primary samples resolved by the scene-box test (not traced), pixels, radiance sum."""
+                     threads: int = 0, pixels: bool = False) -> dict:
+    """Mode X over the full-width rows row0 + k*stride (bench.py's cpu_baseline; the whole-frame and
+    strided-row parity tests): rays traced, primary samples resolved by the scene-box test (not
+    traced), pixels, radiance sum; with pixels=True also the rows' pixels as gio_render writes them
+    ("rows": the row indices, "rgb": (rows, w, 3) fp64, "q": (rows, w, 3) RGB888)."""
+    rows = [row0 + k * stride for k in range(n_rows) if row0 + k * stride < h]
     out = np.zeros(4)
+    rgb = np.zeros((len(rows), w, 3)) if pixels else None
+    q = np.zeros((len(rows), w, 3), np.uint8) if pixels else None
     lib = oracle()
-    rc = lib.gio_time_rows(scn.encode(), w, h, spp, depth, seed, row0, stride, n_rows, threads, _p(out, ctypes.c_double))
+    rc = lib.gio_time_rows(scn.encode(), w, h, spp, depth, seed, row0, stride, n_rows, threads, _p(out, ctypes.c_double),
+                           _p(rgb, ctypes.c_double) if pixels else None, _p(q, ctypes.c_uint8) if pixels else None)
     if rc != 0:
         raise RuntimeError(f"gio_time_rows failed ({rc}): {lib.gio_last_error().decode()}")
-    return {"rays": int(out[0]), "resolved": int(out[1]), "pixels": int(out[2]), "sum": float(out[3])}
+    r = {"rays": int(out[0]), "resolved": int(out[1]), "pixels": int(out[2]), "sum": float(out[3])}
+    if pixels:
+        r.update(rows=rows, rgb=rgb, q=q)
+    return r
 
 
 def oracle_no_shadow(on: bool) -> None:
@@ -196,6 +206,22 @@ def ref_boxes(recs: np.ndarray) -> np.ndarray:
             f.write(np.ascontiguousarray(recs, "<f8").tobytes())
         subprocess.run([REF_HARNESS, "boxes", rp, op], check=True)
         return np.frombuffer(open(op, "rb").read(), dtype="<i4").copy()
+
+
+def dropin_demo() -> str:
+    """integration/_build/dropin_demo (the reference app's classes + the C++ drop-in headers; built by
+    integration/Makefile where the reference tree exists).  Skips when it was never built; FAILS when
+    it was built against a gi.h of another GI_ABI_VERSION than the tree's (a stale build travelled
+    with the snapshot: it would refuse every render)."""
+    import pytest
+    import re
+    exe = os.path.join(ROOT, "integration", "_build", "dropin_demo")
+    if not os.path.exists(exe):
+        pytest.skip("integration/_build/dropin_demo not built (needs the reference tree)")
+    want = re.search(r"#define GI_ABI_VERSION (\d+)", open(os.path.join(ROOT, "include", "gi.h")).read()).group(1)
+    got = subprocess.run([exe, "--abi"], capture_output=True, text=True, timeout=60).stdout.strip()
+    assert got == want, f"stale {exe}: built against GI_ABI_VERSION {got!r}, the tree's gi.h has {want} (rebuild: make -C integration)"
+    return exe
 
 
 def whole_frame_digest(rgb: np.ndarray, q: np.ndarray) -> dict:

@@ -172,9 +172,7 @@ def test_cpp_dropin_octree_intersect_matches_reference(tmp_path, scene, w, h):
     """include/gi_dropin/octree.h's Octree::intersect(const Ray&) (octree.h:46-68), called from the
     reference app's own classes (integration/dropin_demo.cpp, built where the reference tree
     exists): candidate-list lengths equal the compiled reference's on every pixel's primary ray."""
-    exe = os.path.join(U.ROOT, "integration", "_build", "dropin_demo")
-    if not os.path.exists(exe):
-        pytest.skip("integration/_build/dropin_demo not built (needs the reference tree)")
+    exe = U.dropin_demo()
     out = tmp_path / "c.bin"
     subprocess.run([exe, str(w), str(h), str(out), scene, "cands"], check=True, timeout=120)
     c = np.fromfile(out, np.int32)
@@ -208,3 +206,29 @@ def test_allocation_failure_returns_nomem_not_abort(tmp_path):
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "rc -5 host memory exhausted" in r.stdout, r.stdout
+
+
+def test_cpp_dropin_refuses_other_abi_loudly(tmp_path):
+    """a drop-in build whose gi.h has another GI_ABI_VERSION than the loaded libgi
+    refuses to render AND says so -- RayTracer::lastStatus() == GI_ERR_ABI, dropin_demo exits 3 --
+    instead of leaving a black Image behind a zero exit.  (Built here, where the reference tree
+    exists; the check runs before any device call, so no GPU is needed.)"""
+    if not os.path.isdir("/root/reference/include"):
+        pytest.skip("needs the reference tree to build the demo")
+    hdr = open(HDR).read()
+    m = re.search(r"#define GI_ABI_VERSION (\d+)", hdr)
+    other = tmp_path / "inc"
+    other.mkdir()
+    (other / "gi.h").write_text(hdr.replace(m.group(0), "#define GI_ABI_VERSION %d" % (int(m.group(1)) - 1)))
+    exe = tmp_path / "demo_other_abi"
+    subprocess.run(["make", "-s", "-C", os.path.join(U.ROOT, "integration"), f"OUT={exe}", f"EXTRA_INC=-I{other}"],
+                   check=True, timeout=300)
+    env = dict(os.environ, QT_QPA_PLATFORM="offscreen",
+               LD_LIBRARY_PATH=os.path.join(U.ROOT, "2019global_amd") + ":" + os.environ.get("LD_LIBRARY_PATH", ""))
+    assert subprocess.run([str(exe), "--abi"], capture_output=True, text=True, check=True, env=env).stdout.strip() == \
+        str(int(m.group(1)) - 1)
+    r = subprocess.run([str(exe), "32", "32", str(tmp_path / "f.rgb")], capture_output=True, text=True, env=env,
+                       timeout=120)
+    assert r.returncode == 3, (r.returncode, r.stderr)
+    assert "ABI" in r.stderr and "status -100" in r.stderr, r.stderr
+    assert not (tmp_path / "f.rgb").exists()

@@ -374,10 +374,23 @@ def test_mode_x_multi_sample_units_bit_exact(torch_cuda, tmp_path):
     assert U.bits_equal(k1[win[1]:win[3], win[0]:win[2]].reshape(-1, 3), o["rgb"]).all()
 
 
-def test_mode_x_c3_config_windows_and_shards(torch_cuda):
+def _check_rows(sc, f, f8, w, h, spp, depth, seed, row0=0, stride=1, what=""):
+    """The device frame's full-width rows row0 + k*stride against the oracle (gio_time_rows, 16 host
+    threads: the GPU box's CPU share), bit for bit in fp64 and RGB888; names the first differing rows."""
+    o = U.oracle_time_rows(sc.to_scn(), w, h, spp, depth, seed, row0, stride, h, threads=16, pixels=True)
+    g, g8 = f[o["rows"]], f8[o["rows"]]
+    same = U.bits_equal(g, o["rgb"]).all(2)
+    bad = [o["rows"][i] for i in np.nonzero(~same.all(1))[0]]
+    assert not bad, f"{what}: {int((~same).sum())} pixels in {len(bad)} rows differ from the oracle (rows {bad[:8]})"
+    assert (g8 == o["q"]).all(), f"{what}: RGB888"
+    return o
+
+
+def test_mode_x_c3_config_whole_frame_and_shards(torch_cuda):
     """The bench's own workload: C3 = Cornell 1920x1080, depth 8, 64 spp (single-sample work units by
-    default, GI_X_MAX_RUN = 1, for the whole frame and for an 8-way shard of it).  Three windows
-    against the oracle, and the 8-shard frame against the whole frame bit for bit."""
+    default, GI_X_MAX_RUN = 1, for the whole frame and for an 8-way shard of it).  EVERY pixel against
+    the oracle bit for bit (round 5 compared three windows, 768 pixels), and the
+    8-shard frame against the whole frame bit for bit."""
     torch = torch_cuda
     sc = S.cornell_scene()
     d = dev_scene("cornell")
@@ -387,11 +400,9 @@ def test_mode_x_c3_config_windows_and_shards(torch_cuda):
     d.render_device(cam_of(sc), sc.light, w, h, full.data_ptr(), full8.data_ptr(), **kw)
     torch.cuda.synchronize()
     f = full.cpu().numpy().reshape(h, w, 3)
-    for win in ((700, 1000, 716, 1016), (1100, 800, 1116, 816), (1180, 1040, 1196, 1056)):   # edge, wall, floor
-        o = U.oracle_render(sc.to_scn(), w, h, window=win, **{k: v for k, v in kw.items() if k != "mode"}, mode=1)
-        g = f[win[1]:win[3], win[0]:win[2]].reshape(-1, 3)
-        assert (o["hit"] >= 0).any()
-        assert U.bits_equal(g, o["rgb"]).all(), f"window {win}"
+    f8 = full8.cpu().numpy().reshape(h, w, 3)
+    o = _check_rows(sc, f, f8, w, h, 64, 8, 2019, what="C3 whole frame")
+    assert o["pixels"] == w * h and o["rays"] > 100_000_000
     n = 8
     per = gi.shard_tiles(w, h, n) * gi.TILE * gi.TILE * 3
     packed = torch.zeros(n * per, dtype=torch.float64, device="cuda")
@@ -544,9 +555,7 @@ def test_cpp_dropin_raytracer_matches_reference_run(torch_cuda, tmp_path):
     """The reference app's own classes + include/gi_dropin/raytracer.h (built by integration/Makefile
     where the reference tree exists) give RayTracer::run's frame of the main.cpp scene."""
     import subprocess
-    exe = os.path.join(U.ROOT, "integration", "_build", "dropin_demo")
-    if not os.path.exists(exe):
-        pytest.skip("integration/_build/dropin_demo not built (needs the reference tree)")
+    exe = U.dropin_demo()
     out = tmp_path / "f.rgb"
     env = dict(os.environ, QT_QPA_PLATFORM="offscreen")
     subprocess.run([exe, "200", "200", str(out)], check=True, env=env, timeout=120)
@@ -570,9 +579,7 @@ def test_cpp_dropin_raytracer_mode_x_opt_in(torch_cuda, tmp_path, band_env):
     opt-in the same binary renders the reference's Mode R frame (the default is unchanged).  Also
     over two tile shards (GI_DEVICES=0,0: gi_multi)."""
     import subprocess
-    exe = os.path.join(U.ROOT, "integration", "_build", "dropin_demo")
-    if not os.path.exists(exe):
-        pytest.skip("integration/_build/dropin_demo not built (needs the reference tree)")
+    exe = U.dropin_demo()
     sc = S.cornell_scene()
     scn = tmp_path / "c.scn"
     scn.write_text(sc.to_scn())
@@ -604,9 +611,7 @@ def test_cpp_dropin_progressive_passes(torch_cuda, tmp_path):
     does), the image holds that pass -- exactly the 2-sample frame of the oracle; run to the end, the
     frame is the 8-sample oracle frame bit for bit, after 4 passes."""
     import subprocess
-    exe = os.path.join(U.ROOT, "integration", "_build", "dropin_demo")
-    if not os.path.exists(exe):
-        pytest.skip("integration/_build/dropin_demo not built (needs the reference tree)")
+    exe = U.dropin_demo()
     sc = S.cornell_scene()
     scn = tmp_path / "c.scn"
     scn.write_text(sc.to_scn())
@@ -773,26 +778,25 @@ def _check_windows(sc, frame, frame8, w, h, wins, spp, depth, seed, min_hit=None
     return hits
 
 
-def test_mode_x_c4_config_windows(torch_cuda):
+def test_mode_x_c4_config_whole_frame(torch_cuda):
     """BASELINE configs[3] (C4): the 100k-triangle soup at 1920x1080, depth 8, Mode X, whole frame on
-    the device; windows against the oracle bit for bit -- the soup's centre (the frame's longest
-    paths: pixel (960, 960) looks along +x through the soup's core, raytracer.h:26-30 with A.12),
-    its left edge, a mid region, its lower right, and background."""
+    the device; EVERY pixel against the oracle bit for bit, plus a window at the
+    soup's centre (the frame's longest paths: pixel (960, 960) looks along +x through the soup's core,
+    raytracer.h:26-30 with A.12) that must hold hits."""
     torch = torch_cuda
     sc = S.soup_scene(100000)
     w, h, kw = 1920, 1080, dict(mode=gi.MODE_X, spp=1, depth=8, seed=2019)
     rgb, rgb8 = _render_frame_device(torch, "soup100000", w, h, **kw)
     f = rgb.cpu().numpy().reshape(h, w, 3)
     f8 = rgb8.cpu().numpy().reshape(h, w, 3)
-    wins = ((952, 952, 968, 968), (704, 952, 720, 968), (1100, 1000, 1116, 1016), (1180, 1060, 1196, 1076),
-            (200, 100, 216, 116))
-    _check_windows(sc, f, f8, w, h, wins, 1, 8, 2019, min_hit=600)
+    _check_rows(sc, f, f8, w, h, 1, 8, 2019, what="C4 whole frame")
+    _check_windows(sc, f, f8, w, h, ((952, 952, 968, 968),), 1, 8, 2019, min_hit=200)
     assert float(f.max()) <= 1.0 and float(f.min()) >= 0.0
 
 
-def test_mode_x_c5_config_windows_and_8_shards(torch_cuda):
+def test_mode_x_c5_config_rows_and_8_shards(torch_cuda):
     """BASELINE configs[4] (C5): the 100k soup at 3840x2160, depth 8, 256 spp -- the whole frame on
-    one device, windows against the oracle bit for bit, and the 8-way tile-sharded frame (the
+    one device, every 16th row against the oracle bit for bit, and the 8-way tile-sharded frame (the
     config's 8-GPU split, rendered shard by shard here) equal to the single frame bit for bit."""
     torch = torch_cuda
     sc = S.soup_scene(100000)
@@ -801,8 +805,10 @@ def test_mode_x_c5_config_windows_and_8_shards(torch_cuda):
     full, full8 = _render_frame_device(torch, "soup100000", w, h, **kw)
     f = full.cpu().numpy().reshape(h, w, 3)
     f8 = full8.cpu().numpy().reshape(h, w, 3)
-    wins = ((1916, 1916, 1924, 1924), (1696, 1916, 1704, 1924), (2096, 2096, 2104, 2104), (1000, 400, 1008, 408))
-    _check_windows(sc, f, f8, w, h, wins, 256, 8, 2019, min_hit=150)
+    # every 16th full-width row (135 rows = 518,400 pixels x 256 spp; rows 1908 and 1924 cross the
+    # soup's core), bit for bit against the oracle (round 5 compared 256 pixels)
+    _check_rows(sc, f, f8, w, h, 256, 8, 2019, row0=4, stride=16, what="C5 strided rows")
+    _check_windows(sc, f, f8, w, h, ((1916, 1916, 1924, 1924),), 256, 8, 2019, min_hit=50)
     n = 8
     per = gi.shard_tiles(w, h, n) * gi.TILE * gi.TILE * 3
     packed = torch.zeros(n * per, dtype=torch.float64, device="cuda")
@@ -884,9 +890,7 @@ def test_cpp_dropin_multi_device_matches_reference_run(torch_cuda, tmp_path):
     """The drop-in RayTracer with GI_DEVICES=0,0 (two tile shards through gi_multi) still gives
     RayTracer::run's frame of the main.cpp scene."""
     import subprocess
-    exe = os.path.join(U.ROOT, "integration", "_build", "dropin_demo")
-    if not os.path.exists(exe):
-        pytest.skip("integration/_build/dropin_demo not built (needs the reference tree)")
+    exe = U.dropin_demo()
     out = tmp_path / "f.rgb"
     env = dict(os.environ, QT_QPA_PLATFORM="offscreen", GI_DEVICES="0,0")
     subprocess.run([exe, "200", "200", str(out)], check=True, env=env, timeout=120)
@@ -1137,3 +1141,51 @@ def test_mode_r_kernels_frame_identical(torch_cuda, tmp_path):
     assert frames["flat"]["stats"][gi.STAT_R_PAIRS] > 0
     print("R-C4 pairs", int(frames["flat"]["stats"][gi.STAT_R_PAIRS]), "overflowed tiles without a pool",
           int(frames["flat_overflow"]["stats"][gi.STAT_R_OVF_TILES]), "of", tiles)
+
+
+def _strip_scene(n=5000, seed=6, size=0.03):
+    """n small triangles in a thin vertical strip that a 2048-wide frame sees in ONE 8-pixel tile
+    column (tiles X, X + 256, X + 512, ... at 256 tiles per row): k_rf_reach's chunks of 64 hits then
+    hold tiles whose indices differ by multiples of 256, the case that broke round 5's memo tag
+    (ADVICE r05, high)."""
+    rng = np.random.default_rng(seed)
+    s = S.Scene(entities=[], name="strip")
+    # pixel column x looks at y = 20.48 - 0.02 x on the plane x = 0 (raytracer.h:26-30, 41-43 at
+    # w = 2048): tile column 128 covers y in (-0.14, 0.02]; rows reach z in [-1.28, 20.48]
+    c = np.stack([rng.uniform(-2.0, 2.0, n), rng.uniform(-0.13, 0.01, n), rng.uniform(-1.0, 20.0, n)], 1)
+    for k in range(n):
+        v = c[k] + rng.uniform(-size, size, (3, 3))
+        s.imp_triangle(tuple(v[0]), tuple(v[1]), tuple(v[2]), tuple(rng.integers(0, 2, 3)))
+    return s
+
+
+@pytest.mark.parametrize("size", [0.03, 0.3])
+def test_mode_r_flat_reach_sparse_tile_column(torch_cuda, tmp_path, size):
+    """Mode R's flat phases (the default above 4096 entities) on a scene hit only in one tile column of
+    a 2048-wide frame: every pixel equals k_mode_r's (GI_R_FLAT=0, a child process) bit for bit and the
+    strip's pixels equal the oracle's (within 1e-5 relative, RGB888 exact).  The reach phase's node-test
+    memo must never hand one tile's result to a tile 256 (or any multiple) further on."""
+    import subprocess
+    import sys
+    sc = _strip_scene(size=size)   # (0.3: triangles over several tile columns and octree leaves)
+    w, h = 2048, 1088
+    d = gi.DeviceScene.from_scene(sc)
+    assert d.r_kernel() == "k_rf_walk"
+    rgb, rgb8 = d.render(cam_of(sc), sc.light, w, h)
+    scn = tmp_path / "strip.scn"
+    scn.write_text(sc.to_scn())
+    out = tmp_path / "r0.npy"
+    code = ("import sys, numpy as np; sys.path.insert(0, %r); sys.path.insert(0, %r); import oracle_util as U; "
+            "gi = U.pkg(); S = U.scenes(); sc = S.parse_scn(open(%r).read()); d = gi.DeviceScene.from_scene(sc); "
+            "np.save(%r, d.render(gi.Camera(sc.cam_pos, sc.cam_look, sc.focal), sc.light, %d, %d)[0])"
+            ) % (U.ROOT, os.path.join(U.ROOT, "tests"), str(scn), str(out), w, h)
+    subprocess.run([sys.executable, "-c", code], check=True, timeout=300, env=dict(os.environ, GI_R_FLAT="0"))
+    ref = np.load(out)
+    same = U.bits_equal(rgb, ref).all(2)
+    assert same.all(), f"{int((~same).sum())} pixels differ from k_mode_r (rows {np.nonzero(~same.all(1))[0][:8]})"
+    win = (1016, 0, 1040, h)
+    o = U.oracle_render(sc.to_scn(), w, h, window=win, threads=16)
+    g = rgb[:, win[0]:win[2]].reshape(-1, 3)
+    assert (o["hit"] >= 0).sum() > 1000
+    assert_rel(g, o["rgb"], "strip window")
+    assert (rgb8[:, win[0]:win[2]].reshape(-1, 3) == o["q"]).all()

@@ -211,3 +211,18 @@ def test_reduced_mode_x_anchored_to_reference(name):
     ent, tex, far, exact, far_max = U.anchor_counts(o["rgb"], o["hit"], o["uv"], z)
     assert (ent, tex, far, exact) == U.ANCHOR[name]
     assert far_max <= U.ANCHOR_ABS
+
+
+@pytest.mark.parametrize("scene,spp", [("cornell", 3), ("soup1000", 2), ("main", 1)])
+def test_time_rows_pixels_equal_render(scene, spp):
+    """gio_time_rows' per-pixel output (the whole-frame / strided-row GPU parity tests and bench.py's
+    self-check compare against it) is gio_render's Mode X frame on those rows, bit for bit -- the
+    background samples it resolves by its scene-box test add exactly +0."""
+    sc = S.named_scene(scene)
+    w, h, depth = 48, 40, 5
+    full = U.oracle_render(sc.to_scn(), w, h, mode=1, spp=spp, depth=depth, seed=13)
+    r = U.oracle_time_rows(sc.to_scn(), w, h, spp, depth, 13, 3, 7, 100, pixels=True)
+    assert r["rows"] == list(range(3, h, 7))
+    f = full["rgb"].reshape(h, w, 3)[r["rows"]]
+    assert U.bits_equal(r["rgb"], f).all()
+    assert (r["q"] == full["q"].reshape(h, w, 3)[r["rows"]]).all()
