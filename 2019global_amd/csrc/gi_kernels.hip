@@ -2276,6 +2276,7 @@ hipError_t launch_wf(const DevScene& sc, int kv, size_t lds_bytes, int resident,
                      hipEvent_t ev_begin, hipEvent_t ev_end);
 hipError_t wf_occupancy(const DevScene& sc, int kv, size_t lds_bytes, int form, int* per_cu);
 size_t wf_slot_bytes();
+size_t wf_scene_lds_bytes(const DevScene& sc);
 
 #ifndef GI_WF_MAX_DEPTH
 #define GI_WF_MAX_DEPTH 64   // the wavefront form launches once per bounce: deeper paths run k_mode_x
@@ -2334,7 +2335,7 @@ hipError_t x_launch_config(const DevScene& sc, int device, XLaunchCfg& cfg) {
         64 * kWavesPerBlock, cfg.lds_bytes);
     if (e != hipSuccess) return e;
     cfg.resident = std::max(1, cus) * std::max(1, per_cu);
-    cfg.wf_lds_bytes = (lds ? (size_t)sc.x_lds_bytes : 16 * 256 * sizeof(int)) + wf_slot_bytes();
+    cfg.wf_lds_bytes = (lds ? wf_scene_lds_bytes(sc) : 16 * 256 * sizeof(int)) + wf_slot_bytes();
     e = wf_occupancy(sc, cfg.kv, cfg.wf_lds_bytes, 1, &per_cu);
     if (e != hipSuccess) return e;
     cfg.wf_resident = std::max(1, cus) * std::max(1, per_cu);

@@ -48,6 +48,7 @@ constexpr long long kWfTile = 8;   // pixel tiles are 8 x 8 (GI_TILE)
 // LDS-resident scenes test leaf records two at a time (PAIR: two interleaved fp64 chains) and their
 // node slab tests issue the 12 loads at once (round 5: C3 4.90 -> 4.81 ms against axis by axis)
 constexpr size_t kWfSlotBytes = 9 * 256 * sizeof(double);
+
 // a path's identity where the shading needs it: RNG key, sample, bounce
 struct PathId {
     uint64_t key;
@@ -657,6 +658,10 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
 
 // dynamic LDS of the bounce kernel beyond the scene / level stack: the per-lane path slots
 size_t wf_slot_bytes() { return kWfSlotBytes; }
+// the scene's share of that LDS (LDS-resident scenes): the staged records (entity records included:
+// read from global memory by the shading instead, C3 4.65 -> 4.69 ms, and 5 waves per SIMD with them
+// there, 96 VGPRs and 120 B of scratch, 4.79 ms; profiles/r06_ab.txt)
+size_t wf_scene_lds_bytes(const DevScene& sc) { return (size_t)sc.x_lds_bytes; }
 
 // The kernel variant for a scene: f(LDS, W4, SH, TRI, CN) with each a std::integral_constant<bool>
 // (kv: 2 * LDS-resident + light-shading, XLaunchCfg::kv)
