@@ -320,7 +320,7 @@ GI_HD void mx_disk(double u1, double u2, double& dx, double& dy, double& r2) {
     const double q = num / r;
     double sn, cs;
     mx_sincos_q(QPI * q, sn, cs);
-    const bool zero = a == 0.0 && b == 0.0;
+    const bool zero = (a == 0.0) & (b == 0.0);
     dx = zero ? 0.0 : r * (ax ? cs : sn);
     dy = zero ? 0.0 : r * (ax ? sn : cs);
     r2 = zero ? 0.0 : r * r;
@@ -333,8 +333,9 @@ GI_HD V3 texel(V3 color, int32_t u, int32_t v) {
     int f = (u % 32) * 32 + (v % 32);
     if (f < 0 || f >= 1024) f = ((f % 1024) + 1024) % 1024;
     const int i = f >> 5, j = f & 31;
-    if ((i <= 16 && j <= 16) || (i > 16 && j > 16)) return v3(1, 1, 1);
-    return v3((double)x86_trunc(color.x), (double)x86_trunc(color.y), (double)x86_trunc(color.z));
+    const bool white = ((i <= 16) & (j <= 16)) | ((i > 16) & (j > 16));   // (a select, not a branch)
+    const V3 c = v3((double)x86_trunc(color.x), (double)x86_trunc(color.y), (double)x86_trunc(color.z));
+    return white ? v3(1, 1, 1) : c;
 }
 
 // Image::setPixel quantisation (image.h:14-16): (int)(255*c); an out-of-range channel makes the

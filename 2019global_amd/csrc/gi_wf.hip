@@ -342,7 +342,7 @@ __device__ __forceinline__ bool x_segment(const DevScene& sc, const WFView& v, c
         ++nrays;   // the shadow ray
         const XPrim& p = v.XP[best];   // the facing normal (after the shadow ray: fewer live values)
         V3 N = (TRI || p.kind == 0) ? ld3(p.n) : normalize(P - ld3(p.a));
-        if (!(dot(d, N) < 0)) N = -N;
+        N = dot(d, N) < 0 ? N : -N;
         const REnt& e = v.EN[p.ent];
         int32_t tu, tv;
         x_texcoord<TRI>(sc, e, P, tu, tv);
@@ -367,7 +367,7 @@ __device__ __forceinline__ bool x_segment(const DevScene& sc, const WFView& v, c
                 cont = true;
             } else {
                 T = vmul(T, tc * 0.5);
-                if (!(T.x == 0.0 && T.y == 0.0 && T.z == 0.0)) {
+                if (!((T.x == 0.0) & (T.y == 0.0) & (T.z == 0.0))) {
                     double sx, sy, r2;   // concentric disk + Malley
                     mx_disk(mx_u01k(key, smp, b, 2), mx_u01k(key, smp, b, 3), sx, sy, r2);
                     const double sz = gsqrt(1.0 - r2);

@@ -54,13 +54,12 @@ def main():
                           "wave_iterations": st[gi.STAT_X_ITERS], "lane_trav_steps": st[gi.STAT_X_TRAV],
                           "handler_runs": st[gi.STAT_X_HANDLE], "nodes": st[gi.STAT_NODES], "prims": st[gi.STAT_PRIMS],
                           "clk_per_iter": round(st[gi.STAT_X_CYC_ALL] / max(1, st[gi.STAT_X_ITERS]), 1),
-                          # GI_X_TAILPROBE builds (GI_LIB=...libgi_tailprobe.so): the longest drain after a
-                          # wave first finds the block counter exhausted, and the longest wave life
-                          "probe": {"exhaust_max_avg_ms": (st[16] / 1e5, st[17] / 1e5 / max(1, st[23])),
-                                    "t1_max_avg_ms": (st[18] / 1e5, st[19] / 1e5 / max(1, st[23])),
-                                    "t2_max_avg_ms": (st[20] / 1e5, st[21] / 1e5 / max(1, st[23])),
-                                    "life_avg_ms": st[22] / 1e5 / max(1, st[23]), "waves": st[23],
-                                    "iters_after_exhaust": st[24], "of_those_le_t1": st[25]},
+                          # GI_X_STEPPROBE builds (GI_LIB=...libgi_stepprobe.so): the wave clock of the
+                          # UL traversal steps by part -- pop + load round trip, leaf tests, node test,
+                          # climb / prefetch / restart -- per step
+                          "step_probe": {"steps": st[20],
+                                         "clk_per_step": {k: round(st[i] / max(1, st[20]), 1) for k, i in
+                                                          (("load", 16), ("leaf", 17), ("node", 18), ("climb", 19))}},
                           "clk_share": {k: round(st[i] / max(1, st[gi.STAT_X_CYC_ALL]), 3) for k, i in
                                         (("trav", gi.STAT_X_CYC_TRAV), ("shade", gi.STAT_X_CYC_HIT),
                                          ("next", gi.STAT_X_CYC_NEXT))}}), flush=True)
