@@ -104,9 +104,17 @@ GI_HD bool tri_hit(V3 p1, V3 p2, V3 p3, V3 n, V3 pos, const float* e1f, const fl
     const V3 right = o - pos;
     const float solz = i20 * (float)right.x + i21 * (float)right.y + i22 * (float)right.z;
     const V3 point = o + (double)solz * d;
-    const V3 d1 = normalize(cross(p1 - point, p2 - point));
-    const V3 d2 = normalize(cross(p2 - point, p3 - point));
-    const V3 d3 = normalize(cross(p3 - point, p1 - point));
+    const V3 c1 = cross(p1 - point, p2 - point), c2 = cross(p2 - point, p3 - point), c3 = cross(p3 - point, p1 - point);
+    // Exact-safe early rejection (no normalisation): acceptance below needs |d1 - d2|^2 < 1e-3 and
+    // |d2 - d3|^2 < 1e-3, i.e. d1.d2 and d2.d3 > 0.9995, or a sub-normal shorter than 1e-3.  With every
+    // |c_k| > 1e-100 the normalised d_k have length ~1 (no short one), and c1.c2 <= 0 or c2.c3 <= 0
+    // (rounding errors ~1e-16 |c_i||c_j|) puts the pair ~90 degrees or more apart: the test below would
+    // reject too.  NaN / inf components fail the length guard or the comparison and take the full test.
+    const double n1 = dot(c1, c1), n2 = dot(c2, c2), n3 = dot(c3, c3);
+    if ((n1 > 1e-200) & (n2 > 1e-200) & (n3 > 1e-200) & ((dot(c1, c2) <= 0.0) | (dot(c2, c3) <= 0.0))) return false;
+    const V3 d1 = normalize(c1);
+    const V3 d2 = normalize(c2);
+    const V3 d3 = normalize(c3);
     // glm::length(d_k) < 1e-3 branches (:201-230): a normalised vector has length ~1, inf or NaN;
     // test the squared length first so the sqrt only runs when the branch can fire.
     const double q1 = dot(d1, d1), q2 = dot(d2, d2), q3 = dot(d3, d3);

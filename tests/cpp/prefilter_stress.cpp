@@ -16,6 +16,35 @@ static bool raw(V3 p1, V3 p2, V3 p3, V3 o, V3 d) {
     V3 P, N;
     return tri_hit(p1, p2, p3, n, pos, e1f, e2f, o, d, P, N);
 }
+// tri_hit without its early rejection (the reference's acceptance test evaluated in full, as round 5
+// shipped it): the product's early rejection of unnormalised sub-normals must never change a result
+static bool full(V3 p1, V3 p2, V3 p3, V3 o, V3 d) {
+    const V3 e1 = p2 - p1, e2 = p3 - p1;
+    const V3 n = normalize(cross(e1, e2));
+    const V3 pos = 0.5 * (0.5 * (p1 + p2) + p3);
+    const float e1f[3] = {(float)e1.x, (float)e1.y, (float)e1.z};
+    const float e2f[3] = {(float)e2.x, (float)e2.y, (float)e2.z};
+    if (dot(n, d) == 0) return false;
+    const float m00 = e1f[0], m01 = e2f[0], m02 = (float)(-d.x);
+    const float m10 = e1f[1], m11 = e2f[1], m12 = (float)(-d.y);
+    const float m20 = e1f[2], m21 = e2f[2], m22 = (float)(-d.z);
+    const float det = m00 * (m11 * m22 - m21 * m12) - m10 * (m01 * m22 - m21 * m02) + m20 * (m01 * m12 - m11 * m02);
+    const float ood = 1.0f / det;
+    const float i20 = (m10 * m21 - m20 * m11) * ood;
+    const float i21 = (-(m00 * m21 - m20 * m01)) * ood;
+    const float i22 = (m00 * m11 - m10 * m01) * ood;
+    const V3 right = o - pos;
+    const float solz = i20 * (float)right.x + i21 * (float)right.y + i22 * (float)right.z;
+    const V3 point = o + (double)solz * d;
+    const V3 d1 = normalize(cross(p1 - point, p2 - point));
+    const V3 d2 = normalize(cross(p2 - point, p3 - point));
+    const V3 d3 = normalize(cross(p3 - point, p1 - point));
+    const double q1 = dot(d1, d1), q2 = dot(d2, d2), q3 = dot(d3, d3);
+    const bool short_d = (q1 < 1e-5 && gsqrt(q1) < 1.0e-3) || (q2 < 1e-5 && gsqrt(q2) < 1.0e-3) ||
+                         (q3 < 1e-5 && gsqrt(q3) < 1.0e-3);
+    const bool inside = sq3(d1 - d2) < 1.0e-3 && sq3(d2 - d3) < 1.0e-3;
+    return short_d || inside;
+}
 int main(int argc, char** argv) {
     std::mt19937_64 g(1);
     std::uniform_real_distribution<double> U(-1, 1);
@@ -34,8 +63,11 @@ int main(int argc, char** argv) {
         else if (mode == 2) tgt = p1 + (p2 - p1) * a + v3(U(g), U(g), U(g)) * (sc * 1e-3);   // near an edge
         else tgt = v3(U(g), U(g), U(g)) * (sc * 2);                           // anywhere
         V3 d = normalize(tgt - o);
-        bool r = raw(p1, p2, p3, o, d), f = tri_hit_corners(p1, p2, p3, o, d);
-        ++n; hits += r; if (r != f) { ++bad; if (bad < 5) printf("mismatch it=%ld mode=%d raw=%d\n", it, mode, r); }
+        bool r = raw(p1, p2, p3, o, d), f = tri_hit_corners(p1, p2, p3, o, d), u = full(p1, p2, p3, o, d);
+        // spurious ExpBox faces (A.4): the third corner reflected through the origin
+        bool rs = raw(p1, p2, -p3, o, d), us = full(p1, p2, -p3, o, d);
+        ++n; hits += r;
+        if (r != f || r != u || rs != us) { ++bad; if (bad < 5) printf("mismatch it=%ld mode=%d raw=%d full=%d\n", it, mode, r, u); }
         if (mode == 2) near += r;
     }
     printf("cases %ld raw hits %ld near-edge hits %ld mismatches %ld\n", n, hits, near, bad);
