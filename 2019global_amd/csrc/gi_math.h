@@ -165,13 +165,16 @@ GI_HD bool tri_hit_corners(V3 p1, V3 p2, V3 p3, V3 o, V3 d) {
 GI_HD bool box_hit(V3 mn, V3 mx, V3 o, V3 d) {
     const V3 dlb = mn, drb = v3(mx.x, mn.y, mn.z), dlt = v3(mn.x, mx.y, mn.z), drt = v3(mx.x, mx.y, mn.z);
     const V3 ulb = v3(mn.x, mn.y, mx.z), urb = v3(mx.x, mn.y, mx.z), ult = v3(mn.x, mx.y, mx.z), urt = mx;
-    // faces in ExpBox::faces order (entities.h:400-405); || short-circuits like an OR of bools
-    return tri_hit_corners(dlb, urb, ulb, o, d) || tri_hit_corners(dlb, urb, -ulb, o, d) ||
-           tri_hit_corners(dlb, ult, dlt, o, d) || tri_hit_corners(dlb, ult, -dlt, o, d) ||
-           tri_hit_corners(dlb, drt, dlt, o, d) || tri_hit_corners(dlb, drt, -dlt, o, d) ||
-           tri_hit_corners(urt, ulb, ult, o, d) || tri_hit_corners(urt, ulb, -ult, o, d) ||
-           tri_hit_corners(urt, drb, drt, o, d) || tri_hit_corners(urt, drb, -drt, o, d) ||
-           tri_hit_corners(urt, dlt, drt, o, d) || tri_hit_corners(urt, dlt, -drt, o, d);
+    // the OR of the 12 face tests (ExpBox::faces, entities.h:400-405; || short-circuits like an OR of
+    // bools, and the tests have no side effects, so any order gives the same answer)
+    // the spurious faces first (A.4: p4 = -p3, triangles through the box's mirror image): they accept
+    // most of the rays that pass a node test, so a passing test ends sooner (R-C3 -5%, R-C4 +-0)
+    return tri_hit_corners(dlb, urb, -ulb, o, d) || tri_hit_corners(dlb, ult, -dlt, o, d) ||
+           tri_hit_corners(dlb, drt, -dlt, o, d) || tri_hit_corners(urt, ulb, -ult, o, d) ||
+           tri_hit_corners(urt, drb, -drt, o, d) || tri_hit_corners(urt, dlt, -drt, o, d) ||
+           tri_hit_corners(dlb, urb, ulb, o, d) || tri_hit_corners(dlb, ult, dlt, o, d) ||
+           tri_hit_corners(dlb, drt, dlt, o, d) || tri_hit_corners(urt, ulb, ult, o, d) ||
+           tri_hit_corners(urt, drb, drt, o, d) || tri_hit_corners(urt, dlt, drt, o, d);
 }
 
 // ImpSphere::intersect (entities.h:53-96): the quadratic in the dominant-axis parameterisation
