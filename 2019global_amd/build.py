@@ -82,8 +82,10 @@ def build(verbose: bool = False, force: bool = False, variant: str = "", hip_def
         src = os.path.join(CSRC, s)
         obj = os.path.join(objdir, s + (f".{variant}" if variant else "") + ".o")
         if force or _stale(obj, [src] + hdrs):
+            # (A/B variants only: GI_VARIANT_FLAGS adds code-generation flags, e.g. -mllvm scheduler options)
+            extra = os.environ.get("GI_VARIANT_FLAGS", "").split() if variant else []
             cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-Wshadow", *COMMON, *[f"-D{d}" for d in hip_defines],
-                   "-munsafe-fp-atomics", "-c", src, "-o", obj]
+                   *extra, "-munsafe-fp-atomics", "-c", src, "-o", obj]
             if verbose:
                 print(" ".join(cmd), flush=True)
             jobs.append((cmd, subprocess.Popen(cmd)))

@@ -1221,9 +1221,6 @@ enum : int { PH_CLOSEST = 0, PH_SHADOW = 1, PH_NEED = 2, PH_START = 3, PH_DEAD =
 #define GI_X_MIN_WAVES_LDS 4   // LDS-resident scenes (<= 128 VGPRs; the few spills sit in the handler)
 #endif
 
-#ifndef GI_X_STEPPROBE
-#define GI_X_STEPPROBE 0   // (measurement build) k_mode_x STATS launches time the parts of each UL step
-#endif
 struct XCounters {
     uint64_t rays = 0, nodes = 0, prims = 0, px = 0, res = 0;   // res: samples resolved without traversal
     uint64_t iters = 0, trav = 0, handle = 0, hlanes = 0, hclose = 0, hshadow = 0;   // wave-level (lane 0)
@@ -1235,10 +1232,6 @@ struct XCounters {
     // divergence profile (wave-level, lane 0): loop iterations in which some lane ran a node test /
     // a leaf test / an inline bounce restart / a handler start-loop pass, and the lanes that did
     uint64_t it_node = 0, ln_node = 0, it_leaf = 0, ln_leaf = 0, it_rs = 0, ln_rs = 0, it_st = 0, ln_st = 0;
-#if GI_X_STEPPROBE
-    // (measurement build, STATS launches, UL steps: the wave's clock in each part of a traversal step)
-    uint64_t pr_load = 0, pr_leaf = 0, pr_node = 0, pr_climb = 0, pr_steps = 0;
-#endif
 };
 
 // Mode X work list (k_x_classify -> k_mode_x -> k_x_reduce).  A pixel whose every jittered primary
@@ -1551,22 +1544,7 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                     ur.q[2] = qb[2];
                     ur.q[3] = qb[3];
                 }
-#if GI_X_STEPPROBE
-                uint64_t pq0 = 0, pq1 = 0, pq2 = 0;
-                if (STATS) {
-                    __builtin_amdgcn_s_waitcnt(0);   // (probe: the step's load round trip ends here)
-                    pq0 = clock64();
-                    cnt.pr_load += pq0 - t0;
-                    ++cnt.pr_steps;
-                }
-#endif
                 if (ch < 0) leaf_test_from(ur, H + ~ch, cntl);
-#if GI_X_STEPPROBE
-                if (STATS) {
-                    pq1 = clock64();
-                    cnt.pr_leaf += pq1 - pq0;
-                }
-#endif
                 if (ch >= 0) {
                     ++nnode;
                     const uint32_t cm = children_mask_q(ur.q[0], ur.q[1], ur.q[2], ur.q[3], of, ivf, tbest_f, dmask);
@@ -1577,13 +1555,6 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
                         if (NST) nst[level * 256] = ch;
                     }
                 }
-#if GI_X_STEPPROBE
-                if (STATS) {
-                    pq2 = clock64();
-                    cnt.pr_node += pq2 - pq1;
-                    cnt.pr_climb -= pq2;   // (+ t1 below: the climb, prefetch and restart)
-                }
-#endif
             } else if (keep) {
                 if (ch < 0) {             // leaf: fp64 primitive tests (these decide the result)
                     leaf_test(H + ~ch, PF ? pf_cnt : (int)nd->cnt[c]);
@@ -1689,9 +1660,6 @@ __device__ __forceinline__ void mode_x_wave(const DevScene& sc, NodeP W, HotP H,
         }
         const uint64_t t1 = STATS ? clock64() : 0;
         uint64_t t2 = t1;
-#if GI_X_STEPPROBE
-        if (STATS && UL && trav) cnt.pr_climb += t1;
-#endif
         if (HELP && handle && phase == PH_HELP) {   // a helper's answer to its owner; idle again
             ++nrays;
             hp_.res[wbase + howner] = best >= 0 ? 2 : 1;
@@ -2098,13 +2066,6 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
             atomicAdd(stats + GI_STAT_X_CYC_HIT, (unsigned long long)c.cyc_hit);
             atomicAdd(stats + GI_STAT_X_CYC_NEXT, (unsigned long long)c.cyc_next);
             atomicAdd(stats + GI_STAT_X_CYC_ALL, (unsigned long long)c.cyc_all);
-#if GI_X_STEPPROBE   // (probe build: slots 16-20 hold the UL step's parts instead of the divergence profile)
-            atomicAdd(stats + 16, (unsigned long long)c.pr_load);
-            atomicAdd(stats + 17, (unsigned long long)c.pr_leaf);
-            atomicAdd(stats + 18, (unsigned long long)c.pr_node);
-            atomicAdd(stats + 19, (unsigned long long)c.pr_climb);
-            atomicAdd(stats + 20, (unsigned long long)c.pr_steps);
-#else
             atomicAdd(stats + GI_STAT_X_IT_NODE, (unsigned long long)c.it_node);
             atomicAdd(stats + GI_STAT_X_LN_NODE, (unsigned long long)c.ln_node);
             atomicAdd(stats + GI_STAT_X_IT_LEAF, (unsigned long long)c.it_leaf);
@@ -2113,7 +2074,6 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_X_MIN_WAVES_LDS : GI_X_MIN_WA
             atomicAdd(stats + GI_STAT_X_LN_RS, (unsigned long long)c.ln_rs);
             atomicAdd(stats + GI_STAT_X_IT_ST, (unsigned long long)c.it_st);
             atomicAdd(stats + GI_STAT_X_LN_ST, (unsigned long long)c.ln_st);
-#endif
         }
         wave_add_stats(stats, c.rays, c.nodes, c.prims, c.px);
         uint64_t cr = c.res, pm = c.path_max;

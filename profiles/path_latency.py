@@ -54,12 +54,8 @@ def main():
                           "wave_iterations": st[gi.STAT_X_ITERS], "lane_trav_steps": st[gi.STAT_X_TRAV],
                           "handler_runs": st[gi.STAT_X_HANDLE], "nodes": st[gi.STAT_NODES], "prims": st[gi.STAT_PRIMS],
                           "clk_per_iter": round(st[gi.STAT_X_CYC_ALL] / max(1, st[gi.STAT_X_ITERS]), 1),
-                          # GI_X_STEPPROBE builds (GI_LIB=...libgi_stepprobe.so): the wave clock of the
-                          # UL traversal steps by part -- pop + load round trip, leaf tests, node test,
-                          # climb / prefetch / restart -- per step
-                          "step_probe": {"steps": st[20],
-                                         "clk_per_step": {k: round(st[i] / max(1, st[20]), 1) for k, i in
-                                                          (("load", 16), ("leaf", 17), ("node", 18), ("climb", 19))}},
+                          # (round 6's GI_X_STEPPROBE measurement build read slots 16-20 here; its data is
+                          # profiles/r06_c4_stepprobe.jsonl and the build was removed after)
                           "clk_share": {k: round(st[i] / max(1, st[gi.STAT_X_CYC_ALL]), 3) for k, i in
                                         (("trav", gi.STAT_X_CYC_TRAV), ("shade", gi.STAT_X_CYC_HIT),
                                          ("next", gi.STAT_X_CYC_NEXT))}}), flush=True)
