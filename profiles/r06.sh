@@ -153,6 +153,23 @@ evidence)
     GI_X_WF=2 timeout -k 10 600 bash profiles/profile.sh r06seg C5 > $O/prof_seg.log 2>&1 || { tail -5 $O/prof_seg.log; exit 1; } ;;
   esac
   echo "evidence $1 done" ;;
+final)
+  # round-6 final evidence: suite; PMC of the Mode R workloads (their kernels changed after evidence 1);
+  # a rocprofv3 kernel trace of the default C3 bench itself (the line and the trace from one process);
+  # bench lines of R-C4 / R-C3 against the fresh PMC, and the default C3 bench with its CPU baseline
+  O=gpurun_out/r06fin; mkdir -p $O
+  timeout -k 10 600 python3 -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -20 $O/gpu_tests.log; exit 1; }
+  tail -1 $O/gpu_tests.log
+  timeout -k 10 900 bash profiles/profile.sh r06 R-C4 R-C3 > $O/prof.log 2>&1 || { tail -5 $O/prof.log; exit 1; }
+  cp gpurun_out/r06prof/r06_r-c4_pmc.json gpurun_out/r06prof/r06_r-c3_pmc.json profiles/
+  export TMPDIR=/tmp
+  ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/c3trace -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-host-path > $GRAFT_REPO_ROOT/$O/C3_under_rocprof.json 2> $GRAFT_REPO_ROOT/$O/C3_under_rocprof.err ) || { tail -5 $O/C3_under_rocprof.err; exit 1; }
+  for W in R-C4 R-C3; do
+    timeout -k 10 300 python3 bench.py --workload $W --steps 10 --warmup 2 --no-cpu-baseline > $O/bench_$W.json 2> $O/bench_$W.err || { tail -5 $O/bench_$W.err; exit 1; }
+  done
+  timeout -k 10 400 python3 bench.py --steps 20 --warmup 2 > $O/bench_C3.json 2> $O/bench_C3.err || { tail -5 $O/bench_C3.err; exit 1; }
+  tail -c 300 $O/bench_C3.json
+  echo "final done" ;;
 *)
   sed -n 2,19p "$0"; exit 2 ;;
 esac
