@@ -65,9 +65,6 @@ struct WFQ {
     long long cap;
 };
 
-#ifndef GI_WF_NODE_DEFER
-#define GI_WF_NODE_DEFER 0   // (A/B) LDS-resident scenes: deferred node tests run once this many lanes wait
-#endif
 // Closest hit (ANY = false: the (t, primitive) minimum over t > MX_TMIN) or any hit before tmax
 // (ANY: a shadow ray; true on the first primitive found) of the ray o + t d through the 8-wide BVH.
 // Stackless: 8-bit "children left" mask per level (SH: one 64-bit word, trees of <= 8 levels);
@@ -92,55 +89,7 @@ __device__ __forceinline__ int wf_trace(NodeP W, HotP H, V3 o, V3 d, double tmax
         lvl_set<SH>(mlo, mhi, 0, rm);
         raying = rm != 0;
     }
-    // DEFER (LDS-resident scenes): a lane that pops an interior child does not test it in that step;
-    // the deferred node tests run together in a step of their own once GI_WF_NODE_DEFER lanes wait
-    // (or no lane can pop anything else), so the wave runs the node-test block less often with more
-    // lanes in it (the same masks, descents and hits: only the schedule changes)
-    constexpr bool DEFER = GI_WF_NODE_DEFER > 0 && !NST;
-    bool pend = false;
-    int pch = 0;
-    auto climb = [&]() {
-        uint32_t rest = lvl_get<SH>(mlo, mhi, level);
-        if (rest == 0 && level > 0) {   // climb to the nearest level with children left
-            if constexpr (NST) {
-                const uint64_t lm = level >= 8 ? mlo : mlo & ((1ull << (8 * level)) - 1);
-                const uint64_t hm = level <= 8 ? 0ull : mhi & ((1ull << (8 * (level - 8))) - 1);
-                level = hm ? 8 + (63 - __clzll((long long)hm)) / 8 : lm ? (63 - __clzll((long long)lm)) / 8 : 0;
-                rest = lvl_get<SH>(mlo, mhi, level);
-                node = level == 0 ? 0 : nst[level * 256];
-            } else {
-                do {
-                    --level;
-                    node = level == 0 ? 0 : W[node].parent;   // the root is node 0: no load
-                    rest = lvl_get<SH>(mlo, mhi, level);
-                } while (rest == 0 && level > 0);
-            }
-        }
-        raying = rest != 0;
-    };
     while (raying) {
-        if constexpr (DEFER) {
-            const unsigned long long mp = __ballot(pend);
-            if (mp) {
-                if (__popcll(mp) >= GI_WF_NODE_DEFER || __ballot(!pend) == 0) {
-                    if (pend) {   // the deferred node tests, in one step
-                        ++nsteps;
-                        ++nnode;
-                        pend = false;
-                        const uint32_t cm = children_mask<AXIS>(W + pch, of, ivf, tbf, dmask);
-                        if (cm) {
-                            node = pch;
-                            ++level;
-                            lvl_set<SH>(mlo, mhi, level, cm);
-                        } else {
-                            climb();
-                        }
-                    }
-                    continue;
-                }
-                if (pend) continue;   // (waits for the next node step)
-            }
-        }
         ++nsteps;
         const auto* nd = W + node;
         const uint32_t msk = lvl_get<SH>(mlo, mhi, level);
@@ -195,9 +144,6 @@ __device__ __forceinline__ int wf_trace(NodeP W, HotP H, V3 o, V3 d, double tmax
                         }
                     }
                 }
-            } else if (DEFER) {   // interior: its node test waits for the next node step
-                pend = true;
-                pch = ch;
             } else {        // interior: descend if any of its children is hit (fp32 slabs)
                 ++nnode;
                 const uint32_t cm = children_mask<AXIS>(W + ch, of, ivf, tbf, dmask);
@@ -210,7 +156,23 @@ __device__ __forceinline__ int wf_trace(NodeP W, HotP H, V3 o, V3 d, double tmax
             }
         }
         if (ANY && best >= 0) break;
-        if (!pend) climb();   // (a deferred descent keeps the lane raying)
+        uint32_t rest = lvl_get<SH>(mlo, mhi, level);
+        if (rest == 0 && level > 0) {   // climb to the nearest level with children left
+            if constexpr (NST) {
+                const uint64_t lm = level >= 8 ? mlo : mlo & ((1ull << (8 * level)) - 1);
+                const uint64_t hm = level <= 8 ? 0ull : mhi & ((1ull << (8 * (level - 8))) - 1);
+                level = hm ? 8 + (63 - __clzll((long long)hm)) / 8 : lm ? (63 - __clzll((long long)lm)) / 8 : 0;
+                rest = lvl_get<SH>(mlo, mhi, level);
+                node = level == 0 ? 0 : nst[level * 256];
+            } else {
+                do {
+                    --level;
+                    node = level == 0 ? 0 : W[node].parent;   // the root is node 0: no load
+                    rest = lvl_get<SH>(mlo, mhi, level);
+                } while (rest == 0 && level > 0);
+            }
+        }
+        raying = rest != 0;
     }
     t_out = tb;
     return best;
