@@ -221,10 +221,20 @@ def cpu_baseline(scn_text, w, h, mode, spp, depth, seed, target_s=16.0, target_1
         U.oracle_render(scn_text, w, h, mode=0, window=win, threads=threads)
         dt = time.perf_counter() - t
         rays = (win[2] - win[0]) * (win[3] - win[1])
+        # one thread on the window's middle rows (about a quarter of it)
+        q = (win[3] - win[1]) // 4
+        win1 = (win[0], win[1] + q, win[2], win[3] - q)
+        t = time.perf_counter()
+        U.oracle_render(scn_text, w, h, mode=0, window=win1, threads=1)
+        dt1 = time.perf_counter() - t
+        rays1 = (win1[2] - win1[0]) * (win1[3] - win1[1])
         return {"value": round(rays / dt / 1e6, 4), "unit": "Mray/s", "cores": threads, "kind": "port",
+                "value_1t": round(rays1 / dt1 / 1e6, 4), "cores_1t": 1,
+                "value_all": round(rays / dt / 1e6, 4), "cores_all": threads,
                 "cpu_model": model, "host_cores": host_cores,
                 "sample": f"Mode R window x[{win[0]},{win[2]}) y[{win[1]},{win[3]}), {rays} rays, {dt:.2f} s wall, "
-                          f"OpenMP over {threads} threads"}
+                          f"OpenMP over {threads} threads; value_1t: rows y[{win1[1]},{win1[3]}) of it, {rays1} rays, "
+                          f"{dt1:.2f} s on 1 thread"}
 
     def run(row0, stride, n_rows, nt, pixels=False):
         t = time.perf_counter()
