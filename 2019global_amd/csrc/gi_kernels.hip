@@ -337,6 +337,21 @@ __device__ __forceinline__ RPathR load_rpath(const RPathRec* p) {
     for (int i = 0; i < 4; ++i) r.q[i] = s[i];
     return r;
 }
+// G > 1 (k_rf_reach's lane groups): G consecutive lanes hold the same ray and walk the same path in
+// step; each tests its part of the 12 ExpBox faces (box_hit_part) and a ballot ORs the group's parts,
+// so every decision below is the group's and its lanes never diverge.  Needs the group's lanes active.
+template <int G>
+__device__ __forceinline__ bool r_box_test(V3 mn, V3 mx, V3 o, V3 d) {
+    if constexpr (G == 1) {
+        return box_hit(mn, mx, o, d);
+    } else {
+        static_assert(G == 4, "box_hit_part splits the faces over 4 lanes");
+        const int lane = (int)(threadIdx.x & 63);
+        const unsigned long long b = __ballot(box_hit_part(mn, mx, o, d, lane & 3));
+        return ((b >> (lane & ~3)) & 0xFull) != 0;
+    }
+}
+template <int G = 1>
 __device__ __forceinline__ bool r_path_reachable(const DevScene& sc, int p0, int p1, V3 o, V3 d, uint32_t& nnode,
                                                  RMemo memo = RMemo{nullptr}) {
     if (p0 >= p1) return true;
@@ -348,20 +363,20 @@ __device__ __forceinline__ bool r_path_reachable(const DevScene& sc, int p0, int
         const int ni = nd.r.node;
         if (GI_R_MEMO > 0 && memo.e) {
             int* slot = memo.e + r_memo_slot(ni);
-            const int m = *slot;
+            const int m = *slot;   // (a group's lanes read it in one instruction: the same value)
             const int key = (ni << 9) | memo.tag;   // (the scenes using a memo have < 2^22 nodes)
             if ((m & ~1) == key) {
                 if (!(m & 1)) return false;
                 continue;
             }
             ++nnode;
-            const bool ok = box_hit(ld3(nd.r.mn), ld3(nd.r.mx), o, d);
+            const bool ok = r_box_test<G>(ld3(nd.r.mn), ld3(nd.r.mx), o, d);
             *slot = key | (ok ? 1 : 0);
             if (!ok) return false;
             continue;
         }
         ++nnode;
-        if (!box_hit(ld3(nd.r.mn), ld3(nd.r.mx), o, d)) return false;
+        if (!r_box_test<G>(ld3(nd.r.mn), ld3(nd.r.mx), o, d)) return false;
     }
     return true;
 }
@@ -1073,44 +1088,49 @@ __global__ __launch_bounds__(1024) void k_rf_scan(const unsigned* in, unsigned* 
     if (t == 0) out[n] = carry;
 }
 // per hitting pair: its entity's latest reachable appearance that beats the pixel's best rank.
-// Persistent waves take chunks of 64 consecutive hits of the whole frame in turn (hoff numbers them
-// across the segments, so chunks are full; a chunk's first segment by a binary search, each lane's
-// from there), so the hits of a soup-core tile are shared by many waves.  One wave per workgroup:
-// its LDS holds a node-test memo (RMemo, GI_R_MEMO entries) per pixel slot of a tile, cleared at
-// every chunk and each entry tagged with its lane's run of equal tiles in the chunk, so lanes of
-// different tiles never read each other's results.
-template <bool STATS>
-__global__ __launch_bounds__(64) void k_rf_reach(DevScene sc, CamDev cam, TileMap m, RFlat f, unsigned long long* stats) {
-    __shared__ __attribute__((aligned(16))) int s_memo[GI_R_MEMO > 0 ? 64 * GI_R_MEMO : 4];
+// Persistent waves take chunks of 64 / G consecutive hits of the whole frame in turn (hoff numbers
+// them across the segments, so chunks are full; a chunk's first segment by a binary search, each
+// hit's from there), so the hits of a soup-core tile are shared by many waves.  G lanes per hit (G =
+// 4: each tests 3 of a node's 12 ExpBox faces, r_box_test): a wave's node-test step runs the union
+// of its lanes' face tests, which with 64 hits of mixed outcomes is nearly all 12 whether or not a
+// face accepts early, so splitting the faces shortens every hit's chain of tests about G-fold for
+// the same instructions per hit -- what a sparse launch (an eighth of R-C4: ~500 chunks of 64 on a
+// chip of 2,560 wave slots) waits on.  One wave per workgroup: its LDS holds a node-test memo
+// (RMemo, GI_R_MEMO entries) per pixel slot of a tile, cleared at every chunk and each entry tagged
+// with its hit's run of equal tiles in the chunk, so hits of different tiles never read each
+// other's results.
+template <bool STATS, int G>
+__device__ __forceinline__ void rf_reach_chunks(const DevScene& sc, const CamDev& cam, const RFlat& f, unsigned long long* stats,
+                                                int* s_memo, long long n_seg, long long n_hits) {
+    constexpr int H = 64 / G;   // hits per chunk
     const int lane = threadIdx.x & 63;
-    const long long n_regions = m.n_local;
+    const int hl = lane / G;   // this lane's hit in the chunk; lane % G its part of the face tests
     const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_w = ((long long)gridDim.x * blockDim.x) >> 6;
-    const long long n_seg = f.soff[n_regions], n_hits = f.hoff[n_seg];
     const bool use_memo = GI_R_MEMO > 0 && sc.n_rnodes < (1 << 22);
     uint32_t nnode = 0;
     // (chunks from a device counter instead, as waves free up: R-C4 0.80 -> 0.88 ms)
-    for (long long c = gw; 64 * c < n_hits; c += n_w) {
-        const long long i = 64 * c + lane;
-        long long sg = rf_find(f.hoff, n_seg, 64 * c);   // the chunk's first segment (uniform)
+    for (long long c = gw; H * c < n_hits; c += n_w) {
+        const long long i = H * c + hl;
+        long long sg = rf_find(f.hoff, n_seg, H * c);   // the chunk's first segment (uniform)
         long long r = -1;
         if (i < n_hits) {
-            while (sg + 1 < n_seg && (long long)f.hoff[sg + 1] <= i) ++sg;   // this lane's
+            while (sg + 1 < n_seg && (long long)f.hoff[sg + 1] <= i) ++sg;   // this hit's
             r = f.sreg[sg];
         }
-        // the memo is the chunk's: cleared here (each lane its row), its entries tagged with the
-        // lane's run of equal tiles in the chunk (<= 64 runs, so the tag fits its 8 bits).  Two lanes
-        // share a tag only if they hold the same tile, hence with the same row the same pixel: no
-        // entry is ever read for another ray (a tag of the tile's low bits alone let tiles r and
-        // r + 256 of one chunk, or of the wave's earlier chunks, read each other's results)
-        const long long r_prev = __shfl(r, lane > 0 ? lane - 1 : 0);
-        const unsigned long long runs = __ballot(r >= 0 && (lane == 0 || r != r_prev));
+        // the memo is the chunk's: cleared here (each lane a row), its entries tagged with the hit's
+        // run of equal tiles in the chunk (<= 64 runs, so the tag fits its 8 bits).  Two hits share a
+        // tag only if they hold the same tile, hence with the same row the same pixel: no entry is
+        // ever read for another ray (a tag of the tile's low bits alone let tiles r and r + 256 of
+        // one chunk, or of the wave's earlier chunks, read each other's results)
+        const long long r_prev = __shfl(r, lane >= G ? lane - G : 0);
+        const unsigned long long runs = __ballot(lane % G == 0 && r >= 0 && (hl == 0 || r != r_prev));
         const int run_ord = __popcll(runs & ((2ull << lane) - 1)) - 1;
         if (use_memo) {
             int4* row = reinterpret_cast<int4*>(s_memo + lane * GI_R_MEMO);
             for (int k = 0; k < GI_R_MEMO / 4; ++k) row[k] = make_int4(-1, -1, -1, -1);   // (matches no key)
         }
         __builtin_amdgcn_wave_barrier();
-        if (r >= 0) {
+        if (r >= 0) {   // (every value below is the hit's: a group's lanes stay together)
             const unsigned p = (unsigned)(sg - (long long)f.soff[r]) * GI_RF_SEG + (unsigned)(i - (long long)f.hoff[sg]);
             const unsigned pg = p < GI_RF_S0 ? 0u : f.pt[(size_t)r * GI_RF_KMAX + rf_page(p)];
             const unsigned pr = *rf_pair(f, r, p, pg);
@@ -1122,15 +1142,30 @@ __global__ __launch_bounds__(64) void k_rf_reach(DevScene sc, CamDev cam, TileMa
             for (int a = sc.app_off[e]; a < a1; ++a) {
                 const RApp ap = sc.app_rec[a];
                 const long long rk = ap.rank;
-                if (rk <= (long long)*(volatile unsigned long long*)(f.best + slot) - 1) break;
-                if (r_path_reachable(sc, ap.p0, ap.p1, cam.pos, d, nnode, memo)) {
-                    atomicMax(f.best + slot, (unsigned long long)(rk + 1));
+                long long bst = (long long)*(volatile unsigned long long*)(f.best + slot) - 1;
+                if (G > 1) bst = __shfl(bst, lane & ~(G - 1));   // one reading for the group (others raise it)
+                if (rk <= bst) break;
+                if (r_path_reachable<G>(sc, ap.p0, ap.p1, cam.pos, d, nnode, memo)) {
+                    if (lane % G == 0) atomicMax(f.best + slot, (unsigned long long)(rk + 1));
                     break;
                 }
             }
         }
     }
-    if (STATS) wave_add_stats(stats, 0, nnode, 0, 0);
+    if (STATS) wave_add_stats(stats, 0, lane % G == 0 ? nnode : 0u, 0, 0);   // (node tests per hit, not per lane)
+}
+// G = 4 for launches of at most kRfGroupHits hits (<= 2,560 chunks of 16: one per resident wave of
+// the chip, 10 per CU by the memo's LDS), else G = 1.  R-C4 (266 k hits) and its half and quarter
+// shares run faster at G = 1 (whole frame 0.67 against 0.89 ms: where the chip is full, the early
+// face exits of the single-lane test save more than the shorter chains); an eighth (33 k hits)
+// at G = 4 (rank 0 / 7: 0.33 / 0.37 -> 0.30 / 0.31 ms).  group: 0 chooses, 1 or 4 forces (tests).
+constexpr long long kRfGroupHits = 40960;
+template <bool STATS>
+__global__ __launch_bounds__(64) void k_rf_reach(DevScene sc, CamDev cam, TileMap m, RFlat f, unsigned long long* stats, int group) {
+    __shared__ __attribute__((aligned(16))) int s_memo[GI_R_MEMO > 0 ? 64 * GI_R_MEMO : 4];
+    const long long n_seg = f.soff[m.n_local], n_hits = f.hoff[n_seg];
+    if (group == 4 || (group == 0 && n_hits <= kRfGroupHits)) rf_reach_chunks<STATS, 4>(sc, cam, f, stats, s_memo, n_seg, n_hits);
+    else rf_reach_chunks<STATS, 1>(sc, cam, f, stats, s_memo, n_seg, n_hits);
 }
 // per pixel: the best rank's entity, shaded (overflowed tiles: left to k_mode_r_batch)
 template <bool STATS, bool TRI>
@@ -2244,12 +2279,13 @@ long long shard_tiles(int w, int h, int shard_count) { return make_map(w, h, sha
 // among kernels whose frames are identical bit for bit (tests/test_gpu_parity.py compares them):
 // GI_X_WF (0/1/2: force a Mode X form for a whole suite run), GI_X_HELP=0 (no shadow-ray handoff),
 // GI_R_FLAT (0/1/2: force a Mode R kernel), GI_RF_PER_SLOT (the flat Mode R pool size: 0 forces the
-// per-tile overflow path).
+// per-tile overflow path), GI_RF_GROUP (1/4: force k_rf_reach's lanes per hit).
 struct XEnv {
     int run_log2 = 0, help = 1, wf = -1;
     int r_flat = -1;                  // Mode R kernels (GI_R_FLAT): 1 the flat phases for every scene, 0 k_mode_r
                                       // for every scene, 2 k_mode_r_batch for the whole frame (tests); -1 by size
     int rf_per_slot = 16;             // flat Mode R: pool pairs per pixel slot of the frame (GI_RF_PER_SLOT)
+    int rf_group = 0;                 // k_rf_reach lanes per hit (GI_RF_GROUP): 0 by the launch's hits, 1 or 4 (tests)
 };
 const XEnv& x_env() {
     static XEnv env;
@@ -2259,6 +2295,7 @@ const XEnv& x_env() {
         if (const char* v = std::getenv("GI_R_FLAT")) env.r_flat = std::atoi(v);
         if (const char* v = std::getenv("GI_RF_PER_SLOT")) env.rf_per_slot = std::max(0, std::min(1024, std::atoi(v)));
         if (const char* v = std::getenv("GI_X_WF")) env.wf = std::atoi(v);
+        if (const char* v = std::getenv("GI_RF_GROUP")) env.rf_group = (std::atoi(v) == 1 || std::atoi(v) == 4) ? std::atoi(v) : 0;
         const char* v = std::getenv("GI_X_MAX_RUN");
         const int r = v ? std::max(1, std::min(128, std::atoi(v))) : GI_X_MAX_RUN;
         int lg = 0;
@@ -2379,6 +2416,7 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
             // when the list is empty
             const dim3 bgrid((unsigned)std::min<long long>(2 * m.n_local, 2048));
             const dim3 hgrid(16384);   // k_rf_hit: persistent waves (one per workgroup) over the segments
+            const int rgroup = x_env().rf_group;
             if (stats) hipLaunchKernelGGL(k_rf_walk<true>, pgrid, block, 0, stream, sc, cam, m, tau, f, st);
             else hipLaunchKernelGGL(k_rf_walk<false>, pgrid, block, 0, stream, sc, cam, m, tau, f, st);
 #define GI_LAUNCH_RF(S, T)                                                                                                \
@@ -2386,7 +2424,7 @@ hipError_t launch_render(const DevScene& sc, const XLaunchCfg& xc, const CamDev&
         hipLaunchKernelGGL(k_rf_scan, dim3(1), dim3(1024), 0, stream, f.rcnt, f.soff, nullptr, m.n_local, GI_RF_SEG);    \
         hipLaunchKernelGGL((k_rf_hit<S, T>), hgrid, dim3(64), 0, stream, sc, cam, m, f, st);                              \
         hipLaunchKernelGGL(k_rf_scan, dim3(1), dim3(1024), 0, stream, f.shc, f.hoff, f.soff + m.n_local, 0ll, 1u);       \
-        hipLaunchKernelGGL(k_rf_reach<S>, dim3(4 * fgrid.x), dim3(64), 0, stream, sc, cam, m, f, st);                     \
+        hipLaunchKernelGGL(k_rf_reach<S>, dim3(4 * fgrid.x), dim3(64), 0, stream, sc, cam, m, f, st, rgroup);              \
         hipLaunchKernelGGL((k_rf_shade<S, T>), pgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, f, st);             \
         hipLaunchKernelGGL((k_mode_r_batch<S, T>), bgrid, block, 0, stream, sc, cam, light, m, rgb, rgb8, st, tau,        \
                            (const unsigned*)xs.rf_ovf, (const unsigned*)(xs.rf_cnt + 1));                                 \

@@ -177,6 +177,26 @@ GI_HD bool box_hit(V3 mn, V3 mx, V3 o, V3 d) {
            tri_hit_corners(urt, drb, drt, o, d) || tri_hit_corners(urt, dlt, drt, o, d);
 }
 
+// box_hit split over four lanes: part j in [0, 4) tests faces j, j + 4, j + 8 of box_hit's order
+// (spurious faces 0-5, real faces 6-11), so the OR over the four parts is box_hit's answer.  Face
+// f's rectangle k = f % 6 has corners p1 (dlb for k < 3, else urt), p2 and p3 (-p3 for the spurious
+// triangle), each corner picked from mn / mx by its 3 bits (x = 1, y = 2, z = 4) -- the same corners
+// and triangles as box_hit, selected per lane so that every lane runs the same code.
+GI_HD V3 box_corner(V3 mn, V3 mx, int bits) {
+    return v3((bits & 1) ? mx.x : mn.x, (bits & 2) ? mx.y : mn.y, (bits & 4) ? mx.z : mn.z);
+}
+GI_HD bool box_face_hit(V3 mn, V3 mx, V3 o, V3 d, int f) {
+    const int k = f >= 6 ? f - 6 : f;
+    // p2 and p3 corner bits of rectangles k = 0..5 (urb ult drt ulb drb dlt; ulb dlt dlt ult drt drt), 4 bits each
+    const int b2 = (0x214365 >> (4 * k)) & 7, b3 = (0x336224 >> (4 * k)) & 7;
+    const V3 p3 = box_corner(mn, mx, b3);
+    return tri_hit_corners(box_corner(mn, mx, k < 3 ? 0 : 7), box_corner(mn, mx, b2), f < 6 ? -p3 : p3, o, d);
+}
+GI_HD bool box_hit_part(V3 mn, V3 mx, V3 o, V3 d, int part) {
+    return box_face_hit(mn, mx, o, d, part) || box_face_hit(mn, mx, o, d, part + 4) ||
+           box_face_hit(mn, mx, o, d, part + 8);
+}
+
 // ImpSphere::intersect (entities.h:53-96): the quadratic in the dominant-axis parameterisation
 // with its fp32/fp64 mix; a line test on |root| (A.2).
 GI_HD bool sphere_hit(V3 pos, float radius, V3 o, V3 d, V3& P, V3& N) {

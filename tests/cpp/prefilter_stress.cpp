@@ -70,6 +70,28 @@ int main(int argc, char** argv) {
         if (r != f || r != u || rs != us) { ++bad; if (bad < 5) printf("mismatch it=%ld mode=%d raw=%d full=%d\n", it, mode, r, u); }
         if (mode == 2) near += r;
     }
+    // box_hit_part: the OR of its four parts (3 faces each, for four cooperating lanes) is box_hit
+    long nb = 0, bhits = 0, bbad = 0;
+    for (long it = 0; it < N / 8; ++it) {
+        const double sc = std::pow(10.0, 2 * U(g));
+        const V3 c = v3(U(g), U(g), U(g)) * (sc * (it % 2 ? 0.5 : 4.0));
+        const V3 hw = v3(U(g) + 1.01, U(g) + 1.01, U(g) + 1.01) * (sc * 0.25);
+        const V3 mn = c - hw, mx = c + hw;
+        const V3 o = v3(U(g), U(g), U(g)) * (sc * 10);
+        V3 tgt;
+        const int mode = it % 3;
+        if (mode == 0) tgt = c + vmul(hw, v3(U(g), U(g), U(g)));               // through the box
+        else if (mode == 1) tgt = c + vmul(hw, v3(U(g), U(g), U(g)) * 1.05);   // near its faces
+        else tgt = -c + vmul(hw, v3(U(g), U(g), U(g)));                        // its mirror image (A.4)
+        const V3 d = normalize(tgt - o);
+        const bool b = box_hit(mn, mx, o, d);
+        const bool q = box_hit_part(mn, mx, o, d, 0) || box_hit_part(mn, mx, o, d, 1) ||
+                       box_hit_part(mn, mx, o, d, 2) || box_hit_part(mn, mx, o, d, 3);
+        ++nb; bhits += b;
+        if (b != q) { ++bbad; if (bbad < 5) printf("box mismatch it=%ld mode=%d box_hit=%d parts=%d\n", it, mode, b, q); }
+    }
+    printf("box cases %ld hits %ld box mismatches %ld\n", nb, bhits, bbad);
+    bad += bbad;
     printf("cases %ld raw hits %ld near-edge hits %ld mismatches %ld\n", n, hits, near, bad);
     return bad != 0;
 }

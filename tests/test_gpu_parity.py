@@ -1036,6 +1036,51 @@ def test_mode_r_large_scene_kernels_on_small_scenes(torch_cuda, tmp_path, kernel
             assert U.bits_equal(p.cpu().numpy(), ref[name + "_packed"]).all(), name + " packed"
 
 
+@pytest.mark.parametrize("group", ["1", "4"])
+def test_mode_r_reach_lane_groups_bit_exact(torch_cuda, tmp_path, group):
+    """k_rf_reach with one lane per hit (GI_RF_GROUP=1) or four (GI_RF_GROUP=4: the 12 ExpBox faces of
+    a node test split over the hit's lanes, OR-ed by a ballot), forced in a child process on launches
+    the default gives to the other: the 100k soup's whole 1080p frame (266 k hits, default 1) and its
+    8 shards (~33 k hits each, default 4), and the one-tile-column strip -- bit for bit the frames of
+    the default choice."""
+    import subprocess
+    import sys
+    w, h, n = 1920, 1080, 8
+    strip = tmp_path / "strip.scn"
+    strip.write_text(_strip_scene(size=0.3).to_scn())
+    out = tmp_path / "groups.npz"
+    code = ("import sys, numpy as np; sys.path.insert(0, %r); sys.path.insert(0, %r); import oracle_util as U; "
+            "import torch; gi = U.pkg(); S = U.scenes(); res = {}\n"
+            "sc = S.named_scene('soup100000'); d = gi.DeviceScene.from_scene(sc)\n"
+            "cam = gi.Camera(sc.cam_pos, sc.cam_look, sc.focal)\n"
+            "res['full'] = d.render(cam, sc.light, %d, %d)[0]\n"
+            "per = gi.shard_tiles(%d, %d, %d) * gi.TILE * gi.TILE * 3\n"
+            "p = torch.zeros(%d * per, dtype=torch.float64, device='cuda')\n"
+            "for r in range(%d): d.render_device(cam, sc.light, %d, %d, p.data_ptr() + r * per * 8, 0, shard_count=%d, shard_index=r)\n"
+            "torch.cuda.synchronize(); res['packed'] = p.cpu().numpy()\n"
+            "st = S.parse_scn(open(%r).read()); ds = gi.DeviceScene.from_scene(st)\n"
+            "res['strip'] = ds.render(gi.Camera(st.cam_pos, st.cam_look, st.focal), st.light, 2048, 1088)[0]\n"
+            "np.savez(%r, **res)") % (U.ROOT, os.path.join(U.ROOT, "tests"), w, h, w, h, n, n, n, w, h, n, str(strip), str(out))
+    subprocess.run([sys.executable, "-c", code], check=True, timeout=300, env=dict(os.environ, GI_RF_GROUP=group))
+    ref = np.load(out)
+    torch = torch_cuda
+    sc = _scene("soup100000")
+    d = dev_scene("soup100000")
+    assert d.r_kernel() == "k_rf_walk"
+    rgb, _ = d.render(cam_of(sc), sc.light, w, h)
+    assert U.bits_equal(rgb, ref["full"]).all(), "whole frame"
+    per = gi.shard_tiles(w, h, n) * gi.TILE * gi.TILE * 3
+    p = torch.zeros(n * per, dtype=torch.float64, device="cuda")
+    for r in range(n):
+        d.render_device(cam_of(sc), sc.light, w, h, p.data_ptr() + r * per * 8, 0, shard_count=n, shard_index=r)
+    torch.cuda.synchronize()
+    assert U.bits_equal(p.cpu().numpy(), ref["packed"]).all(), "8 shards"
+    st = _strip_scene(size=0.3)
+    ds = gi.DeviceScene.from_scene(st)
+    rs, _ = ds.render(cam_of(st), st.light, 2048, 1088)
+    assert U.bits_equal(rs, ref["strip"]).all(), "strip"
+
+
 @pytest.mark.parametrize("accel", [{"GI_XACCEL": "octree"}, {"GI_XLEAF_MAX": "1"}, {"GI_XSBVH": "1"}])
 def test_mode_x_other_acceleration_structures_bit_exact(torch_cuda, accel):
     """Mode X over the SAT octree (GI_XACCEL=octree: up to 12 levels, so the kernel keeps its two-word
