@@ -469,6 +469,98 @@ struct XBuild {
     }
 };
 
+// Plane groups (Mode X; DESIGN.md §5 "own-plane leaves"): triangles that lie in one plane share a
+// group id (XPrim::pad[0], 0..253; kXNoPlane otherwise), and a wide-node leaf child all of whose
+// records are one group carries its id (byte c of XWNode::pad; kXNoPlane otherwise).  A ray leaving
+// a surface point of group g can skip g's leaves outright: its origin lies on g's plane to within
+// rounding, so the exact test of any triangle in that plane finds t within a few ulps of 0 -- below
+// MX_TMIN -- unless the ray is nearly parallel to the plane.  The kernels skip only when
+// |d . n| >= x_skip_a * max|cam| + x_skip_b, K = 2000 times the worst rounding:
+//   * the origin P = o + t d of a hit on X is off X's plane by ~u (|o| + |P| + |o - v0| / s): the
+//     rounding of P and of the exact test's t (whose error along the ray, ~u |o - v0| / (s |d . n|),
+//     shrinks with the incidence), s the sine of the triangle's smallest angle;
+//   * a triangle Y of the group lies within tau of X's plane (measured here), and its own test's t
+//     error is ~u |P - v0_Y| / (s_Y |d . n|);
+// so |t_Y| <= (u (|cam| + 4 E) / s_min + tau) / |d . n| up to small constants, and |d . n| >=
+// K (u (|cam| + 4 E) / s_min + tau) / MX_TMIN keeps it below MX_TMIN / K.  Triangles with s < 1e-3
+// join no group.  The CPU checker (tests/cpp/xaccel_check.cpp) runs the skip against brute force on
+// rays from surface points, down to incidences just above the bound.
+constexpr int kXNoPlane = 255;
+void assign_plane_groups(HostScene& hs) {
+    const size_t np = hs.xprims.size();
+    hs.x_skip_a = 0.0;
+    hs.x_skip_b = 2.0;   // > 1 >= |d . n|: no skip
+    for (XPrim& p : hs.xprims) p.pad[0] = kXNoPlane;
+    for (XWNode& w : hs.xwnodes) memset(w.pad, 0xFF, sizeof w.pad);
+    double E = 0.0;
+    for (const XPrim& p : hs.xprims)
+        for (int k = 0; k < 3; ++k) {
+            if (p.kind == 1) {
+                E = std::max(E, std::fabs(p.a[k]) + std::fabs(p.b[0]));
+            } else {
+                E = std::max(E, std::fabs(p.a[k]));
+                E = std::max(E, std::fabs(p.a[k] + p.b[k]));
+                E = std::max(E, std::fabs(p.a[k] + p.c[k]));
+            }
+        }
+    struct G {
+        V3 n;
+        double off;
+    };
+    std::vector<G> groups;
+    double s_min = 1.0, tau = 0.0;
+    const double tol = 1e-12 * std::max(E, 1.0);
+    for (size_t i = 0; i < np; ++i) {
+        XPrim& p = hs.xprims[i];
+        if (p.kind != 0) continue;
+        const V3 v0 = ld3(p.a), e1 = ld3(p.b), e2 = ld3(p.c), e3 = e2 - e1;
+        const V3 cr = cross(e1, e2);
+        const double area2 = std::sqrt(dot(cr, cr)), l1 = std::sqrt(dot(e1, e1)), l2 = std::sqrt(dot(e2, e2)),
+                     l3 = std::sqrt(dot(e3, e3));
+        if (!(area2 > 0.0) || !std::isfinite(area2)) continue;
+        const double s = std::min(std::min(area2 / (l1 * l2), area2 / (l1 * l3)), area2 / (l2 * l3));
+        if (!(s >= 1e-3)) continue;
+        V3 n = cr * (1.0 / area2);
+        if (n.x < 0 || (n.x == 0 && (n.y < 0 || (n.y == 0 && n.z < 0)))) n = -n;
+        const V3 vs[3] = {v0, v0 + e1, v0 + e2};
+        int g = -1;
+        double dev = 0.0;
+        for (size_t k = 0; k < groups.size() && g < 0; ++k) {
+            const V3 dn = n - groups[k].n;
+            if (std::max(std::fabs(dn.x), std::max(std::fabs(dn.y), std::fabs(dn.z))) > 1e-12) continue;
+            double m = 0.0;
+            for (const V3& v : vs) m = std::max(m, std::fabs(dot(groups[k].n, v) - groups[k].off));
+            if (m <= tol) {
+                g = (int)k;
+                dev = m;
+            }
+        }
+        if (g < 0) {
+            if (groups.size() >= 254) continue;
+            groups.push_back(G{n, dot(n, v0)});
+            g = (int)groups.size() - 1;
+            for (const V3& v : vs) dev = std::max(dev, std::fabs(dot(n, v) - groups[g].off));
+        }
+        p.pad[0] = g;
+        tau = std::max(tau, dev);
+        s_min = std::min(s_min, s);
+    }
+    if (groups.empty()) return;
+    for (XWNode& w : hs.xwnodes) {
+        uint8_t* b = reinterpret_cast<uint8_t*>(w.pad);
+        for (int c = 0; c < 8; ++c) {
+            if (w.child[c] >= 0 || w.child[c] == XEMPTY || w.cnt[c] == 0) continue;
+            int g = hs.xprims[hs.xhot[~w.child[c]].prim].pad[0];
+            for (int j = 1; j < w.cnt[c] && g != kXNoPlane; ++j)
+                if (hs.xprims[hs.xhot[~w.child[c] + j].prim].pad[0] != g) g = kXNoPlane;
+            b[c] = (uint8_t)g;
+        }
+    }
+    const double K = 2000.0, u = 0x1.0p-53, tmin = 1e-7;
+    hs.x_skip_a = K * u / (s_min * tmin);
+    hs.x_skip_b = K * (4.0 * u * E / s_min + tau + 4.0 * u * E) / tmin;
+}
+
 }  // namespace
 
 bool build_host_scene(const gi_scene_desc& desc, HostScene& hs, std::string& err) {
@@ -577,6 +669,7 @@ bool build_host_scene(const gi_scene_desc& desc, HostScene& hs, std::string& err
         int leaf_max = 4;
         if (const char* lm = std::getenv("GI_XLEAF_MAX")) leaf_max = std::max(1, std::atoi(lm));
         build_xbvh(hs.xprims, bounds, leaf_max, hs, true);
+        assign_plane_groups(hs);
         return true;
     }
     hs.xnodes.resize(1);
@@ -692,6 +785,7 @@ bool build_host_scene(const gi_scene_desc& desc, HostScene& hs, std::string& err
         }
     }
     finalize_xwnodes(hs.xwnodes);
+    assign_plane_groups(hs);
     return true;
 }
 

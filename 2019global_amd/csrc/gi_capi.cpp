@@ -499,6 +499,8 @@ int scene_create_on(const gi_scene_desc* desc, int device, gi_scene** out) {
     d.x_max_depth = h.x_max_depth;
     d.x_handle8 = h.x_handle8;
     d.x_flags = h.x_flags;
+    d.x_skip_a = h.x_skip_a;
+    d.x_skip_b = h.x_skip_b;
     d.n_xhot = (int32_t)h.xhot.size();
     d.n_r_always = (int32_t)h.r_always.size();
     d.rc_ext = (float)h.rc_ext;

@@ -228,15 +228,30 @@ __device__ __forceinline__ uint32_t xor_permute8(uint32_t m, int dm) {
     m = (dm & 4) ? (((m << 4) & 0xF0u) | ((m >> 4) & 0x0Fu)) : m;
     return m;
 }
+// bit c set iff child c is a leaf of plane group `skip` (byte c of the node's pad; gi_build.cpp
+// assign_plane_groups): SWAR compare of the 8 bytes with skip, zero bytes gathered to bits
+__device__ __forceinline__ uint32_t plane_bits(const XWNode* nd, int skip) {
+    const uint32_t s4 = (uint32_t)skip * 0x01010101u;
+    uint32_t r = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const uint32_t x = (uint32_t)nd->pad[h] ^ s4;
+        const uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);   // 0x80 in the zero bytes
+        r |= (((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u)) << (4 * h);
+    }
+    return r;
+}
 // mask of hit, existing children with bit k for child k ^ dmask (bit order = front-to-back).
 // The node's 48 bounds are fetched by 12 independent 16-byte loads (one memory round trip) and
 // all 8 slab tests run branch-free; existence comes from the node's precomputed bit mask.
 // AXIS: the slab tests accumulate axis by axis (4 float4 live instead of 12: fewer VGPRs at the
 // node step, which lets the LDS-resident kernel run 4 waves per SIMD); otherwise all 12 loads are
 // issued at once (one memory round trip: the HBM-resident kernel's choice).  Same mask either way.
-template <bool AXIS>
-__device__ __forceinline__ uint32_t children_mask(const XWNode* nd, F3 of, F3 ivf, float tmax, int dmask) {
+// SKIP: the leaf children of plane group skip left out (the own-plane skip; skip 254 matches none).
+template <bool AXIS, bool SKIP = false>
+__device__ __forceinline__ uint32_t children_mask(const XWNode* nd, F3 of, F3 ivf, float tmax, int dmask, int skip = 254) {
     const float4* b = reinterpret_cast<const float4*>(nd);
+    const uint32_t ex = SKIP ? ((uint32_t)nd->exists & ~plane_bits(nd, skip)) : (uint32_t)nd->exists;
     const F3 no = neg_oiv(of, ivf);
     const int sm = iv_signs(ivf);   // near / far planes per axis (see child_hit)
     if constexpr (AXIS) {
@@ -265,7 +280,7 @@ __device__ __forceinline__ uint32_t children_mask(const XWNode* nd, F3 of, F3 iv
     uint32_t m = 0;
 #pragma unroll
     for (int c = 0; c < 8; ++c) m |= tn[c] <= tf[c] ? 1u << c : 0u;
-    return xor_permute8(m & (uint32_t)nd->exists, dmask);
+    return xor_permute8(m & ex, dmask);
     } else {
     // all 12 quads at once (one memory round trip), the near and far planes' addressed directly
     float4 q[12];
@@ -277,7 +292,6 @@ __device__ __forceinline__ uint32_t children_mask(const XWNode* nd, F3 of, F3 iv
         q[6 + 2 * a] = b[fq];
         q[6 + 2 * a + 1] = b[fq + 1];
     }
-    const int ex = nd->exists;
     const float* v = reinterpret_cast<const float*>(q);   // near[3][8] then far[3][8]
     uint32_t m = 0;
 #pragma unroll
@@ -289,7 +303,7 @@ __device__ __forceinline__ uint32_t children_mask(const XWNode* nd, F3 of, F3 iv
                                fminf(__builtin_fmaf(fz, ivf.z, no.z), tmax));
         m |= tn <= tf ? 1u << c : 0u;
     }
-    return xor_permute8(m & (uint32_t)ex, dmask);
+    return xor_permute8(m & ex, dmask);
     }
 }
 

@@ -65,7 +65,7 @@ struct XPrim {             // 112 bytes
     double n[3];           // triangle geometric normal normalize(cross(e1,e2))
     int32_t kind;          // 0 triangle, 1 sphere
     int32_t ent;
-    int32_t pad[2];
+    int32_t pad[2];        // pad[0]: plane group (gi_build.cpp assign_plane_groups; 255 none)
 };
 static_assert(sizeof(XPrim) == 112, "XPrim layout");
 
@@ -88,7 +88,7 @@ struct XWNode {            // 256 bytes, 2 cache lines
     int32_t parent;        // wide node of the parent cell, -1 at the root (stackless traversal)
     uint16_t cnt[8];       // leaf children: number of xhot records
     int32_t exists;        // bit c set iff child[c] != XEMPTY (branch-free culling)
-    int32_t pad[2];
+    int32_t pad[2];        // byte c: plane group of leaf child c, 255 none (Mode X scene nodes)
 };
 static_assert(sizeof(XWNode) == 256, "XWNode layout");
 // The same node quantised into one 128-byte cache line (HBM-resident scenes, k_mode_x): child c's
@@ -166,6 +166,7 @@ struct HostScene {
     int32_t x_flags = 0;     // Mode X schedule flags (DevScene::x_flags), chosen by the builder
     double x_est_nodes = 0, x_est_prims = 0;   // SAH estimates per random ray through the root
     bool x_spatial = false;  // the Mode X BVH was built with spatial splits (a primitive in several leaves)
+    double x_skip_a = 0.0, x_skip_b = 2.0;   // own-plane leaf skip: |d . n| >= a * max|cam| + b (gi_build.cpp)
 };
 
 // Sets XWNode::exists from the child references (both Mode X builders call it last).
@@ -209,6 +210,7 @@ struct DevScene {
                            // ExpBox (the 4-wave kinds): HBM-resident k_mode_x's TRI specialisation
     int32_t r_tri_only;    // every entity an ImpTriangle: the Mode R kernels' TRI specialisation
     float root_lo[3], root_hi[3];   // Mode X: union of the root's fp32 child boxes (conservative)
+    double x_skip_a, x_skip_b;      // Mode X own-plane leaf skip bound (HostScene, gi_build.cpp)
     // Mode R candidate reconstruction (HostScene fields of the same names)
     const int32_t* app_off;
     const RApp* app_rec;

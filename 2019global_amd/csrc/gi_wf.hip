@@ -74,7 +74,10 @@ struct WFQ {
 // re-tested against the current best t (its box is a ds_read away).
 template <bool ANY, bool PAIR, bool AXIS, bool SH, bool TRI, bool NST, typename NodeP, typename HotP>
 __device__ __forceinline__ int wf_trace(NodeP W, HotP H, V3 o, V3 d, double tmax, bool act, int* nst, double& t_out,
-                                        uint32_t& nnode, uint32_t& nprim, uint32_t& nsteps) {
+                                        uint32_t& nnode, uint32_t& nprim, uint32_t& nsteps, int skip = 254) {
+    // the own-plane skip (XWNode scenes; gi_build.cpp assign_plane_groups): leaves of group skip are
+    // never entered -- their exact tests would all find t below MX_TMIN for this ray
+    constexpr bool kSkip = std::is_same<NodeP, const XWNode*>::value;
     const F3 of = f3((float)o.x, (float)o.y, (float)o.z);
     const F3 ivf = inv_dir(d);
     const int dmask = (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
@@ -85,7 +88,9 @@ __device__ __forceinline__ int wf_trace(NodeP W, HotP H, V3 o, V3 d, double tmax
     int node = 0, level = 0;
     bool raying = false;
     if (act) {
-        const uint32_t rm = children_mask<AXIS>(W, of, ivf, tbf, dmask);
+        uint32_t rm;
+        if constexpr (kSkip) rm = children_mask<AXIS, true>(W, of, ivf, tbf, dmask, skip);
+        else rm = children_mask<AXIS>(W, of, ivf, tbf, dmask);
         lvl_set<SH>(mlo, mhi, 0, rm);
         raying = rm != 0;
     }
@@ -146,7 +151,9 @@ __device__ __forceinline__ int wf_trace(NodeP W, HotP H, V3 o, V3 d, double tmax
                 }
             } else {        // interior: descend if any of its children is hit (fp32 slabs)
                 ++nnode;
-                const uint32_t cm = children_mask<AXIS>(W + ch, of, ivf, tbf, dmask);
+                uint32_t cm;
+                if constexpr (kSkip) cm = children_mask<AXIS, true>(W + ch, of, ivf, tbf, dmask, skip);
+                else cm = children_mask<AXIS>(W + ch, of, ivf, tbf, dmask);
                 if (cm) {
                     node = ch;
                     ++level;
@@ -290,7 +297,8 @@ __device__ __forceinline__ void wf_wave_steps(uint32_t n, uint64_t& it, uint64_t
 template <bool STATS, bool LDS, bool SH, bool TRI, bool CN, typename KeyF>
 __device__ __forceinline__ bool x_segment(const DevScene& sc, const WFView& v, const V3& light, int depth, bool no_shadow, bool act,
                                           const KeyF& id_of, V3& o, V3& d, V3& L, V3& T,
-                                          uint32_t& nnode, uint32_t& nprim, uint32_t& nrays, WFSegStats& ws) {
+                                          uint32_t& nnode, uint32_t& nprim, uint32_t& nrays, WFSegStats& ws,
+                                          double skip_cos = 2.0, int* splane = nullptr) {
     uint32_t st_steps = 0;
     uint64_t c0 = STATS ? clock64() : 0;
     V3 P = o, Ld = v3(0, 0, 1);
@@ -298,9 +306,11 @@ __device__ __forceinline__ bool x_segment(const DevScene& sc, const WFView& v, c
     // ---- closest hit
     double tbest = INFINITY;
     int best;
-    if constexpr (LDS) best = wf_trace<false, true, false, SH, TRI, false>(v.LW, v.LH, o, d, INFINITY, act, v.nst, tbest, nnode, nprim, st_steps);
+    // the own-plane skip of this ray (k_seg carries it from the previous segment; 254: none)
+    const int skip_c = splane ? *splane : 254;
+    if constexpr (LDS) best = wf_trace<false, true, false, SH, TRI, false>(v.LW, v.LH, o, d, INFINITY, act, v.nst, tbest, nnode, nprim, st_steps, skip_c);
     else if constexpr (CN) best = wf_trace<false, false, false, SH, TRI, true>(sc.xcnodes, sc.xhot, o, d, INFINITY, act, v.nst, tbest, nnode, nprim, st_steps);
-    else best = wf_trace<false, false, false, SH, TRI, true>(sc.xwnodes, sc.xhot, o, d, INFINITY, act, v.nst, tbest, nnode, nprim, st_steps);
+    else best = wf_trace<false, false, false, SH, TRI, true>(sc.xwnodes, sc.xhot, o, d, INFINITY, act, v.nst, tbest, nnode, nprim, st_steps, skip_c);
     if (act) ++nrays;
     if (STATS) {
         wf_wave_steps(st_steps, ws.it_c, ws.ln_c);
@@ -312,18 +322,24 @@ __device__ __forceinline__ bool x_segment(const DevScene& sc, const WFView& v, c
     const bool hit = act && best >= 0;
     // ---- the hit point and its shadow ray toward the point light
     double ldist = 0.0;
+    int pg = 254;   // the hit's plane group: the shadow ray and the next ray leave its plane
+    V3 pn = v3(0, 0, 1);
     if (hit) {
         P = o + tbest * d;
         const V3 lv = light - P;
         ldist = gsqrt(dot(lv, lv));
         Ld = normalize(lv);
+        const XPrim& px = v.XP[best];
+        pg = px.pad[0] < 254 ? px.pad[0] : 254;
+        pn = ld3(px.n);
     }
     if (!no_shadow) {
         double tdummy;
         int sb;
-        if constexpr (LDS) sb = wf_trace<true, true, false, SH, TRI, false>(v.LW, v.LH, P, Ld, ldist, hit, v.nst, tdummy, nnode, nprim, st_steps);
+        const int skip_s = (pg < 254 && fabs(dot(Ld, pn)) >= skip_cos) ? pg : 254;
+        if constexpr (LDS) sb = wf_trace<true, true, false, SH, TRI, false>(v.LW, v.LH, P, Ld, ldist, hit, v.nst, tdummy, nnode, nprim, st_steps, skip_s);
         else if constexpr (CN) sb = wf_trace<true, false, false, SH, TRI, true>(sc.xcnodes, sc.xhot, P, Ld, ldist, hit, v.nst, tdummy, nnode, nprim, st_steps);
-        else sb = wf_trace<true, false, false, SH, TRI, true>(sc.xwnodes, sc.xhot, P, Ld, ldist, hit, v.nst, tdummy, nnode, nprim, st_steps);
+        else sb = wf_trace<true, false, false, SH, TRI, true>(sc.xwnodes, sc.xhot, P, Ld, ldist, hit, v.nst, tdummy, nnode, nprim, st_steps, skip_s);
         occl = sb >= 0;
         if (STATS) wf_wave_steps(st_steps, ws.it_s, ws.ln_s);
     }
@@ -385,6 +401,7 @@ __device__ __forceinline__ bool x_segment(const DevScene& sc, const WFView& v, c
         if (cont) {
             v.pl[0] = L.x; v.pl[256] = L.y; v.pl[512] = L.z;
             v.pl[768] = T.x; v.pl[1024] = T.y; v.pl[1280] = T.z;
+            if (splane) *splane = (pg < 254 && fabs(dot(d, pn)) >= skip_cos) ? pg : 254;
         }
     }
     if (STATS) ws.cyc_sh += clock64() - c0;
@@ -467,8 +484,11 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
             v.pl[768] = T.x; v.pl[1024] = T.y; v.pl[1280] = T.z;
         }
         WFSegStats ws;
+        // (the queue carries no plane: the closest ray is not skipped here, the shadow ray is)
+        const double skip_cos = sc.x_skip_a * fmax(fabs(cam.pos.x), fmax(fabs(cam.pos.y), fabs(cam.pos.z))) + sc.x_skip_b;
+        int splane = 254;
         const bool cont = x_segment<false, LDS, SH, TRI, CN>(sc, v, light, depth, no_shadow, act, [&] { return PathId{key, smp, b}; }, o, d, L, T,
-                                                             nnode, nprim, nrays, ws);
+                                                             nnode, nprim, nrays, ws, skip_cos, &splane);
         // ---- live paths to the next bounce's queue: one atomic per wave, entries in lane order
         const unsigned long long mc = __ballot(cont);
         if (mc) {
@@ -539,6 +559,9 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
     long long idx = -1;
     uint64_t key = 0;
     V3 o = cam.pos, d = v3(1, 0, 0), L = v3(0, 0, 0), T = v3(1, 1, 1);
+    int splane = 254;   // the own-plane skip of the lane's next ray (254: none; primary rays)
+    // (gi_build.cpp assign_plane_groups: the bound on |d . n| above which a surface's own plane is skipped)
+    const double skip_cos = sc.x_skip_a * fmax(fabs(cam.pos.x), fmax(fabs(cam.pos.y), fabs(cam.pos.z))) + sc.x_skip_b;
     WFSegStats ws;
     const uint64_t t_begin = STATS ? clock64() : 0;
     for (;;) {
@@ -598,6 +621,7 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
                     live = true;
                     o = cam.pos;
                     d = normalize(d0);
+                    splane = 254;
                     L = v3(0, 0, 0);
                     T = v3(1, 1, 1);
                     v.pl[0] = 0.0; v.pl[256] = 0.0; v.pl[512] = 0.0;
@@ -621,7 +645,7 @@ __global__ __launch_bounds__(256, (LDS && W4) ? GI_WF_MIN_WAVES_LDS : GI_WF_MIN_
         const bool cont = x_segment<STATS, LDS, SH, TRI, CN>(
             sc, v, light, depth, no_shadow, live,
             [&] { return PathId{slot_get_u64(v.pl, 6), (unsigned)(slot_get_u64(v.pl, 7) >> 32), (int)slot_get_u64(v.pl, 8)}; },
-            o, d, L, T, nnode, nprim, nrays, ws);
+            o, d, L, T, nnode, nprim, nrays, ws, skip_cos, &splane);
         if (live) {
             if (cont) {
                 slot_put_u64(v.pl, 8, slot_get_u64(v.pl, 8) + 1);

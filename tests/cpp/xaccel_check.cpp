@@ -110,10 +110,13 @@ static bool child_hit(const XWNode* nd, int c, F3 of, F3 ivf, float tmax) {
     const float tf = std::fmin(std::fmin(std::fmax(tx0, tx1), std::fmax(ty0, ty1)), std::fmin(std::fmax(tz0, tz1), tmax));
     return tn <= tf;
 }
-static uint32_t children_mask(const XWNode* nd, F3 of, F3 ivf, float tmax, int dmask) {
+// skip: a plane group whose leaf children are left out (the kernels' own-plane skip; -1 none)
+static uint32_t children_mask(const XWNode* nd, F3 of, F3 ivf, float tmax, int dmask, int skip = -1) {
     uint32_t m = 0;
+    const uint8_t* pg = reinterpret_cast<const uint8_t*>(nd->pad);
     for (int c = 0; c < 8; ++c)
-        if (nd->child[c] != XEMPTY && child_hit(nd, c, of, ivf, tmax)) m |= 1u << (c ^ dmask);
+        if (nd->child[c] != XEMPTY && child_hit(nd, c, of, ivf, tmax) && !(nd->child[c] < 0 && pg[c] == skip))
+            m |= 1u << (c ^ dmask);
     return m;
 }
 static uint32_t lvl_get(uint64_t lo, uint64_t hi, int l) { return (uint32_t)((l < 8 ? lo >> (8 * l) : hi >> (8 * (l - 8))) & 0xFF); }
@@ -124,7 +127,7 @@ static void lvl_set(uint64_t& lo, uint64_t& hi, int l, uint32_t m) {
 
 // k_mode_x's traversal of one ray; shadow: any hit with t < tmax
 static long g_prim_tests = 0;
-static int traverse(const HostScene& s, V3 o, V3 d, bool shadow, double tmax, double& tbest, long& visits) {
+static int traverse(const HostScene& s, V3 o, V3 d, bool shadow, double tmax, double& tbest, long& visits, int skip = -1) {
     // the device uses v_rcp_f32 (1 ulp) here; the correctly rounded fp32 reciprocal stands in for it
     const F3 of = {(float)o.x, (float)o.y, (float)o.z}, ivf = {inv_clamp((float)d.x), inv_clamp((float)d.y), inv_clamp((float)d.z)};
     const int dmask = (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
@@ -132,7 +135,7 @@ static int traverse(const HostScene& s, V3 o, V3 d, bool shadow, double tmax, do
     float tbest_f = shadow ? up32(tmax) : INFINITY;
     int best = -1, node = 0, level = 0;
     uint64_t mlo = 0, mhi = 0;
-    const uint32_t rm = children_mask(&s.xwnodes[0], of, ivf, tbest_f, dmask);
+    const uint32_t rm = children_mask(&s.xwnodes[0], of, ivf, tbest_f, dmask, skip);
     lvl_set(mlo, mhi, 0, rm);
     bool raying = rm != 0;
     while (raying) {   // one iteration = one traversal step of k_mode_x
@@ -159,7 +162,7 @@ static int traverse(const HostScene& s, V3 o, V3 d, bool shadow, double tmax, do
                 }
             } else {
                 ++visits;
-                const uint32_t cm = children_mask(&s.xwnodes[ch], of, ivf, tbest_f, dmask);
+                const uint32_t cm = children_mask(&s.xwnodes[ch], of, ivf, tbest_f, dmask, skip);
                 if (cm) {
                     node = ch;
                     ++level;
@@ -290,6 +293,60 @@ static bool read_scn(const char* path, std::vector<gi_entity_desc>& ents) {
     return !ents.empty();
 }
 
+// The own-plane skip (gi_build.cpp assign_plane_groups; gi_wf.hip x_segment): rays leaving a hit
+// point on a grouped triangle -- the hit computed as the kernel does, P = o + t d with t from the exact
+// test -- toward random targets (shadow: any hit before tmax) and in directions of prescribed incidence
+// |d . n| from 1 down to just above the scene's bound, with the origin's group skipped when the
+// incidence clears the bound: the same closest hit (t, primitive) / the same any-hit answer as brute
+// force.  Below the bound the kernels do not skip; those rays are checked unskipped.  Returns mismatches.
+static long check_plane_skip(const HostScene& hs, int nrays, long& skipped, long& total) {
+    long bad = 0;
+    const int np = (int)hs.xprims.size();
+    if (np == 0) return 0;
+    for (int r = 0; r < nrays; ++r) {
+        const int i = (int)(urand() * np) % np;
+        const XPrim& x = hs.xprims[i];
+        if (x.kind != 0 || x.pad[0] == 255) continue;
+        const V3 o = (r % 4 == 0) ? v3(-10, 0, 0) : v3(urand() * 12 - 1, urand() * 12 - 6, urand() * 12 - 6);
+        double a = urand(), b = urand();
+        if (a + b > 1) { a = 1 - a; b = 1 - b; }
+        const V3 tgt = ld3(x.a) + ld3(x.b) * a + ld3(x.c) * b;
+        const V3 d = normalize(tgt - o);
+        const double t = prim_t(hot_of(x, i), o, d, 1e-7);
+        if (!std::isfinite(t)) continue;
+        const V3 P = o + t * d;   // as x_segment computes the hit point
+        const V3 n = ld3(x.n);
+        const double cmin = hs.x_skip_a * std::max(std::fabs(o.x), std::max(std::fabs(o.y), std::fabs(o.z))) + hs.x_skip_b;
+        V3 d2;
+        double tmax = INFINITY;
+        const int kind = r % 5;
+        if (kind == 0) {   // shadow ray toward a random point
+            const V3 L = v3(urand() * 12 - 1, urand() * 12 - 6, urand() * 12 - 6);
+            tmax = std::sqrt(sq3(L - P));
+            d2 = normalize(L - P);
+        } else {           // incidence c: random tangent direction tilted to |d . n| = c, either side
+            const double c = kind == 1 ? urand() : kind == 2 ? cmin * (1.0 + 3.0 * urand()) : kind == 3 ? cmin * (1.0 + 1e-3 * urand()) : cmin * 0.5;
+            V3 tg = cross(n, v3(urand() - 0.5, urand() - 0.5, urand() - 0.5));
+            if (sq3(tg) == 0.0) continue;
+            tg = normalize(tg);
+            const double sg = urand() < 0.5 ? -1.0 : 1.0;
+            d2 = normalize(tg * std::sqrt(std::max(0.0, 1.0 - c * c)) + n * (sg * c));
+        }
+        const bool shadow = kind == 0;
+        const int skip = std::fabs(dot(d2, n)) >= cmin ? x.pad[0] : -1;
+        double t1, t2;
+        long v = 0;
+        const int p1 = traverse(hs, P, d2, shadow, tmax, t1, v, skip);
+        const int p2 = brute(hs, P, d2, shadow, tmax, t2);
+        ++total;
+        skipped += skip >= 0;
+        if (shadow ? ((p1 >= 0) != (p2 >= 0)) : (p1 != p2 || !(t1 == t2 || (std::isinf(t1) && std::isinf(t2))))) {
+            if (++bad < 5) std::printf("plane skip mismatch: prim %d kind %d skip %d got %d want %d (t %.17g %.17g)\n", i, kind, skip, p1, p2, t1, t2);
+        }
+    }
+    return bad;
+}
+
 int main(int argc, char** argv) {
     const int nrays = argc > 1 ? std::atoi(argv[1]) : 20000;
     long mism = 0, total = 0, visits = 0;
@@ -298,6 +355,17 @@ int main(int argc, char** argv) {
         std::vector<gi_entity_desc> ents;
         if (scene == 4 && !read_scn(argv[2], ents)) return 2;
         const int ntri = scene == 0 ? 40 : scene == 1 ? 3000 : scene == 2 ? 20000 : scene == 3 ? 300 : 0;
+        for (int i = 0; scene == 0 && i < 60; ++i) {   // tilted quads: two triangles in one plane each
+            const V3 c = v3(urand() * 10, urand() * 10 - 5, urand() * 10 - 5);
+            const V3 u = normalize(v3(urand() - 0.5, urand() - 0.5, urand() - 0.5));
+            const V3 w = normalize(cross(u, v3(urand() - 0.5, urand() - 0.5, urand() - 0.5)));
+            const double su = 0.3 + urand(), sw = 0.3 + urand();
+            const V3 q[4] = {c - u * su - w * sw, c + u * su - w * sw, c + u * su + w * sw, c - u * su + w * sw};
+            double v1[9] = {q[0].x, q[0].y, q[0].z, q[1].x, q[1].y, q[1].z, q[2].x, q[2].y, q[2].z};
+            double v2[9] = {q[0].x, q[0].y, q[0].z, q[2].x, q[2].y, q[2].z, q[3].x, q[3].y, q[3].z};
+            ents.push_back(tri(v1));
+            ents.push_back(tri(v2));
+        }
         for (int i = 0; i < ntri; ++i) {
             double c[3] = {urand() * 10, urand() * 10 - 5, urand() * 10 - 5}, v[9];
             const double sz = scene == 3 ? 6.0 : 0.6;   // scene 3: large overlapping triangles
@@ -348,6 +416,13 @@ int main(int argc, char** argv) {
         }
         }
         g_xc = nullptr;
+        {
+            long skipped = 0, tot = 0;
+            const long pb = check_plane_skip(hs, 4 * nrays, skipped, tot);
+            mism += pb;
+            std::printf("scene %d plane skip: %ld rays, %ld skipping, bound %.3g + %.3g |cam|, mismatches %ld\n", scene, tot, skipped,
+                        hs.x_skip_b, hs.x_skip_a, pb);
+        }
         std::printf("scene %d: %zu prims, %zu wide nodes, %zu leaf records, depth %d; per ray: %.2f node visits, %.2f prim tests"
                     " (SAH estimate %.2f / %.2f)\n",
                     scene, hs.xprims.size(), hs.xwnodes.size(), hs.xhot.size(), hs.x_max_depth,
