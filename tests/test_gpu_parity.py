@@ -1081,6 +1081,49 @@ def test_mode_r_reach_lane_groups_bit_exact(torch_cuda, tmp_path, group):
     assert U.bits_equal(rs, ref["strip"]).all(), "strip"
 
 
+def _grazing_scene(light_mode: str):
+    """The Cornell box plus two tilted quads (coplanar pairs on oblique planes), with the light put
+    almost into a surface's plane: "floor" 1e-9 above the floor (z = -5), "tilted" 1e-9 off the first
+    tilted quad's plane.  Shadow rays from that surface then leave it at an incidence ~1e-10, far
+    below the own-plane skip's bound, and must be traced unskipped."""
+    s = S.cornell_scene()
+    s.name = "grazing_" + light_mode
+    rng = np.random.default_rng(11)
+    centres = [np.array([4.0, 1.5, 0.5]), np.array([3.0, -2.0, 2.5])]
+    planes = []
+    for c in centres:
+        u = rng.normal(size=3); u /= np.linalg.norm(u)
+        v = np.cross(u, rng.normal(size=3)); v /= np.linalg.norm(v)
+        q = [c - u - v, c + u - v, c + u + v, c - u + v]
+        s.imp_triangle(tuple(q[0]), tuple(q[1]), tuple(q[2]), (1, 1, 1))
+        s.imp_triangle(tuple(q[0]), tuple(q[2]), tuple(q[3]), (1, 1, 1))
+        planes.append((c, np.cross(u, v)))
+    if light_mode == "floor":
+        s.light = (5.0, 0.5, -5.0 + 1e-9)
+    else:
+        c, n = planes[0]
+        w = np.cross(n, [0.0, 0.0, 1.0]); w /= np.linalg.norm(w)
+        s.light = tuple(c + 1.7 * w + 1e-9 * n)
+    return s
+
+
+@pytest.mark.parametrize("light_mode", ["floor", "tilted"])
+def test_mode_x_own_plane_skip_grazing_light(torch_cuda, light_mode):
+    """The own-plane leaf skip (gi_build.cpp assign_plane_groups) with the light almost in a
+    surface's plane: the shadow rays leaving that surface graze it, fall below the skip's incidence
+    bound and are traced in full; every other ray may skip its own plane.  Mode X frames (k_seg, the
+    default form for this LDS-resident scene) bit for bit equal the oracle's, which never skips."""
+    sc = _grazing_scene(light_mode)
+    d = gi.DeviceScene.from_scene(sc)
+    assert d.x_form(spp=4, depth=6) == "k_seg"
+    w, h, spp, depth = 96, 64, 4, 6
+    rgb, _ = d.render(cam_of(sc), sc.light, w, h, mode=gi.MODE_X, spp=spp, depth=depth, seed=3)
+    o = U.oracle_render(sc.to_scn(), w, h, mode=1, spp=spp, depth=depth, seed=3)
+    same = U.bits_equal(rgb.reshape(-1, 3), o["rgb"]).all(1)
+    assert same.all(), f"{int((~same).sum())} of {same.size} pixels differ"
+    assert (o["rgb"] > 0).any()
+
+
 @pytest.mark.parametrize("accel", [{"GI_XACCEL": "octree"}, {"GI_XLEAF_MAX": "1"}, {"GI_XSBVH": "1"}])
 def test_mode_x_other_acceleration_structures_bit_exact(torch_cuda, accel):
     """Mode X over the SAT octree (GI_XACCEL=octree: up to 12 levels, so the kernel keeps its two-word
