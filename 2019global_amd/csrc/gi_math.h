@@ -87,12 +87,11 @@ GI_HD void make_tri(V3 p1, V3 p2, V3 p3, TriRec& t) {
     t.e2f[0] = (float)e2.x; t.e2f[1] = (float)e2.y; t.e2f[2] = (float)e2.z;
 }
 
-// ImpTriangle::intersect (entities.h:150-249).  fp32 solve: glm::mat3(e1, e2, -dir) transposed,
-// glm's cofactor inverse (func_matrix.inl:272-294) and vec3 * mat3 (type_mat3x3.inl:437-443);
-// only sol.z is used.  No t > 0 test (A.3).
-GI_HD bool tri_hit(V3 p1, V3 p2, V3 p3, V3 n, V3 pos, const float* e1f, const float* e2f, V3 o, V3 d,
-                   V3& P, V3& N) {
-    if (dot(n, d) == 0) return false;
+// ImpTriangle::intersect (entities.h:150-249) after its parallel test: the fp32 solve --
+// glm::mat3(e1, e2, -dir) transposed, glm's cofactor inverse (func_matrix.inl:272-294) and
+// vec3 * mat3 (type_mat3x3.inl:437-443); only sol.z is used -- then the acceptance test on the
+// three sub-triangle normals at the computed point.  No t > 0 test (A.3).
+GI_HD bool tri_accept(V3 p1, V3 p2, V3 p3, V3 pos, const float* e1f, const float* e2f, V3 o, V3 d, V3& P) {
     const float m00 = e1f[0], m01 = e2f[0], m02 = (float)(-d.x);
     const float m10 = e1f[1], m11 = e2f[1], m12 = (float)(-d.y);
     const float m20 = e1f[2], m21 = e2f[2], m22 = (float)(-d.z);
@@ -123,6 +122,13 @@ GI_HD bool tri_hit(V3 p1, V3 p2, V3 p3, V3 n, V3 pos, const float* e1f, const fl
     const bool inside = sq3(d1 - d2) < 1.0e-3 && sq3(d2 - d3) < 1.0e-3;   // :232-237
     if (!(short_d || inside)) return false;
     P = point;
+    return true;
+}
+// ImpTriangle::intersect (entities.h:150-249) with the triangle's derived members n, pos, e1f, e2f
+GI_HD bool tri_hit(V3 p1, V3 p2, V3 p3, V3 n, V3 pos, const float* e1f, const float* e2f, V3 o, V3 d,
+                   V3& P, V3& N) {
+    if (dot(n, d) == 0) return false;
+    if (!tri_accept(p1, p2, p3, pos, e1f, e2f, o, d, P)) return false;
     N = dot(d, n) < 0 ? n : -n;
     return true;
 }
@@ -147,16 +153,26 @@ GI_HD bool tri_hit(const TriRec& t, V3 o, V3 d, V3& P, V3& N) {
     return tri_hit(ld3(t.p1), ld3(t.p2), ld3(t.p3), ld3(t.n), ld3(t.pos), t.e1f, t.e2f, o, d, P, N);
 }
 
-// A triangle built on the fly from three corners (ExpBox faces, entities.h:319-324).
+// A triangle built on the fly from three corners (ExpBox faces, entities.h:319-324), its normal
+// used only by the parallel test dot(normalize(c), d) == 0, c = cross(e1, e2).  normalize scales the
+// components of c by one rounded factor s: the computed dot is s sum(c_i d_i (1 + e_i)) plus its own
+// rounding, |e_i| <= u, the rounding <= 3u (1 + u) s sum |c_i d_i|; so whenever |sum c_i d_i| exceeds
+// ~4.5u sum |c_i d_i| it is nonzero.  dot(c, d) computed (rounding <= 3u sum |c_i d_i|) above 1e-12 of
+// sum |c_i d_i| proves that, with c and d in the normal range, and the square root and division of
+// the normalisation are skipped; otherwise the test runs as the reference writes it.
 GI_HD bool tri_hit_corners(V3 p1, V3 p2, V3 p3, V3 o, V3 d) {
     if (!tri_may_hit(p1, p2, p3, o, d)) return false;
     const V3 e1 = p2 - p1, e2 = p3 - p1;
-    const V3 n = normalize(cross(e1, e2));
+    const V3 c = cross(e1, e2);
+    const double cd = dot(c, d);
+    const double ca = fabs(c.x * d.x) + fabs(c.y * d.y) + fabs(c.z * d.z);
+    const bool clear = (fabs(cd) > 1e-12 * ca) & (ca > 1e-200) & (ca < 1e200);
+    if (!clear && dot(normalize(c), d) == 0) return false;
     const V3 pos = 0.5 * (0.5 * (p1 + p2) + p3);
     const float e1f[3] = {(float)e1.x, (float)e1.y, (float)e1.z};
     const float e2f[3] = {(float)e2.x, (float)e2.y, (float)e2.z};
-    V3 P, N;
-    return tri_hit(p1, p2, p3, n, pos, e1f, e2f, o, d, P, N);
+    V3 P;
+    return tri_accept(p1, p2, p3, pos, e1f, e2f, o, d, P);
 }
 
 // ExpBox(min,max).intersect (entities.h:379-440) as Octree::Node::intersect uses it: true iff any

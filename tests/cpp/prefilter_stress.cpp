@@ -65,9 +65,19 @@ int main(int argc, char** argv) {
         V3 d = normalize(tgt - o);
         bool r = raw(p1, p2, p3, o, d), f = tri_hit_corners(p1, p2, p3, o, d), u = full(p1, p2, p3, o, d);
         // spurious ExpBox faces (A.4): the third corner reflected through the origin
-        bool rs = raw(p1, p2, -p3, o, d), us = full(p1, p2, -p3, o, d);
+        bool rs = raw(p1, p2, -p3, o, d), us = full(p1, p2, -p3, o, d), fs = tri_hit_corners(p1, p2, -p3, o, d);
+        // nearly parallel rays: tri_hit_corners' parallel test skips the normalisation only when
+        // dot(cross(e1, e2), d) is clearly nonzero; here it is 0 or within a few ulps of 0
+        const V3 nrm = cross(p2 - p1, p3 - p1);
+        V3 dp = d - nrm * (dot(d, nrm) / dot(nrm, nrm));
+        if (it % 5 == 0) dp = dp + nrm * (1e-17 * U(g) / std::sqrt(dot(nrm, nrm)));
+        if (dot(dp, dp) > 0) {
+            dp = normalize(dp);
+            const bool rp = raw(p1, p2, p3, o, dp), fp = tri_hit_corners(p1, p2, p3, o, dp);
+            if (rp != fp) { ++bad; if (bad < 5) printf("parallel mismatch it=%ld raw=%d corners=%d\n", it, rp, fp); }
+        }
         ++n; hits += r;
-        if (r != f || r != u || rs != us) { ++bad; if (bad < 5) printf("mismatch it=%ld mode=%d raw=%d full=%d\n", it, mode, r, u); }
+        if (r != f || r != u || rs != us || rs != fs) { ++bad; if (bad < 5) printf("mismatch it=%ld mode=%d raw=%d full=%d\n", it, mode, r, u); }
         if (mode == 2) near += r;
     }
     // box_hit_part: the OR of its four parts (3 faces each, for four cooperating lanes) is box_hit
