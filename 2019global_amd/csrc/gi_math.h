@@ -110,7 +110,26 @@ GI_HD bool tri_accept(V3 p1, V3 p2, V3 p3, V3 pos, const float* e1f, const float
     // (rounding errors ~1e-16 |c_i||c_j|) puts the pair ~90 degrees or more apart: the test below would
     // reject too.  NaN / inf components fail the length guard or the comparison and take the full test.
     const double n1 = dot(c1, c1), n2 = dot(c2, c2), n3 = dot(c3, c3);
-    if ((n1 > 1e-200) & (n2 > 1e-200) & (n3 > 1e-200) & ((dot(c1, c2) <= 0.0) | (dot(c2, c3) <= 0.0))) return false;
+    const double x12 = dot(c1, c2), x23 = dot(c2, c3);
+    if ((n1 > 1e-200) & (n2 > 1e-200) & (n3 > 1e-200) & ((x12 <= 0.0) | (x23 <= 0.0))) return false;
+    // Both comparisons decided without the normalisations where the answer is clear.  With the
+    // c_k's squared lengths in [1e-150, 1e150] the d_k are unit vectors to ~5u, so the computed
+    // |d_j - d_k|^2 is 2 - 2 cos(c_j, c_k) to ~50u; cos^2 from the unnormalised dot products (relative
+    // rounding ~1e-15) set against the threshold moved by 1e-9 either way: a pair clearly below 1e-3
+    // is below it in the reference's arithmetic too, a pair clearly above it is above (and no d_k is
+    // short), so the answer is the reference's; within the 1e-9 band the test runs as written.
+    if ((n1 > 1e-150) & (n2 > 1e-150) & (n3 > 1e-150) & (n1 < 1e150) & (n2 < 1e150) & (n3 < 1e150)) {
+        constexpr double kIn = (1.0 - (1.0e-3 - 1e-9) / 2.0) * (1.0 - (1.0e-3 - 1e-9) / 2.0);
+        constexpr double kOut = (1.0 - (1.0e-3 + 1e-9) / 2.0) * (1.0 - (1.0e-3 + 1e-9) / 2.0);
+        const double p12 = n1 * n2, p23 = n2 * n3;
+        const bool in = (x12 > 0.0) & (x23 > 0.0) & (x12 * x12 > kIn * p12) & (x23 * x23 > kIn * p23);
+        const bool out = (x12 <= 0.0) | (x23 <= 0.0) | (x12 * x12 < kOut * p12) | (x23 * x23 < kOut * p23);
+        if (in) {
+            P = point;
+            return true;
+        }
+        if (out) return false;
+    }
     const V3 d1 = normalize(c1);
     const V3 d2 = normalize(c2);
     const V3 d3 = normalize(c3);

@@ -60,7 +60,8 @@ int main(int argc, char** argv) {
         double a = (U(g) + 1) / 2, b = (U(g) + 1) / 2 * (1 - a);
         if (mode == 0) tgt = p1 + (p2 - p1) * a + (p3 - p1) * b;            // inside
         else if (mode == 1) tgt = p1 + (p2 - p1) * a;                         // on an edge
-        else if (mode == 2) tgt = p1 + (p2 - p1) * a + v3(U(g), U(g), U(g)) * (sc * 1e-3);   // near an edge
+        else if (mode == 2) tgt = (it % 8 == 2) ? p1 + (p2 - p1) * a + (p3 - p1) * b + cross(p2 - p1, p3 - p1) * (0.02 * U(g) * (a + b) * (1 - a - b) / sc)   // just off the plane: the acceptance angle's edge
+                                                : p1 + (p2 - p1) * a + v3(U(g), U(g), U(g)) * (sc * 1e-3);   // near an edge
         else tgt = v3(U(g), U(g), U(g)) * (sc * 2);                           // anywhere
         V3 d = normalize(tgt - o);
         bool r = raw(p1, p2, p3, o, d), f = tri_hit_corners(p1, p2, p3, o, d), u = full(p1, p2, p3, o, d);
