@@ -19,7 +19,8 @@
 //     behind the same run(w, h); default GI_MODE_R, 1 spp, depth 1 (raytracer.h:41-84).
 //   * progressive samples (Mode X): setIntegrator(GI_MODE_X, spp, depth, seed, pass) or GI_PASS=n
 //     renders the frame's spp in passes of n samples; after each pass the whole frame's running
-//     estimate -- exactly the frame of that many samples -- goes through Image::setPixel, so a 64-spp
+//     estimate -- exactly the frame of that many samples (for a pass ending at sample 1 the jittered
+//     first sample, not the unjittered spp = 1 frame) -- goes through Image::setPixel, so a 64-spp
 //     frame shows a first image after the first pass instead of nothing until it is done (the
 //     viewer restarts on every resize, viewer.h:41-52), and stop() is honoured between passes (the
 //     image keeps the last delivered pass).  The last pass's frame is the one-shot frame bit for
